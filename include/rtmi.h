@@ -1,0 +1,261 @@
+/*
+ * rtmi.h — C-ABI of the MI355X-native (gfx950) trace/shade backend for
+ * johnnovak/nim-raytracer.
+ *
+ * The reference has no FFI: its hot path is the Nim proc
+ *     proc renderLine*(scene: Scene, opts: Options, fb: var Framebuf,
+ *                      y: Natural, step: Natural = 1, maxStep: Natural = 1): Stats
+ * (src/renderer/renderer.nim:162-211) plus proc initRenderer*()
+ * (src/renderer/renderer.nim:214-215), called per scanline from worker
+ * threads (src/raytracer.nim:25-32, src/concurrency/workerpool.nim:99).
+ * This header is what a Nim `{.importc, dynlib: "librtmi.so".}` module binds
+ * in its place. Plain C types only: pointers, sizes,
+ * fixed-width integers and doubles. No torch/HIP types in any signature;
+ * device streams are passed as opaque `void*` (a hipStream_t, NULL = the
+ * scene's own stream).
+ *
+ * Conventions
+ *  - Every entry point returns int: RT_OK (0) or a negative RT_E_* code.
+ *    The message of the last failure on the calling thread is available via
+ *    rt_last_error(). No entry point aborts the caller's process.
+ *  - Matrices are 4x4 column-major doubles exactly as glm stores Mat4x4
+ *    (m[col*4 + row]); a point transforms as m * (x, y, z, 1).
+ *  - The framebuffer is the reference's Framebuf layout
+ *    (src/utils/framebuf.nim:7-28): w*h*3 float32, interleaved RGB,
+ *    row-major, y = 0 is the top row. Caller-owned; the library never
+ *    retains caller pointers after a call returns.
+ */
+#ifndef RTMI_H
+#define RTMI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RTMI_ABI_VERSION 1
+
+/* ---- error codes ------------------------------------------------------ */
+enum {
+  RT_OK = 0,
+  RT_E_INVALID = -1,     /* bad argument (null pointer, size, index range) */
+  RT_E_UNSUPPORTED = -2, /* valid request this build does not implement    */
+  RT_E_DEVICE = -3,      /* HIP runtime / kernel failure, no usable GPU    */
+  RT_E_NOMEM = -4,       /* host or device allocation failed               */
+  RT_E_IO = -5           /* file could not be read / parsed                */
+};
+
+/* ---- scene description (flattened once from the Nim object graph) ----- */
+
+/* Geometry kinds: Sphere / Plane / Box / TriangleMesh (src/renderer/geom.nim:137-155). */
+enum rt_geom_type { RT_SPHERE = 0, RT_PLANE = 1, RT_BOX = 2, RT_MESH = 3 };
+
+/* Light kinds: DistantLight / PointLight (src/renderer/light.nim:9-17). */
+enum rt_light_type { RT_DISTANT_LIGHT = 0, RT_POINT_LIGHT = 1 };
+
+/* AntialiasKind (src/renderer/renderer.nim:11-12). */
+enum rt_aa_kind {
+  RT_AA_NONE = 0,
+  RT_AA_GRID = 1,
+  RT_AA_JITTERED = 2,
+  RT_AA_MULTI_JITTERED = 3,
+  RT_AA_CORRELATED_MULTI_JITTERED = 4
+};
+
+/* Arithmetic precision of the device path. RT_FP64 repeats the reference's
+ * float64 arithmetic operation for operation (parity mode); RT_FP32 is the
+ * performance mode (parity within the tolerance stated in DESIGN.md). */
+enum rt_precision { RT_FP32 = 0, RT_FP64 = 1 };
+
+/* TriangleMesh data (src/renderer/geom.nim:151-155, src/loaders/obj.nim:87-126).
+ * Face i uses vertices faces[3i..3i+2]; its normal is normals[3i..3i+2]
+ * (one normal per face, obj.nim:65-84). normals == NULL means "compute as
+ * obj.nim calcNormals does": normalize(cross(v1 - v0, v2 - v0)). */
+typedef struct rt_mesh_desc {
+  const double *vertices;  /* num_vertices * 3 (x, y, z), object space */
+  int64_t num_vertices;
+  const int32_t *faces;    /* num_faces * 3 zero-based vertex indices   */
+  int64_t num_faces;
+  const double *normals;   /* num_faces * 3, or NULL                    */
+} rt_mesh_desc;
+
+/* Object{geometry, material} (src/renderer/scene.nim:6-9,
+ * src/renderer/material.nim:4-7). world_to_object is the caller's
+ * objectToWorld.inverse (geom.nim:159-198), passed through unchanged so that
+ * host and device use identical matrices. */
+typedef struct rt_object_desc {
+  int32_t type;                /* rt_geom_type                           */
+  int32_t mesh;                /* RT_MESH: index into rt_scene_desc.meshes */
+  double object_to_world[16];
+  double world_to_object[16];
+  double radius;               /* RT_SPHERE: Sphere.r                    */
+  double box_min[3];           /* RT_BOX: aabb.vmin (object space)       */
+  double box_max[3];           /* RT_BOX: aabb.vmax                      */
+  double albedo[3];            /* Material.albedo                        */
+  double reflection;           /* Material.reflection                    */
+} rt_object_desc;
+
+typedef struct rt_light_desc {
+  int32_t type;                /* rt_light_type                          */
+  int32_t reserved;
+  double color[3];
+  double intensity;
+  double dir[3];               /* DistantLight.dir (travel direction)    */
+  double pos[3];               /* PointLight.pos                         */
+} rt_light_desc;
+
+/* Scene (src/renderer/scene.nim:11-18). */
+typedef struct rt_scene_desc {
+  const rt_object_desc *objects;
+  int32_t num_objects;
+  int32_t num_lights;
+  const rt_light_desc *lights;
+  const rt_mesh_desc *meshes;
+  int32_t num_meshes;
+  int32_t reserved;
+  double fov;                  /* degrees, Scene.fov                     */
+  double camera_to_world[16];  /* Scene.cameraToWorld                    */
+  double bg_color[3];          /* Scene.bgColor                          */
+} rt_scene_desc;
+
+/* Options (src/renderer/renderer.nim:24-28) plus the device-path knobs. */
+typedef struct rt_options {
+  int32_t width, height;       /* Options.width/height                   */
+  int32_t aa_kind;             /* Options.antialias.kind (rt_aa_kind)    */
+  int32_t grid_size;           /* Options.antialias.gridSize (m)         */
+  double bias;                 /* Options.bias                           */
+  int32_t max_ray_depth;       /* Options.maxRayDepth                    */
+  int32_t precision;           /* rt_precision                           */
+  uint64_t seed;               /* stochastic samplers (not yet supported) */
+  uint32_t flags;              /* RT_FLAG_*                              */
+  uint32_t reserved;
+} rt_options;
+
+/* Shadow rays may stop at the first occluder (any-hit). The image is
+ * identical; num_intersection_hits can then differ from the reference's
+ * closest-hit count on scenes where several objects overlap one shadow ray. */
+#define RT_FLAG_ANYHIT_SHADOWS 0x1u
+
+/* Stats (src/renderer/stats.nim:4-13) plus ray counts for Mray/s. */
+typedef struct rt_stats {
+  uint64_t num_primary_rays;        /* renderer.nim:138,155             */
+  uint64_t num_intersection_tests;  /* renderer.nim:58                  */
+  uint64_t num_intersection_hits;   /* renderer.nim:65                  */
+  uint64_t num_shadow_rays;         /* one per light per shaded hit     */
+  uint64_t num_reflection_rays;     /* renderer.nim:114-118             */
+} rt_stats;
+
+/* Device-side work counters of the last render (algorithmic traffic). */
+typedef struct rt_traversal_counters {
+  uint64_t wave_node_fetches;  /* BVH node records fetched (per wave)     */
+  uint64_t wave_tri_fetches;   /* triangle records fetched (per wave)     */
+  uint64_t lane_node_visits;   /* sum over rays of node records visited   */
+  uint64_t lane_tri_tests;     /* sum over rays of triangle tests         */
+} rt_traversal_counters;
+
+typedef struct rt_scene_info {
+  int64_t num_objects, num_lights, num_meshes;
+  int64_t num_triangles;       /* all meshes                             */
+  int64_t num_bvh_nodes;       /* all meshes                             */
+  int32_t max_bvh_depth;
+  int32_t device;
+  int64_t device_bytes;        /* resident scene bytes in HBM            */
+  double build_ms;             /* host BVH build + upload wall time      */
+} rt_scene_info;
+
+typedef struct rt_scene rt_scene; /* opaque, owns device buffers */
+
+/* ---- library ----------------------------------------------------------- */
+
+/* ABI version of the loaded library (RTMI_ABI_VERSION). */
+int rt_version(void);
+
+/* Message of the last failed call on this thread ("" if none). */
+const char *rt_last_error(void);
+
+/* initRenderer* (renderer.nim:214-215) equivalent: bind the calling thread
+ * to HIP device `device` and check it is a gfx950 GPU. Safe to call again. */
+int rt_init(int device);
+
+/* Number of visible GPUs (0 when none; never fails). */
+int rt_device_count(void);
+
+/* ---- scene ------------------------------------------------------------- */
+
+/* Flatten, build the per-mesh BVH and upload everything to the current
+ * device. desc and all arrays it points to may be freed after return. */
+int rt_scene_create(const rt_scene_desc *desc, rt_scene **out_scene);
+int rt_scene_destroy(rt_scene *scene);
+int rt_scene_get_info(const rt_scene *scene, rt_scene_info *out);
+
+/* ---- rendering ----------------------------------------------------------
+ * All render calls implement renderLine (renderer.nim:162-211) for every row
+ * y in countup(y0, y1 - 1, step):
+ *   for x in countup(0, width - 1, step):
+ *     if step < maxStep and (x and (2*step-1)) == 0 and (y and (2*step-1)) == 0:
+ *       continue                      # already rendered at a coarser level
+ *     color = calcPixel(...)          # akNone: 1 sample at (x, y); akGrid: m*m
+ *     fill fb[x..x+step-1, y..y+step-1] (clipped) with color
+ * step and max_step must be powers of two with max_step >= step.
+ * `out` receives the summed Stats of the call (may be NULL for the _device
+ * forms, which then do not synchronise the stream).
+ */
+
+/* Host framebuffer form: fb_rgb is caller memory of fb_w*fb_h*3 floats with
+ * fb_w == opts->width and fb_h == opts->height. Thread-safe: concurrent
+ * callers on disjoint rows are serialised internally (renderLine is called
+ * concurrently by the reference's pool, workerpool.nim:172-223). */
+int rt_render_lines(rt_scene *scene, const rt_options *opts, float *fb_rgb,
+                    int32_t fb_w, int32_t fb_h, int32_t y0, int32_t y1,
+                    int32_t step, int32_t max_step, rt_stats *out);
+
+/* Device framebuffer form (the fast path: whole frame, nothing crosses
+ * PCIe). d_fb is a device pointer to width*height*3 floats. */
+int rt_render_lines_device(rt_scene *scene, const rt_options *opts,
+                           float *d_fb, int32_t y0, int32_t y1, int32_t step,
+                           int32_t max_step, void *hip_stream, rt_stats *out);
+
+/* Multi-GPU shard: image rows are cut into bands of band_h rows; band b is
+ * owned by rank b % world. Renders this rank's bands (step 1) into the
+ * compact device buffer d_bands laid out as
+ *   [ceil(ceil(height/band_h)/world) * band_h rows][width][3] float32,
+ * i.e. local band k occupies rows [k*band_h, (k+1)*band_h). Rows past the
+ * image bottom are left untouched. */
+int rt_render_bands_device(rt_scene *scene, const rt_options *opts,
+                           float *d_bands, int32_t band_h, int32_t rank,
+                           int32_t world, void *hip_stream, rt_stats *out);
+
+/* Rank-0 epilogue of the framebuffer gather: d_gathered holds `world`
+ * compact band buffers back to back (an all-gather of rt_render_bands_device
+ * outputs); writes the interleaved image to d_fb (width*height*3). */
+int rt_unshard_bands_device(const float *d_gathered, float *d_fb,
+                            int32_t width, int32_t height, int32_t band_h,
+                            int32_t world, void *hip_stream);
+
+/* Rows per rank-local compact band buffer (helper for sizing d_bands). */
+int rt_band_rows(int32_t height, int32_t band_h, int32_t world,
+                 int32_t *out_rows);
+
+/* Traversal counters of the last render call on this scene (synchronises
+ * the scene's stream). */
+int rt_scene_last_counters(rt_scene *scene, rt_traversal_counters *out);
+
+/* ---- helpers ----------------------------------------------------------- */
+
+/* glm-style inverse of a column-major 4x4 (what geom.nim's
+ * objectToWorld.inverse computes); RT_E_INVALID if singular. */
+int rt_mat4_inverse(const double m[16], double out[16]);
+
+/* .geom triangle soup (format of test/test.nim:14-26 and the writer
+ * src/loaders/objconv.nim:139-153): int32 N, then N*3 vertices of 3 float32.
+ * Query form: pass vertices == NULL to get *num_triangles only; then pass a
+ * buffer of num_triangles*9 doubles. */
+int rt_load_geom(const char *path, int64_t *num_triangles, double *vertices);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RTMI_H */

@@ -1,0 +1,139 @@
+// rt_common.h — device-resident scene layout shared by the host library
+// (rtmi.cpp) and the gfx950 kernels (rt_device.h).
+//
+// HBM layout (all arrays resident for the scene's lifetime, built once by
+// rt_scene_create):
+//   objects  DevObject<R>[nobj]   scene order (trace order, renderer.nim:53)
+//   lights   DevLight<R>[nlight]
+//   meshes   DevMesh<R>[nmesh]
+//   nodes    BvhNode[...]         64-B BVH2 nodes, both child boxes per node,
+//                                 depth-first order, all meshes concatenated
+//   tris     TriRec<R>[...]       leaf-ordered triangles (v0, e1, e2, face id)
+//   normals  R[3 * faces]         one face normal per ORIGINAL face index
+//                                 (obj.nim calcNormals), looked up by face id
+#pragma once
+#include <stdint.h>
+
+namespace rtmi {
+
+enum : int32_t { GEOM_SPHERE = 0, GEOM_PLANE = 1, GEOM_BOX = 2, GEOM_MESH = 3 };
+enum : int32_t { LIGHT_DISTANT = 0, LIGHT_POINT = 1 };
+
+constexpr int kMaxBvhDepth = 60;      // stack fits one 64-lane VGPR
+constexpr int kMaxShadeLevels = 8;    // primary + 7 reflection bounces
+constexpr int kStatSlots = 10;        // per-wave partial counters
+
+// Geometry + material record. Matrices column-major like glm.
+template <class R>
+struct alignas(16) DevObject {
+  R w2o[16];
+  R o2w[16];
+  R prm[8];      // sphere: prm[0] = r; box: prm[0..2] = vmin, prm[4..6] = vmax
+  R albedo[4];   // rgb, reflection
+  int32_t type;
+  int32_t mesh;
+  int32_t pad0, pad1;
+};
+
+template <class R>
+struct alignas(16) DevLight {
+  R ci[4];       // color * intensity (rgb)  (light.nim:50,57)
+  R v[4];        // distant: dir; point: pos
+  int32_t type;
+  int32_t pad[3];
+};
+
+template <class R>
+struct alignas(16) DevMesh {
+  R lo[4];       // calcAABB (geom.nim:175-188), for the reference's mesh gate
+  R hi[4];
+  int32_t root;        // index into nodes, -1 for an empty mesh
+  int32_t num_faces;
+  int32_t normal_base; // offset (in faces) into normals
+  int32_t pad;
+};
+
+// BVH2 node: both children's boxes in one 64-byte record (one scalar fetch
+// tests two boxes). child n == 0: internal node index c (or c < 0: empty);
+// n > 0: leaf with triangles [c, c + n) of the tris array.
+struct alignas(16) BvhNode {
+  float lo0[3], hi0[3];
+  float lo1[3], hi1[3];
+  int32_t c0, c1, n0, n1;
+};
+static_assert(sizeof(BvhNode) == 64, "BvhNode must be 64 bytes");
+
+struct alignas(16) TriF32 {
+  float v0[3];
+  int32_t id;    // original face index (tie-break + normal lookup)
+  float e1[3];
+  float pad1;
+  float e2[3];
+  float pad2;
+};
+static_assert(sizeof(TriF32) == 48, "TriF32 must be 48 bytes");
+
+struct alignas(16) TriF64 {
+  double v0[3];
+  double e1[3];
+  double e2[3];
+  int32_t id;
+  int32_t pad;
+};
+static_assert(sizeof(TriF64) == 80, "TriF64 must be 80 bytes");
+
+template <class R> struct TriOf;
+template <> struct TriOf<float> { using type = TriF32; };
+template <> struct TriOf<double> { using type = TriF64; };
+
+// Kernel arguments (passed by value).
+template <class R>
+struct RenderParams {
+  const DevObject<R>* objects;
+  const DevLight<R>* lights;
+  const DevMesh<R>* meshes;
+  const BvhNode* nodes;
+  const typename TriOf<R>::type* tris;
+  const R* normals;
+  float* fb;                       // output rows (see mode)
+  unsigned long long* partials;    // [num_waves][kStatSlots]
+  R c2w[16];
+  R bg[4];
+  R f;                             // tan(degToRad(fov) / 2)
+  R aspect;                        // w / h
+  R bias;
+  R inv_len;                       // 1 / samples.len (renderer.nim:159)
+  R sample_step;                   // grid: xs = ys = 1/m
+  R sample_off;                    // grid: xoffs = yoffs = xs * 0.5
+  int32_t nobj, nlight;
+  int32_t width, height;
+  int32_t aa_kind, grid_m, spp;
+  int32_t max_depth;
+  int32_t flags;
+  int32_t max_iters;               // traversal bound: each node entered at most once
+  // work mapping: rows k in [0, nrows), columns j in [0, ncols), x = j*step.
+  int32_t mode;                    // 0: y = y0 + k*step into full image; 1: bands
+  int32_t y0, nrows, ncols, step, max_step;
+  int32_t band_h, rank, world;
+  int32_t lanes_per_px;            // L: lanes sharing one pixel's samples
+  int32_t tile_x, tile_y;          // pixels per wave = tile_x * tile_y = 64 / L
+  int32_t tiles_x;
+  long long ngroups;               // tiles_x * tiles_y
+};
+
+enum : int32_t {
+  STAT_PRIMARY = 0, STAT_TESTS = 1, STAT_HITS = 2, STAT_SHADOW = 3, STAT_REFL = 4,
+  STAT_NODE_FETCH = 5, STAT_TRI_FETCH = 6, STAT_LANE_NODES = 7, STAT_LANE_TRIS = 8
+};
+
+}  // namespace rtmi
+
+// Launchers implemented by the precision-specific translation units.
+extern "C" {
+int rtmi_launch_render_f32(const rtmi::RenderParams<float>* p, int blocks, void* stream);
+int rtmi_launch_render_f64(const rtmi::RenderParams<double>* p, int blocks, void* stream);
+int rtmi_launch_reduce_stats(const unsigned long long* partials, int num_waves,
+                             unsigned long long* acc, void* stream);
+int rtmi_launch_unshard(const float* gathered, float* fb, int width, int height, int band_h,
+                        int world, void* stream);
+}

@@ -1,0 +1,615 @@
+// rt_device.h — gfx950 (CDNA4) trace/shade kernels, templated on the
+// arithmetic type R (float = performance mode, double = parity mode).
+//
+// Design (DESIGN.md "Kernels"):
+//  * One wave = one tile of pixels x samples. With >= 64 samples per pixel
+//    (the benchmark configs) a wave is ONE pixel and its 64 lanes trace 64
+//    sub-pixel samples at a time, so the wave's rays are almost perfectly
+//    coherent.
+//  * Wave-coherent BVH traversal: the node index and the traversal stack are
+//    wave-uniform. Node (64 B, both child boxes) and triangle records are
+//    fetched with SCALAR loads (s_load through the constant address space),
+//    each lane tests the child boxes against its own ray, and __ballot decides
+//    which children the wave visits. The stack lives in one VGPR across the
+//    64 lanes (entry i in lane i: push = v_cndmask, pop = v_readlane), so
+//    there is no per-lane stack, no LDS traffic and no scratch.
+//  * Statistics are wave-uniform popcounts of ballots kept in SGPRs and
+//    written once per wave (no atomics in the hot loop).
+//  * R = double reproduces the oracle's (i.e. the reference's) float64
+//    operation order: compiled with -ffp-contract=off, literal glm vec4
+//    arithmetic including the w components, IEEE division and sqrt.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "rt_common.h"
+
+#define RT_CONST __attribute__((address_space(4)))
+
+namespace rtmi {
+
+template <class T>
+__device__ __forceinline__ const RT_CONST T* cptr(const T* p) {
+  return (const RT_CONST T*)(p);
+}
+
+template <class R> struct Prec;
+template <> struct Prec<float> {
+  static constexpr bool exact = false;
+  __device__ static __forceinline__ float rcp(float x) { return __builtin_amdgcn_rcpf(x); }
+  __device__ static __forceinline__ float div(float a, float b) { return a * __builtin_amdgcn_rcpf(b); }
+  __device__ static __forceinline__ float sqrt(float x) { return __builtin_sqrtf(x); }
+  static constexpr float aabb_tmax_scale = 1.00000024f;  // geom.nim:90 (float form)
+  static constexpr float node_tmax_scale = 1.0000004f;   // conservative BVH culling
+};
+template <> struct Prec<double> {
+  static constexpr bool exact = true;
+  __device__ static __forceinline__ double rcp(double x) { return 1.0 / x; }
+  __device__ static __forceinline__ double div(double a, double b) { return a / b; }
+  __device__ static __forceinline__ double sqrt(double x) { return __builtin_sqrt(x); }
+  static constexpr double aabb_tmax_scale = 1.0000000000000004;  // geom.nim:91
+  static constexpr double node_tmax_scale = 1.000000000001;
+};
+
+template <class R> struct V3 { R x, y, z; };
+
+// Nim system.nim float min/max (NaN semantics kept).
+template <class R> __device__ __forceinline__ R nmin(R x, R y) { return x <= y ? x : y; }
+template <class R> __device__ __forceinline__ R nmax(R x, R y) { return y <= x ? x : y; }
+// mathutils.sign (mathutils.nim:12-18)
+template <class R> __device__ __forceinline__ R nsign(R x) { return x > R(0) ? R(1) : (x < R(0) ? R(-1) : R(0)); }
+
+template <class R> __device__ __forceinline__ R pinf() { return __builtin_huge_val(); }
+template <> __device__ __forceinline__ float pinf<float>() { return __builtin_huge_valf(); }
+
+// glm Mat4 * Vec4 (sum of columns scaled by v, accumulated from zero in
+// column order). w is 1 for points and 0 for directions; in exact mode the
+// w column is multiplied literally, as the reference does.
+template <class R, class M>
+__device__ __forceinline__ V3<R> xform(const M& m, V3<R> v, R w) {
+  V3<R> r;
+  if constexpr (Prec<R>::exact) {
+    r.x = R(0); r.y = R(0); r.z = R(0);
+    r.x = r.x + m[0] * v.x;  r.y = r.y + m[1] * v.x;  r.z = r.z + m[2] * v.x;
+    r.x = r.x + m[4] * v.y;  r.y = r.y + m[5] * v.y;  r.z = r.z + m[6] * v.y;
+    r.x = r.x + m[8] * v.z;  r.y = r.y + m[9] * v.z;  r.z = r.z + m[10] * v.z;
+    r.x = r.x + m[12] * w;   r.y = r.y + m[13] * w;   r.z = r.z + m[14] * w;
+  } else {
+    r.x = m[0] * v.x + m[4] * v.y + m[8] * v.z + m[12] * w;
+    r.y = m[1] * v.x + m[5] * v.y + m[9] * v.z + m[13] * w;
+    r.z = m[2] * v.x + m[6] * v.y + m[10] * v.z + m[14] * w;
+  }
+  return r;
+}
+
+// vec4 dot with explicit w terms (exact mode keeps the literal sum order).
+template <class R>
+__device__ __forceinline__ R dot4(V3<R> a, R aw, V3<R> b, R bw) {
+  if constexpr (Prec<R>::exact) {
+    R r = R(0);
+    r = r + a.x * b.x; r = r + a.y * b.y; r = r + a.z * b.z; r = r + aw * bw;
+    return r;
+  } else {
+    return a.x * b.x + a.y * b.y + a.z * b.z;
+  }
+}
+
+// normalize of a vec4 direction (w = 0): v / length(v).
+template <class R>
+__device__ __forceinline__ V3<R> normalize_dir(V3<R> v) {
+  const R len = Prec<R>::sqrt(dot4(v, R(0), v, R(0)));
+  if constexpr (Prec<R>::exact) {
+    return V3<R>{v.x / len, v.y / len, v.z / len};
+  } else {
+    const R il = R(1) / len;
+    return V3<R>{v.x * il, v.y * il, v.z * il};
+  }
+}
+
+// ---- wave helpers ----------------------------------------------------------
+__device__ __forceinline__ unsigned long long ballot(bool p) { return __ballot(p); }
+__device__ __forceinline__ unsigned long long popc(unsigned long long m) {
+  return (unsigned long long)__popcll(m);
+}
+
+struct WaveStats {
+  unsigned long long v[kStatSlots];
+};
+
+// ---- primitive intersections (object space) -------------------------------
+// Object-space ray as initRay builds it (geom.nim:41-48).
+template <class R>
+struct ORay {
+  V3<R> o, d, inv;
+};
+
+template <class R>
+__device__ __forceinline__ ORay<R> init_oray(V3<R> o, V3<R> d) {
+  ORay<R> r;
+  r.o = o;
+  r.d = d;
+  r.inv = V3<R>{Prec<R>::rcp(d.x), Prec<R>::rcp(d.y), Prec<R>::rcp(d.z)};
+  return r;
+}
+
+// AABB.intersect (geom.nim:76-96), returns tmin or -inf.
+template <class R>
+__device__ __forceinline__ R aabb_ref(V3<R> lo, V3<R> hi, const ORay<R>& r) {
+  const bool sx = r.inv.x < R(0), sy = r.inv.y < R(0), sz = r.inv.z < R(0);
+  const R txmin = ((sx ? hi.x : lo.x) - r.o.x) * r.inv.x;
+  const R txmax = ((sx ? lo.x : hi.x) - r.o.x) * r.inv.x;
+  const R tymin = ((sy ? hi.y : lo.y) - r.o.y) * r.inv.y;
+  const R tymax = ((sy ? lo.y : hi.y) - r.o.y) * r.inv.y;
+  const R tzmin = ((sz ? hi.z : lo.z) - r.o.z) * r.inv.z;
+  const R tzmax = ((sz ? lo.z : hi.z) - r.o.z) * r.inv.z;
+  const R tmin = nmax(tzmin, nmax(tymin, nmax(txmin, -pinf<R>())));
+  R tmax = nmin(tzmax, nmin(tymax, nmin(txmax, pinf<R>())));
+  tmax *= Prec<R>::aabb_tmax_scale;
+  return tmin <= tmax ? tmin : -pinf<R>();
+}
+
+// Sphere.intersect (geom.nim:215-237), incl. the `/ 2*a` precedence.
+template <class R>
+__device__ __forceinline__ R sphere_ref(R radius, const ORay<R>& r) {
+  const R a = r.d.x * r.d.x + r.d.y * r.d.y + r.d.z * r.d.z;
+  const R b = R(2) * (r.d.x * r.o.x + r.d.y * r.o.y + r.d.z * r.o.z);
+  const R c = r.o.x * r.o.x + r.o.y * r.o.y + r.o.z * r.o.z - radius * radius;
+  const R delta = b * b - R(4) * a * c;
+  if (delta >= R(0)) {
+    const R t1 = Prec<R>::div(-b - nsign(b) * Prec<R>::sqrt(delta), R(2)) * a;
+    const R t2 = Prec<R>::div(c, a * t1);
+    return nmin(t1, t2);
+  }
+  return -pinf<R>();
+}
+
+// Plane.intersect (geom.nim:240-248): y = 0, n = (0,1,0,0).
+template <class R>
+__device__ __forceinline__ R plane_ref(const ORay<R>& r) {
+  const V3<R> n{R(0), R(1), R(0)};
+  const R denom = dot4(n, R(0), r.d, R(0));
+  if (fabs(denom) > R(1e-6)) {
+    return Prec<R>::div(-dot4(r.o, R(1), n, R(0)), denom);
+  }
+  return -pinf<R>();
+}
+
+// rayTriangleIntersectFast (geom.nim:283-336) over a precomputed record
+// (e1 = v1 - v0, e2 = v2 - v0, bitwise what the reference computes). Returns
+// the hit t or NaN-free -inf. Single-sided (det < 1e-6 culled).
+template <class R, class T>
+__device__ __forceinline__ R tri_ref(const T& tri, V3<R> o, V3<R> d) {
+  const R v0v1x = tri.e1[0], v0v1y = tri.e1[1], v0v1z = tri.e1[2];
+  const R v0v2x = tri.e2[0], v0v2y = tri.e2[1], v0v2z = tri.e2[2];
+  const R pvecx = d.y * v0v2z - d.z * v0v2y;
+  const R pvecy = d.z * v0v2x - d.x * v0v2z;
+  const R pvecz = d.x * v0v2y - d.y * v0v2x;
+  const R det = v0v1x * pvecx + v0v1y * pvecy + v0v1z * pvecz;
+  const R inv_det = Prec<R>::rcp(det);
+  const R tvecx = o.x - R(tri.v0[0]), tvecy = o.y - R(tri.v0[1]), tvecz = o.z - R(tri.v0[2]);
+  const R u = (tvecx * pvecx + tvecy * pvecy + tvecz * pvecz) * inv_det;
+  const R qvecx = tvecy * v0v1z - tvecz * v0v1y;
+  const R qvecy = tvecz * v0v1x - tvecx * v0v1z;
+  const R qvecz = tvecx * v0v1y - tvecy * v0v1x;
+  const R v = (d.x * qvecx + d.y * qvecy + d.z * qvecz) * inv_det;
+  const R t = (v0v2x * qvecx + v0v2y * qvecy + v0v2z * qvecz) * inv_det;
+  // det < 1e-6 -> -inf; u < 0 or u > 1 -> -inf; v < 0 or u + v > 1 -> -inf.
+  // (The reference's early outs are order-independent predicates; a NaN
+  // anywhere makes the final `t >= 0` of the caller false, as in Nim.)
+  const bool ok = !(det < R(0.000001)) && !(u < R(0) || u > R(1)) && !(v < R(0) || u + v > R(1));
+  return ok ? t : -pinf<R>();
+}
+
+// ---- wave-coherent BVH traversal -------------------------------------------
+// Closest hit (or any hit) over one mesh for the lanes with `active`, within
+// [0, tbest). Must be called from wave-uniform control flow (the stack push
+// writes lane `sp`). best_id = original face index of the hit, -1 if none;
+// an equal-t hit replaces a larger face index (the reference's brute-force
+// loop keeps the lowest index on ties, geom.nim:354).
+template <class R>
+__device__ __forceinline__ void slab2(const RT_CONST BvhNode& nd, V3<R> o, V3<R> ninv, V3<R> oi,
+                                      R tbest, bool active, bool& h0, bool& h1, R& tn0, R& tn1) {
+  if constexpr (Prec<R>::exact) {
+    const R ax0 = (R(nd.lo0[0]) - o.x) * ninv.x, bx0 = (R(nd.hi0[0]) - o.x) * ninv.x;
+    const R ay0 = (R(nd.lo0[1]) - o.y) * ninv.y, by0 = (R(nd.hi0[1]) - o.y) * ninv.y;
+    const R az0 = (R(nd.lo0[2]) - o.z) * ninv.z, bz0 = (R(nd.hi0[2]) - o.z) * ninv.z;
+    const R ax1 = (R(nd.lo1[0]) - o.x) * ninv.x, bx1 = (R(nd.hi1[0]) - o.x) * ninv.x;
+    const R ay1 = (R(nd.lo1[1]) - o.y) * ninv.y, by1 = (R(nd.hi1[1]) - o.y) * ninv.y;
+    const R az1 = (R(nd.lo1[2]) - o.z) * ninv.z, bz1 = (R(nd.hi1[2]) - o.z) * ninv.z;
+    tn0 = fmax(fmax(fmin(ax0, bx0), fmin(ay0, by0)), fmax(fmin(az0, bz0), R(0)));
+    const R tf0 = fmin(fmin(fmax(ax0, bx0), fmax(ay0, by0)), fmin(fmax(az0, bz0), tbest));
+    tn1 = fmax(fmax(fmin(ax1, bx1), fmin(ay1, by1)), fmax(fmin(az1, bz1), R(0)));
+    const R tf1 = fmin(fmin(fmax(ax1, bx1), fmax(ay1, by1)), fmin(fmax(az1, bz1), tbest));
+    h0 = active && tn0 <= tf0 * Prec<R>::node_tmax_scale;
+    h1 = active && tn1 <= tf1 * Prec<R>::node_tmax_scale;
+  } else {
+    const R ax0 = __builtin_fmaf(nd.lo0[0], ninv.x, -oi.x), bx0 = __builtin_fmaf(nd.hi0[0], ninv.x, -oi.x);
+    const R ay0 = __builtin_fmaf(nd.lo0[1], ninv.y, -oi.y), by0 = __builtin_fmaf(nd.hi0[1], ninv.y, -oi.y);
+    const R az0 = __builtin_fmaf(nd.lo0[2], ninv.z, -oi.z), bz0 = __builtin_fmaf(nd.hi0[2], ninv.z, -oi.z);
+    const R ax1 = __builtin_fmaf(nd.lo1[0], ninv.x, -oi.x), bx1 = __builtin_fmaf(nd.hi1[0], ninv.x, -oi.x);
+    const R ay1 = __builtin_fmaf(nd.lo1[1], ninv.y, -oi.y), by1 = __builtin_fmaf(nd.hi1[1], ninv.y, -oi.y);
+    const R az1 = __builtin_fmaf(nd.lo1[2], ninv.z, -oi.z), bz1 = __builtin_fmaf(nd.hi1[2], ninv.z, -oi.z);
+    tn0 = fmaxf(fmaxf(fminf(ax0, bx0), fminf(ay0, by0)), fmaxf(fminf(az0, bz0), 0.0f));
+    const R tf0 = fminf(fminf(fmaxf(ax0, bx0), fmaxf(ay0, by0)), fminf(fmaxf(az0, bz0), tbest));
+    tn1 = fmaxf(fmaxf(fminf(ax1, bx1), fminf(ay1, by1)), fmaxf(fminf(az1, bz1), 0.0f));
+    const R tf1 = fminf(fminf(fmaxf(ax1, bx1), fmaxf(ay1, by1)), fminf(fmaxf(az1, bz1), tbest));
+    h0 = active && tn0 <= tf0 * Prec<R>::node_tmax_scale;
+    h1 = active && tn1 <= tf1 * Prec<R>::node_tmax_scale;
+  }
+}
+
+template <class R>
+__device__ __forceinline__ void leaf(const RenderParams<R>& p, int first, int count, bool h,
+                                     V3<R> o, V3<R> d, R& tbest, int& best_id, bool& active,
+                                     bool anyhit, WaveStats& ws) {
+  using Tri = typename TriOf<R>::type;
+  const unsigned long long m = ballot(h);
+  ws.v[STAT_TRI_FETCH] += (unsigned long long)count;
+  ws.v[STAT_LANE_TRIS] += popc(m) * (unsigned long long)count;
+  for (int k = 0; k < count; ++k) {
+    const RT_CONST Tri& tri = cptr(p.tris)[first + k];
+    const R t = tri_ref<R>(tri, o, d);
+    const int id = tri.id;
+    const bool acc = h && t >= R(0) && (t < tbest || (t == tbest && id < best_id));
+    if (acc) {
+      tbest = t;
+      best_id = id;
+    }
+  }
+  if (anyhit) active = active && best_id < 0;
+}
+
+template <class R>
+__device__ __forceinline__ void traverse(const RenderParams<R>& p, int root, V3<R> o, V3<R> d,
+                                         bool active, bool anyhit, R& tbest, int& best_id,
+                                         WaveStats& ws) {
+  if (ballot(active) == 0ull || root < 0) return;
+  V3<R> ninv, oi;
+  if constexpr (Prec<R>::exact) {
+    ninv = V3<R>{R(1) / d.x, R(1) / d.y, R(1) / d.z};
+    oi = V3<R>{R(0), R(0), R(0)};
+  } else {
+    // clamp exact-zero components so the fma slab form never sees inf*0
+    const float e = 1e-20f;
+    const float dx = __builtin_fabsf(d.x) < e ? __builtin_copysignf(e, d.x) : d.x;
+    const float dy = __builtin_fabsf(d.y) < e ? __builtin_copysignf(e, d.y) : d.y;
+    const float dz = __builtin_fabsf(d.z) < e ? __builtin_copysignf(e, d.z) : d.z;
+    ninv = V3<R>{Prec<R>::rcp(dx), Prec<R>::rcp(dy), Prec<R>::rcp(dz)};
+    oi = V3<R>{o.x * ninv.x, o.y * ninv.y, o.z * ninv.z};
+  }
+  const int lane = (int)__lane_id();
+  int stack = 0;  // entry i lives in lane i
+  int sp = 0;
+  int node = root;
+  for (int iter = 0; iter < p.max_iters; ++iter) {
+    const RT_CONST BvhNode& nd = cptr(p.nodes)[node];
+    const unsigned long long live = ballot(active);
+    ws.v[STAT_NODE_FETCH] += 1ull;
+    ws.v[STAT_LANE_NODES] += popc(live);
+    bool h0, h1;
+    R tn0, tn1;
+    slab2<R>(nd, o, ninv, oi, tbest, active, h0, h1, tn0, tn1);
+    const int c0 = nd.c0, c1 = nd.c1, n0 = nd.n0, n1 = nd.n1;
+    // empty children (c < 0, n == 0) are never visited
+    unsigned long long m0 = (n0 > 0 || c0 >= 0) ? ballot(h0) : 0ull;
+    unsigned long long m1 = (n1 > 0 || c1 >= 0) ? ballot(h1) : 0ull;
+    if (n0 > 0 && m0) {
+      leaf<R>(p, c0, n0, h0, o, d, tbest, best_id, active, anyhit, ws);
+      m0 = 0;
+    }
+    if (n1 > 0 && m1) {
+      leaf<R>(p, c1, n1, h1, o, d, tbest, best_id, active, anyhit, ws);
+      m1 = 0;
+    }
+    if (anyhit && ballot(active) == 0ull) break;
+    if (m0 && m1) {
+      const unsigned long long both = m0 & m1;
+      const unsigned long long near0 = ballot(h0 && h1 && tn0 <= tn1);
+      const bool first0 = popc(near0) * 2 >= popc(both);
+      const int near = first0 ? c0 : c1;
+      const int far = first0 ? c1 : c0;
+      stack = (lane == sp) ? far : stack;
+      ++sp;
+      node = near;
+    } else if (m0) {
+      node = c0;
+    } else if (m1) {
+      node = c1;
+    } else {
+      if (sp == 0) break;
+      --sp;
+      node = __builtin_amdgcn_readlane(stack, sp);
+    }
+  }
+}
+
+// ---- trace (renderer.nim:47-67) --------------------------------------------
+template <class R>
+struct Hit {
+  int obj;   // -1 = nil
+  int tri;   // original face index of a mesh hit, -1 otherwise
+  R t;
+};
+
+// Linear closest hit over the scene's objects in order, for lanes with
+// `active`; tmin starts at t_near. Wave-uniform control flow only.
+template <class R>
+__device__ __forceinline__ Hit<R> trace(const RenderParams<R>& p, V3<R> o, V3<R> d, R t_near,
+                                        bool active, bool anyhit, WaveStats& ws) {
+  Hit<R> h{-1, -1, t_near};
+  const unsigned long long live = ballot(active);
+  ws.v[STAT_TESTS] += popc(live) * (unsigned long long)p.nobj;
+  for (int i = 0; i < p.nobj; ++i) {
+    const RT_CONST DevObject<R>& ob = cptr(p.objects)[i];
+    const int type = ob.type;
+    const ORay<R> r = init_oray<R>(xform<R>(ob.w2o, o, R(1)), xform<R>(ob.w2o, d, R(0)));
+    R t;
+    int tri = -1;
+    if (type == GEOM_SPHERE) {
+      t = sphere_ref<R>(ob.prm[0], r);
+    } else if (type == GEOM_PLANE) {
+      t = plane_ref<R>(r);
+    } else if (type == GEOM_BOX) {
+      t = aabb_ref<R>(V3<R>{ob.prm[0], ob.prm[1], ob.prm[2]}, V3<R>{ob.prm[4], ob.prm[5], ob.prm[6]}, r);
+    } else if (type == GEOM_MESH) {
+      const RT_CONST DevMesh<R>& m = cptr(p.meshes)[ob.mesh];
+      // TriangleMesh.intersect (geom.nim:339-358): AABB gate (tmin < 0 ->
+      // miss, so rays starting inside the box miss), then closest face.
+      const R gate = aabb_ref<R>(V3<R>{m.lo[0], m.lo[1], m.lo[2]}, V3<R>{m.hi[0], m.hi[1], m.hi[2]}, r);
+      const bool in = active && gate >= R(0);
+      R tb = h.t;
+      int best = -1;
+      traverse<R>(p, m.root, r.o, r.d, in, anyhit, tb, best, ws);
+      t = !(gate >= R(0)) ? -pinf<R>() : (best >= 0 ? tb : pinf<R>());
+      tri = best;
+    } else {
+      t = -pinf<R>();
+    }
+    const bool upd = active && t >= R(0) && t < h.t;
+    ws.v[STAT_HITS] += popc(ballot(upd));
+    if (upd) {
+      h.t = t;
+      h.obj = i;
+      h.tri = tri;
+    }
+  }
+  return h;
+}
+
+// ---- shade (renderer.nim:71-127) -------------------------------------------
+template <class R>
+__device__ __forceinline__ V3<R> object_normal(const DevObject<R>& ob, int type, V3<R> ho) {
+  if (type == GEOM_SPHERE) return normalize_dir<R>(ho);            // geom.nim:364-365
+  if (type == GEOM_PLANE) return V3<R>{R(0), R(1), R(0)};          // geom.nim:367-368
+  if (type == GEOM_BOX) {                                          // geom.nim:370-379
+    const V3<R> vmin{ob.prm[0], ob.prm[1], ob.prm[2]}, vmax{ob.prm[4], ob.prm[5], ob.prm[6]};
+    const V3<R> c{(vmin.x + vmax.x) * R(0.5), (vmin.y + vmax.y) * R(0.5), (vmin.z + vmax.z) * R(0.5)};
+    const V3<R> pp{ho.x - c.x, ho.y - c.y, ho.z - c.z};
+    const V3<R> dd{(vmin.x - vmax.x) * R(0.5), (vmin.y - vmax.y) * R(0.5), (vmin.z - vmax.z) * R(0.5)};
+    // float64: the reference's 1.000001 verbatim. float32: the hit point is
+    // only good to ~1e-5 of the box size, so 1.000001 can truncate every
+    // axis to 0 (a NaN normal); widen to 1.0001 and fall back to the
+    // dominant axis.
+    const R bias = Prec<R>::exact ? R(1.000001) : R(1.0001);
+    const R qx = Prec<R>::div(pp.x, fabs(dd.x)), qy = Prec<R>::div(pp.y, fabs(dd.y)),
+            qz = Prec<R>::div(pp.z, fabs(dd.z));
+    V3<R> n{R((long long)(qx * bias)), R((long long)(qy * bias)), R((long long)(qz * bias))};
+    if constexpr (!Prec<R>::exact) {
+      if (n.x == R(0) && n.y == R(0) && n.z == R(0)) {
+        const R ax = fabs(qx), ay = fabs(qy), az = fabs(qz);
+        if (ax >= ay && ax >= az) n.x = qx < R(0) ? R(-1) : R(1);
+        else if (ay >= az) n.y = qy < R(0) ? R(-1) : R(1);
+        else n.z = qz < R(0) ? R(-1) : R(1);
+      }
+    }
+    return normalize_dir<R>(n);
+  }
+  return V3<R>{R(0), R(0), R(0)};
+}
+
+// One camera sample: trace + shade with the reflection recursion unrolled
+// into a loop of levels. Returns the sample colour (renderer.nim:71-127).
+template <class R>
+__device__ __forceinline__ V3<R> shade_path(const RenderParams<R>& p, V3<R> o, V3<R> d, bool active,
+                                            WaveStats& ws) {
+  const bool anyhit_shadows = (p.flags & 0x1) != 0;
+  constexpr R kPi = R(3.14159265358979323846);
+  bool act = active;
+  int depth = 1;
+  V3<R> terminal{R(0), R(0), R(0)};
+  // perf mode: forward weights; exact mode: the reference's nesting order
+  // (1 - r)*L + r*inner folded from the innermost level outwards.
+  V3<R> facc{R(0), R(0), R(0)};
+  R fw = R(1);
+  V3<R> lvl_c[kMaxShadeLevels];
+  R lvl_r[kMaxShadeLevels];
+  int nlev = 0;
+  for (int lev = 0; lev < kMaxShadeLevels; ++lev) {
+    if (ballot(act) == 0ull) break;
+    const Hit<R> hit = trace<R>(p, o, d, pinf<R>(), act, false, ws);
+    const bool miss = act && hit.obj < 0;
+    if (miss) terminal = V3<R>{p.bg[0], p.bg[1], p.bg[2]};
+    const bool lit = act && hit.obj >= 0;
+    const int oi = lit ? hit.obj : 0;
+    const DevObject<R>& ob = p.objects[oi];
+    const int type = ob.type;
+    const V3<R> hw{o.x + d.x * hit.t, o.y + d.y * hit.t, o.z + d.z * hit.t};
+    const V3<R> ho = xform<R>(ob.w2o, hw, R(1));
+    V3<R> nrm;
+    if (hit.tri >= 0) {
+      const R* fn = p.normals + 3 * (size_t)(p.meshes[ob.mesh].normal_base + hit.tri);
+      nrm = V3<R>{fn[0], fn[1], fn[2]};
+    } else {
+      nrm = object_normal<R>(ob, type, ho);
+    }
+    const V3<R> N = xform<R>(ob.o2w, nrm, R(0));
+    V3<R> local{R(0), R(0), R(0)};
+    for (int li = 0; li < p.nlight; ++li) {
+      const RT_CONST DevLight<R>& L = cptr(p.lights)[li];
+      V3<R> ldir;
+      V3<R> I;
+      R dist;
+      if (L.type == LIGHT_POINT) {  // light.nim:52-62
+        const V3<R> lv{hw.x - L.v[0], hw.y - L.v[1], hw.z - L.v[2]};
+        const R r2 = dot4(lv, R(0), lv, R(0));
+        ldir = normalize_dir<R>(lv);
+        const R den = R(4) * kPi * r2;
+        I = V3<R>{Prec<R>::div(L.ci[0], den), Prec<R>::div(L.ci[1], den), Prec<R>::div(L.ci[2], den)};
+        dist = Prec<R>::sqrt(r2);
+      } else {  // light.nim:46-50
+        ldir = V3<R>{L.v[0], L.v[1], L.v[2]};
+        I = V3<R>{L.ci[0], L.ci[1], L.ci[2]};
+        dist = pinf<R>();
+      }
+      const V3<R> sd{ldir.x * R(-1), ldir.y * R(-1), ldir.z * R(-1)};
+      const V3<R> so{hw.x + N.x * p.bias, hw.y + N.y * p.bias, hw.z + N.z * p.bias};
+      ws.v[STAT_SHADOW] += popc(ballot(lit));
+      const Hit<R> sh = trace<R>(p, so, sd, dist, lit, anyhit_shadows, ws);
+      if (lit && sh.obj < 0) {  // shadeDiffuse (shader.nim:12-17)
+        const R ndl = nmax(R(0), dot4(N, R(0), sd, R(0) * R(-1)));
+        local.x = local.x + Prec<R>::div(ob.albedo[0], kPi) * I.x * ndl;
+        local.y = local.y + Prec<R>::div(ob.albedo[1], kPi) * I.y * ndl;
+        local.z = local.z + Prec<R>::div(ob.albedo[2], kPi) * I.z * ndl;
+      }
+    }
+    const R refl = ob.albedo[3];
+    const bool reflect = lit && refl > R(0) && depth <= p.max_depth;
+    if (lit && !reflect) terminal = local;
+    if constexpr (Prec<R>::exact) {
+      if (reflect) {
+        // shift-register push (static indices keep it in VGPRs)
+#pragma unroll
+        for (int k = kMaxShadeLevels - 1; k > 0; --k) {
+          lvl_c[k] = lvl_c[k - 1];
+          lvl_r[k] = lvl_r[k - 1];
+        }
+        lvl_c[0] = local;
+        lvl_r[0] = refl;
+        ++nlev;
+      }
+    } else {
+      if (reflect) {
+        const R wl = fw * (R(1) - refl);
+        facc = V3<R>{facc.x + wl * local.x, facc.y + wl * local.y, facc.z + wl * local.z};
+        fw = fw * refl;
+      }
+    }
+    ws.v[STAT_REFL] += popc(ballot(reflect));
+    if (reflect) {
+      // renderer.nim:109-118
+      const R ndi = R(2) * dot4(N, R(0), d, R(0));
+      const V3<R> rd{d.x - N.x * ndi, d.y - N.y * ndi, d.z - N.z * ndi};
+      o = V3<R>{hw.x + rd.x * p.bias, hw.y + rd.y * p.bias, hw.z + rd.z * p.bias};
+      d = rd;
+      ++depth;
+    }
+    act = reflect;
+  }
+  if constexpr (Prec<R>::exact) {
+    V3<R> c = terminal;
+#pragma unroll
+    for (int k = 0; k < kMaxShadeLevels; ++k) {
+      if (k < nlev) {
+        const R r = lvl_r[k];
+        c = V3<R>{(R(1) - r) * lvl_c[k].x + r * c.x, (R(1) - r) * lvl_c[k].y + r * c.y,
+                  (R(1) - r) * lvl_c[k].z + r * c.z};
+      }
+    }
+    return c;
+  } else {
+    return V3<R>{facc.x + fw * terminal.x, facc.y + fw * terminal.y, facc.z + fw * terminal.z};
+  }
+}
+
+// ---- the render kernel -----------------------------------------------------
+template <class R>
+__global__ __launch_bounds__(256) void k_render(const RenderParams<R> p) {
+  const int lane = (int)__lane_id();
+  const long long wave = (long long)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const long long nwaves = (long long)gridDim.x * (blockDim.x >> 6);
+  const int L = p.lanes_per_px;
+  const int sub = lane % L;
+  const int pix = lane / L;
+  const int tpx = pix % p.tile_x, tpy = pix / p.tile_x;
+  const int iters = (p.spp + L - 1) / L;
+  const bool grid_aa = p.aa_kind != 0;
+  WaveStats ws;
+#pragma unroll
+  for (int k = 0; k < kStatSlots; ++k) ws.v[k] = 0ull;
+
+  for (long long g = wave; g < p.ngroups; g += nwaves) {
+    const int gx = (int)(g % p.tiles_x), gy = (int)(g / p.tiles_x);
+    const int j = gx * p.tile_x + tpx;
+    const int k = gy * p.tile_y + tpy;
+    const int x = j * p.step;
+    int y, out_row;
+    bool valid = j < p.ncols && k < p.nrows;
+    if (p.mode == 0) {
+      y = p.y0 + k * p.step;
+      out_row = y;
+    } else {
+      const int lb = k / p.band_h, rr = k % p.band_h;
+      y = (lb * p.world + p.rank) * p.band_h + rr;
+      out_row = k;
+      valid = valid && y < p.height;
+    }
+    if (p.step < p.max_step) {  // progressive refinement skip (renderer.nim:175-178)
+      const int mask = p.step * 2 - 1;
+      if ((x & mask) == 0 && (y & mask) == 0) valid = false;
+    }
+    V3<R> acc{R(0), R(0), R(0)};
+    for (int it = 0; it < iters; ++it) {
+      const int s = it * L + sub;
+      const bool sv = valid && s < p.spp;
+      R px = R(x), py = R(y);
+      if (grid_aa) {  // grid() sampling.nim:5-18, p[j*m + i]
+        const int si = s % p.grid_m, sj = s / p.grid_m;
+        px = R(x) + (R(si) * p.sample_step + p.sample_off);
+        py = R(y) + (R(sj) * p.sample_step + p.sample_off);
+      }
+      // castPrimaryRay (renderer.nim:31-44)
+      const R cx = (Prec<R>::div(R(2) * px * p.aspect, R(p.width)) - p.aspect) * p.f;
+      const R cy = (R(1) - Prec<R>::div(R(2) * py, R(p.height))) * p.f;
+      const V3<R> dn = normalize_dir<R>(V3<R>{cx, cy, R(-1)});
+      const V3<R> o = xform<R>(p.c2w, V3<R>{R(0), R(0), R(0)}, R(1));
+      const V3<R> d = xform<R>(p.c2w, dn, R(0));
+      ws.v[STAT_PRIMARY] += popc(ballot(sv));
+      const V3<R> c = shade_path<R>(p, o, d, sv, ws);
+      if (sv) {
+        if (grid_aa) {
+          acc = V3<R>{acc.x + c.x, acc.y + c.y, acc.z + c.z};
+        } else {
+          acc = c;
+        }
+      }
+    }
+    // sum the L lanes of each pixel (exact mode launches with L = 1)
+    for (int off = 1; off < L; off <<= 1) {
+      acc.x += __shfl_xor(acc.x, off);
+      acc.y += __shfl_xor(acc.y, off);
+      acc.z += __shfl_xor(acc.z, off);
+    }
+    if (valid && sub == 0) {
+      if (grid_aa) acc = V3<R>{acc.x * p.inv_len, acc.y * p.inv_len, acc.z * p.inv_len};
+      const float cr = (float)acc.x, cg = (float)acc.y, cb = (float)acc.z;
+      if (p.mode == 0 && p.step > 1) {
+        const int xe = min(x + p.step, p.width), ye = min(y + p.step, p.height);
+        for (int yy = y; yy < ye; ++yy)
+          for (int xx = x; xx < xe; ++xx) {
+            float* q = p.fb + ((size_t)yy * p.width + xx) * 3;
+            q[0] = cr; q[1] = cg; q[2] = cb;
+          }
+      } else {
+        float* q = p.fb + ((size_t)out_row * p.width + x) * 3;
+        q[0] = cr; q[1] = cg; q[2] = cb;
+      }
+    }
+  }
+  if (lane < kStatSlots) {
+    unsigned long long v = 0ull;
+#pragma unroll
+    for (int k = 0; k < kStatSlots; ++k) v = (lane == k) ? ws.v[k] : v;
+    p.partials[wave * kStatSlots + lane] = v;
+  }
+}
+
+}  // namespace rtmi

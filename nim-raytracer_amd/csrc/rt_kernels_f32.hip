@@ -1,0 +1,80 @@
+// rt_kernels_f32.hip — float (performance mode) instantiation of the render
+// kernel, plus the precision-independent helper kernels (stats reduction,
+// multi-GPU band un-interleave). Built with FMA contraction on.
+#include "rt_device.h"
+
+namespace rtmi {
+
+// Sum per-wave partial counters into acc (one block; acc accumulates across
+// launches until the host clears it).
+__global__ __launch_bounds__(256) void k_reduce_stats(const unsigned long long* __restrict__ partials,
+                                                      int num_waves, unsigned long long* __restrict__ acc) {
+  __shared__ unsigned long long red[256];
+  for (int k = 0; k < kStatSlots; ++k) {
+    unsigned long long s = 0;
+    for (int w = threadIdx.x; w < num_waves; w += blockDim.x) s += partials[(size_t)w * kStatSlots + k];
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int off = blockDim.x / 2; off > 0; off >>= 1) {
+      if ((int)threadIdx.x < off) red[threadIdx.x] += red[threadIdx.x + off];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) acc[k] += red[0];
+    __syncthreads();
+  }
+}
+
+// Rank-0 epilogue of the framebuffer gather: gathered = world compact band
+// buffers back to back, each band_rows rows; image row y lives in band
+// b = y / band_h owned by rank b % world as local band b / world.
+__global__ __launch_bounds__(256) void k_unshard(const float4* __restrict__ gathered, float4* __restrict__ fb,
+                                                 int row_f4, int height, int band_h, int world, int band_rows) {
+  const int y = blockIdx.x;
+  if (y >= height) return;
+  const int b = y / band_h, r = y % band_h;
+  const int owner = b % world, lb = b / world;
+  const size_t src_row = (size_t)owner * band_rows + (size_t)lb * band_h + r;
+  const float4* src = gathered + src_row * row_f4;
+  float4* dst = fb + (size_t)y * row_f4;
+  for (int i = threadIdx.x; i < row_f4; i += blockDim.x) dst[i] = src[i];
+}
+
+__global__ __launch_bounds__(256) void k_unshard_scalar(const float* __restrict__ gathered, float* __restrict__ fb,
+                                                        int row_f, int height, int band_h, int world, int band_rows) {
+  const int y = blockIdx.x;
+  if (y >= height) return;
+  const int b = y / band_h, r = y % band_h;
+  const int owner = b % world, lb = b / world;
+  const size_t src_row = (size_t)owner * band_rows + (size_t)lb * band_h + r;
+  for (int i = threadIdx.x; i < row_f; i += blockDim.x) fb[(size_t)y * row_f + i] = gathered[src_row * row_f + i];
+}
+
+template __global__ void k_render<float>(const RenderParams<float>);
+
+}  // namespace rtmi
+
+extern "C" int rtmi_launch_render_f32(const rtmi::RenderParams<float>* p, int blocks, void* stream) {
+  hipLaunchKernelGGL(rtmi::k_render<float>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, *p);
+  return (int)hipGetLastError();
+}
+
+extern "C" int rtmi_launch_reduce_stats(const unsigned long long* partials, int num_waves,
+                                        unsigned long long* acc, void* stream) {
+  hipLaunchKernelGGL(rtmi::k_reduce_stats, dim3(1), dim3(256), 0, (hipStream_t)stream, partials, num_waves, acc);
+  return (int)hipGetLastError();
+}
+
+extern "C" int rtmi_launch_unshard(const float* gathered, float* fb, int width, int height, int band_h,
+                                   int world, void* stream) {
+  const int nbands = (height + band_h - 1) / band_h;
+  const int band_rows = ((nbands + world - 1) / world) * band_h;
+  const int row_f = width * 3;
+  if ((row_f % 4) == 0 && (((uintptr_t)gathered | (uintptr_t)fb) & 15) == 0) {
+    hipLaunchKernelGGL(rtmi::k_unshard, dim3(height), dim3(256), 0, (hipStream_t)stream,
+                       (const float4*)gathered, (float4*)fb, row_f / 4, height, band_h, world, band_rows);
+  } else {
+    hipLaunchKernelGGL(rtmi::k_unshard_scalar, dim3(height), dim3(256), 0, (hipStream_t)stream, gathered, fb,
+                       row_f, height, band_h, world, band_rows);
+  }
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,754 @@
+// rtmi.cpp — C-ABI (include/rtmi.h) of the MI355X trace/shade backend.
+//
+// Replaces the reference's renderLine / initRenderer
+// (src/renderer/renderer.nim:162-215) behind plain C entry points: the scene
+// is flattened and uploaded once (rt_scene_create), then whole frames, row
+// ranges (the pool's scanline messages, src/raytracer.nim:25-32) or
+// multi-GPU bands are rendered by the gfx950 kernels in rt_device.h.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/rtmi.h"
+#include "rt_bvh.h"
+#include "rt_common.h"
+
+using namespace rtmi;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                  \
+  do {                                                                                 \
+    hipError_t e_ = (expr);                                                            \
+    if (e_ != hipSuccess) return fail(RT_E_DEVICE, "%s: %s", #expr, hipGetErrorString(e_)); \
+  } while (0)
+
+template <class T>
+struct DevBuf {
+  T* p = nullptr;
+  size_t n = 0;
+  int alloc(size_t count) {
+    release();
+    if (count == 0) count = 1;
+    hipError_t e = hipMalloc((void**)&p, count * sizeof(T));
+    if (e != hipSuccess) {
+      p = nullptr;
+      return fail(RT_E_NOMEM, "hipMalloc(%zu bytes): %s", count * sizeof(T), hipGetErrorString(e));
+    }
+    n = count;
+    return RT_OK;
+  }
+  int upload(const std::vector<T>& h) {
+    int rc = alloc(h.size());
+    if (rc != RT_OK) return rc;
+    if (!h.empty()) HIP_TRY(hipMemcpy(p, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice));
+    return RT_OK;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
+  size_t bytes() const { return n * sizeof(T); }
+};
+
+template <class R>
+struct PrecisionData {
+  DevBuf<DevObject<R>> objects;
+  DevBuf<DevLight<R>> lights;
+  DevBuf<DevMesh<R>> meshes;
+  DevBuf<typename TriOf<R>::type> tris;
+  DevBuf<R> normals;
+  void release() {
+    objects.release();
+    lights.release();
+    meshes.release();
+    tris.release();
+    normals.release();
+  }
+  size_t bytes() const {
+    return objects.bytes() + lights.bytes() + meshes.bytes() + tris.bytes() + normals.bytes();
+  }
+};
+
+bool is_pow2(int v) { return v > 0 && (v & (v - 1)) == 0; }
+
+int device_of_current() {
+  int d = -1;
+  (void)hipGetDevice(&d);
+  return d;
+}
+
+}  // namespace
+
+struct rt_scene {
+  std::mutex mu;
+  int device = 0;
+  int num_cus = 256;
+  hipStream_t stream = nullptr;
+  hipEvent_t done = nullptr;
+  int32_t nobj = 0, nlight = 0, nmesh = 0;
+  bool any_reflective = false;
+  double fov = 50.0;
+  double c2w[16];
+  double bg[3];
+  PrecisionData<float> f32;
+  PrecisionData<double> f64;
+  DevBuf<BvhNode> nodes;
+  DevBuf<unsigned long long> partials;
+  DevBuf<unsigned long long> acc;
+  DevBuf<float> fb_scratch;
+  int max_waves = 0;
+  int64_t num_triangles = 0, num_nodes = 0;
+  int max_depth = 0;
+  double build_ms = 0.0;
+
+  ~rt_scene() {
+    f32.release();
+    f64.release();
+    nodes.release();
+    partials.release();
+    acc.release();
+    fb_scratch.release();
+    if (done) (void)hipEventDestroy(done);
+    if (stream) (void)hipStreamDestroy(stream);
+  }
+};
+
+extern "C" {
+
+int rt_version(void) { return RTMI_ABI_VERSION; }
+
+const char* rt_last_error(void) { return g_err.c_str(); }
+
+int rt_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  return n;
+}
+
+int rt_init(int device) {
+  const int n = rt_device_count();
+  if (n <= 0) return fail(RT_E_DEVICE, "no HIP device visible");
+  if (device < 0 || device >= n) return fail(RT_E_INVALID, "device %d out of range [0, %d)", device, n);
+  HIP_TRY(hipSetDevice(device));
+  hipDeviceProp_t prop;
+  HIP_TRY(hipGetDeviceProperties(&prop, device));
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+    return fail(RT_E_DEVICE, "device %d is %s; librtmi.so is built for gfx950 (MI355X) only", device,
+                prop.gcnArchName);
+  return RT_OK;
+}
+
+int rt_mat4_inverse(const double m_[16], double out[16]) {
+  if (!m_ || !out) return fail(RT_E_INVALID, "null matrix");
+  // GLM compute_inverse (cofactors times 1/determinant), m[c][r] = m_[c*4+r]
+  auto m = [&](int c, int r) { return m_[c * 4 + r]; };
+  const double Coef00 = m(2, 2) * m(3, 3) - m(3, 2) * m(2, 3);
+  const double Coef02 = m(1, 2) * m(3, 3) - m(3, 2) * m(1, 3);
+  const double Coef03 = m(1, 2) * m(2, 3) - m(2, 2) * m(1, 3);
+  const double Coef04 = m(2, 1) * m(3, 3) - m(3, 1) * m(2, 3);
+  const double Coef06 = m(1, 1) * m(3, 3) - m(3, 1) * m(1, 3);
+  const double Coef07 = m(1, 1) * m(2, 3) - m(2, 1) * m(1, 3);
+  const double Coef08 = m(2, 1) * m(3, 2) - m(3, 1) * m(2, 2);
+  const double Coef10 = m(1, 1) * m(3, 2) - m(3, 1) * m(1, 2);
+  const double Coef11 = m(1, 1) * m(2, 2) - m(2, 1) * m(1, 2);
+  const double Coef12 = m(2, 0) * m(3, 3) - m(3, 0) * m(2, 3);
+  const double Coef14 = m(1, 0) * m(3, 3) - m(3, 0) * m(1, 3);
+  const double Coef15 = m(1, 0) * m(2, 3) - m(2, 0) * m(1, 3);
+  const double Coef16 = m(2, 0) * m(3, 2) - m(3, 0) * m(2, 2);
+  const double Coef18 = m(1, 0) * m(3, 2) - m(3, 0) * m(1, 2);
+  const double Coef19 = m(1, 0) * m(2, 2) - m(2, 0) * m(1, 2);
+  const double Coef20 = m(2, 0) * m(3, 1) - m(3, 0) * m(2, 1);
+  const double Coef22 = m(1, 0) * m(3, 1) - m(3, 0) * m(1, 1);
+  const double Coef23 = m(1, 0) * m(2, 1) - m(2, 0) * m(1, 1);
+  const double Fac0[4] = {Coef00, Coef00, Coef02, Coef03};
+  const double Fac1[4] = {Coef04, Coef04, Coef06, Coef07};
+  const double Fac2[4] = {Coef08, Coef08, Coef10, Coef11};
+  const double Fac3[4] = {Coef12, Coef12, Coef14, Coef15};
+  const double Fac4[4] = {Coef16, Coef16, Coef18, Coef19};
+  const double Fac5[4] = {Coef20, Coef20, Coef22, Coef23};
+  const double Vec0[4] = {m(1, 0), m(0, 0), m(0, 0), m(0, 0)};
+  const double Vec1[4] = {m(1, 1), m(0, 1), m(0, 1), m(0, 1)};
+  const double Vec2[4] = {m(1, 2), m(0, 2), m(0, 2), m(0, 2)};
+  const double Vec3[4] = {m(1, 3), m(0, 3), m(0, 3), m(0, 3)};
+  double inv[4][4];
+  const double SignA[4] = {+1, -1, +1, -1}, SignB[4] = {-1, +1, -1, +1};
+  for (int i = 0; i < 4; ++i) {
+    inv[0][i] = (Vec1[i] * Fac0[i] - Vec2[i] * Fac1[i] + Vec3[i] * Fac2[i]) * SignA[i];
+    inv[1][i] = (Vec0[i] * Fac0[i] - Vec2[i] * Fac3[i] + Vec3[i] * Fac4[i]) * SignB[i];
+    inv[2][i] = (Vec0[i] * Fac1[i] - Vec1[i] * Fac3[i] + Vec3[i] * Fac5[i]) * SignA[i];
+    inv[3][i] = (Vec0[i] * Fac2[i] - Vec1[i] * Fac4[i] + Vec2[i] * Fac5[i]) * SignB[i];
+  }
+  const double Row0[4] = {inv[0][0], inv[1][0], inv[2][0], inv[3][0]};
+  double Dot0[4];
+  for (int i = 0; i < 4; ++i) Dot0[i] = m(0, i) * Row0[i];
+  const double Dot1 = (Dot0[0] + Dot0[1]) + (Dot0[2] + Dot0[3]);
+  if (Dot1 == 0.0 || !std::isfinite(Dot1)) return fail(RT_E_INVALID, "singular matrix");
+  const double one_over_det = 1.0 / Dot1;
+  for (int c = 0; c < 4; ++c)
+    for (int r = 0; r < 4; ++r) out[c * 4 + r] = inv[c][r] * one_over_det;
+  return RT_OK;
+}
+
+int rt_load_geom(const char* path, int64_t* num_triangles, double* vertices) {
+  if (!path || !num_triangles) return fail(RT_E_INVALID, "null argument");
+  FILE* f = std::fopen(path, "rb");
+  if (!f) return fail(RT_E_IO, "cannot open %s", path);
+  int32_t n = 0;
+  if (std::fread(&n, 4, 1, f) != 1 || n < 0) {
+    std::fclose(f);
+    return fail(RT_E_IO, "%s: bad .geom header", path);
+  }
+  if (!vertices) {
+    std::fclose(f);
+    *num_triangles = n;
+    return RT_OK;
+  }
+  if (*num_triangles < n) {
+    std::fclose(f);
+    return fail(RT_E_INVALID, "buffer holds %lld triangles, file has %d", (long long)*num_triangles, n);
+  }
+  std::vector<float> buf((size_t)n * 9);
+  const size_t got = buf.empty() ? 0 : std::fread(buf.data(), sizeof(float), buf.size(), f);
+  std::fclose(f);
+  if (got != buf.size()) return fail(RT_E_IO, "%s: truncated (%zu of %zu floats)", path, got, buf.size());
+  for (size_t i = 0; i < buf.size(); ++i) vertices[i] = (double)buf[i];
+  *num_triangles = n;
+  return RT_OK;
+}
+
+int rt_band_rows(int32_t height, int32_t band_h, int32_t world, int32_t* out_rows) {
+  if (!out_rows || height <= 0 || band_h <= 0 || world <= 0) return fail(RT_E_INVALID, "bad band geometry");
+  const int32_t nbands = (height + band_h - 1) / band_h;
+  *out_rows = ((nbands + world - 1) / world) * band_h;
+  return RT_OK;
+}
+
+}  // extern "C"
+
+namespace {
+
+bool affine(const double* m) { return m[3] == 0.0 && m[7] == 0.0 && m[11] == 0.0 && m[15] == 1.0; }
+
+template <class R>
+void fill_precision(const rt_scene_desc* d, const std::vector<std::vector<double>>& normals,
+                    const std::vector<BvhResult>& bvhs, const std::vector<int32_t>& node_base,
+                    const std::vector<std::vector<double>>& aabbs, std::vector<DevObject<R>>& objs,
+                    std::vector<DevLight<R>>& lights, std::vector<DevMesh<R>>& meshes,
+                    std::vector<typename TriOf<R>::type>& tris, std::vector<R>& nrm) {
+  objs.assign((size_t)d->num_objects, DevObject<R>{});
+  for (int i = 0; i < d->num_objects; ++i) {
+    const rt_object_desc& s = d->objects[i];
+    DevObject<R>& o = objs[(size_t)i];
+    for (int k = 0; k < 16; ++k) {
+      o.w2o[k] = (R)s.world_to_object[k];
+      o.o2w[k] = (R)s.object_to_world[k];
+    }
+    o.prm[0] = (R)(s.type == RT_SPHERE ? s.radius : s.box_min[0]);
+    o.prm[1] = (R)s.box_min[1];
+    o.prm[2] = (R)s.box_min[2];
+    o.prm[4] = (R)s.box_max[0];
+    o.prm[5] = (R)s.box_max[1];
+    o.prm[6] = (R)s.box_max[2];
+    for (int k = 0; k < 3; ++k) o.albedo[k] = (R)s.albedo[k];
+    o.albedo[3] = (R)s.reflection;
+    o.type = s.type;
+    o.mesh = s.type == RT_MESH ? s.mesh : 0;
+  }
+  lights.assign((size_t)d->num_lights, DevLight<R>{});
+  for (int i = 0; i < d->num_lights; ++i) {
+    const rt_light_desc& s = d->lights[i];
+    DevLight<R>& l = lights[(size_t)i];
+    // color * intensity, computed in float64 like light.nim:50,57
+    for (int k = 0; k < 3; ++k) l.ci[k] = (R)(s.color[k] * s.intensity);
+    for (int k = 0; k < 3; ++k) l.v[k] = (R)(s.type == RT_POINT_LIGHT ? s.pos[k] : s.dir[k]);
+    l.type = s.type == RT_POINT_LIGHT ? LIGHT_POINT : LIGHT_DISTANT;
+  }
+  meshes.assign((size_t)d->num_meshes, DevMesh<R>{});
+  tris.clear();
+  nrm.clear();
+  int32_t normal_base = 0;
+  for (int m = 0; m < d->num_meshes; ++m) {
+    const rt_mesh_desc& md = d->meshes[m];
+    DevMesh<R>& dm = meshes[(size_t)m];
+    for (int k = 0; k < 3; ++k) {
+      dm.lo[k] = (R)aabbs[(size_t)m][k];
+      dm.hi[k] = (R)aabbs[(size_t)m][3 + k];
+    }
+    dm.num_faces = (int32_t)md.num_faces;
+    dm.normal_base = normal_base;
+    dm.root = bvhs[(size_t)m].nodes.empty() ? -1 : node_base[(size_t)m];
+    const int32_t tri_base = (int32_t)tris.size();
+    (void)tri_base;
+    for (int32_t face : bvhs[(size_t)m].order) {
+      typename TriOf<R>::type t{};
+      const int32_t* fi = &md.faces[3 * (size_t)face];
+      const double* v0 = &md.vertices[3 * (size_t)fi[0]];
+      const double* v1 = &md.vertices[3 * (size_t)fi[1]];
+      const double* v2 = &md.vertices[3 * (size_t)fi[2]];
+      for (int k = 0; k < 3; ++k) {
+        t.v0[k] = (R)v0[k];
+        t.e1[k] = (R)(v1[k] - v0[k]);  // v0v1 exactly as geom.nim:286-288
+        t.e2[k] = (R)(v2[k] - v0[k]);  // v0v2 exactly as geom.nim:292-294
+      }
+      t.id = face;
+      tris.push_back(t);
+    }
+    for (double x : normals[(size_t)m]) nrm.push_back((R)x);
+    normal_base += (int32_t)md.num_faces;
+  }
+}
+
+}  // namespace
+
+extern "C" int rt_scene_create(const rt_scene_desc* d, rt_scene** out_scene) {
+  if (!d || !out_scene) return fail(RT_E_INVALID, "null argument");
+  *out_scene = nullptr;
+  if (d->num_objects < 0 || d->num_lights < 0 || d->num_meshes < 0)
+    return fail(RT_E_INVALID, "negative counts");
+  if ((d->num_objects > 0 && !d->objects) || (d->num_lights > 0 && !d->lights) ||
+      (d->num_meshes > 0 && !d->meshes))
+    return fail(RT_E_INVALID, "null array with nonzero count");
+  if (!affine(d->camera_to_world)) return fail(RT_E_UNSUPPORTED, "camera_to_world is not affine");
+  const auto t0 = std::chrono::steady_clock::now();
+  bool any_reflective = false;
+  for (int i = 0; i < d->num_objects; ++i) {
+    const rt_object_desc& o = d->objects[i];
+    if (o.type < RT_SPHERE || o.type > RT_MESH) return fail(RT_E_INVALID, "object %d: bad type %d", i, o.type);
+    if (o.type == RT_MESH && (o.mesh < 0 || o.mesh >= d->num_meshes))
+      return fail(RT_E_INVALID, "object %d: mesh index %d out of range", i, o.mesh);
+    if (!affine(o.object_to_world) || !affine(o.world_to_object))
+      return fail(RT_E_UNSUPPORTED, "object %d: non-affine transform", i);
+    if (o.reflection > 0.0) any_reflective = true;
+  }
+  for (int i = 0; i < d->num_lights; ++i)
+    if (d->lights[i].type != RT_DISTANT_LIGHT && d->lights[i].type != RT_POINT_LIGHT)
+      return fail(RT_E_INVALID, "light %d: bad type", i);
+  std::vector<std::vector<double>> normals((size_t)d->num_meshes), aabbs((size_t)d->num_meshes);
+  std::vector<BvhResult> bvhs((size_t)d->num_meshes);
+  std::vector<int32_t> node_base((size_t)d->num_meshes, 0);
+  int64_t ntri = 0, nnodes = 0;
+  int maxdepth = 0;
+  std::vector<BvhNode> all_nodes;
+  for (int m = 0; m < d->num_meshes; ++m) {
+    const rt_mesh_desc& md = d->meshes[m];
+    if (md.num_faces < 0 || md.num_vertices < 0 || (md.num_faces > 0 && (!md.faces || !md.vertices)))
+      return fail(RT_E_INVALID, "mesh %d: bad arrays", m);
+    for (int64_t k = 0; k < md.num_faces * 3; ++k)
+      if (md.faces[k] < 0 || md.faces[k] >= md.num_vertices)
+        return fail(RT_E_INVALID, "mesh %d: face index %d out of range", m, md.faces[k]);
+    // face normals: given, or calcNormals (src/loaders/obj.nim:65-84)
+    std::vector<double>& nr = normals[(size_t)m];
+    nr.resize((size_t)md.num_faces * 3);
+    for (int64_t fidx = 0; fidx < md.num_faces; ++fidx) {
+      if (md.normals) {
+        for (int k = 0; k < 3; ++k) nr[3 * (size_t)fidx + k] = md.normals[3 * fidx + k];
+        continue;
+      }
+      const double* p0 = &md.vertices[3 * (size_t)md.faces[3 * fidx + 0]];
+      const double* p1 = &md.vertices[3 * (size_t)md.faces[3 * fidx + 1]];
+      const double* p2 = &md.vertices[3 * (size_t)md.faces[3 * fidx + 2]];
+      const double ax = p1[0] - p0[0], ay = p1[1] - p0[1], az = p1[2] - p0[2];
+      const double bx = p2[0] - p0[0], by = p2[1] - p0[1], bz = p2[2] - p0[2];
+      const double cx = ay * bz - az * by, cy = az * bx - ax * bz, cz = ax * by - ay * bx;
+      double dd = 0.0;
+      dd = dd + cx * cx;
+      dd = dd + cy * cy;
+      dd = dd + cz * cz;
+      const double len = std::sqrt(dd);
+      nr[3 * (size_t)fidx + 0] = cx / len;
+      nr[3 * (size_t)fidx + 1] = cy / len;
+      nr[3 * (size_t)fidx + 2] = cz / len;
+    }
+    // calcAABB (geom.nim:175-188) over every vertex
+    std::vector<double>& bb = aabbs[(size_t)m];
+    bb = {INFINITY, INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY};
+    for (int64_t v = 0; v < md.num_vertices; ++v)
+      for (int k = 0; k < 3; ++k) {
+        const double x = md.vertices[3 * v + k];
+        if (x < bb[(size_t)k]) bb[(size_t)k] = x;
+        if (x > bb[3 + (size_t)k]) bb[3 + (size_t)k] = x;
+      }
+    const char* err = "BVH build failed";
+    BvhBuildParams prm;
+    if (!build_bvh(md.vertices, md.faces, md.num_faces, prm, &bvhs[(size_t)m], &err))
+      return fail(RT_E_INVALID, "mesh %d: %s", m, err);
+    node_base[(size_t)m] = (int32_t)all_nodes.size();
+    for (BvhNode nd : bvhs[(size_t)m].nodes) {
+      if (nd.n0 == 0 && nd.c0 >= 0) nd.c0 += node_base[(size_t)m];
+      if (nd.n1 == 0 && nd.c1 >= 0) nd.c1 += node_base[(size_t)m];
+      if (nd.n0 > 0) nd.c0 += (int32_t)ntri;
+      if (nd.n1 > 0) nd.c1 += (int32_t)ntri;
+      all_nodes.push_back(nd);
+    }
+    ntri += md.num_faces;
+    nnodes += (int64_t)bvhs[(size_t)m].nodes.size();
+    maxdepth = std::max(maxdepth, bvhs[(size_t)m].max_depth);
+  }
+  if (ntri > INT32_MAX / 2) return fail(RT_E_UNSUPPORTED, "too many triangles");
+
+  int dev = device_of_current();
+  if (dev < 0 || rt_device_count() <= 0) return fail(RT_E_DEVICE, "no HIP device (call rt_init)");
+  hipDeviceProp_t prop;
+  HIP_TRY(hipGetDeviceProperties(&prop, dev));
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+    return fail(RT_E_DEVICE, "device %d is %s; librtmi.so is built for gfx950 only", dev, prop.gcnArchName);
+
+  std::unique_ptr<rt_scene> s(new rt_scene());
+  s->device = dev;
+  s->num_cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+  s->nobj = d->num_objects;
+  s->nlight = d->num_lights;
+  s->nmesh = d->num_meshes;
+  s->any_reflective = any_reflective;
+  s->fov = d->fov;
+  std::memcpy(s->c2w, d->camera_to_world, sizeof s->c2w);
+  std::memcpy(s->bg, d->bg_color, sizeof s->bg);
+  HIP_TRY(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
+  HIP_TRY(hipEventCreateWithFlags(&s->done, hipEventDisableTiming));
+  {
+    std::vector<DevObject<float>> o;
+    std::vector<DevLight<float>> l;
+    std::vector<DevMesh<float>> m;
+    std::vector<TriF32> t;
+    std::vector<float> n;
+    fill_precision<float>(d, normals, bvhs, node_base, aabbs, o, l, m, t, n);
+    int rc;
+    if ((rc = s->f32.objects.upload(o)) || (rc = s->f32.lights.upload(l)) || (rc = s->f32.meshes.upload(m)) ||
+        (rc = s->f32.tris.upload(t)) || (rc = s->f32.normals.upload(n)))
+      return rc;
+  }
+  {
+    std::vector<DevObject<double>> o;
+    std::vector<DevLight<double>> l;
+    std::vector<DevMesh<double>> m;
+    std::vector<TriF64> t;
+    std::vector<double> n;
+    fill_precision<double>(d, normals, bvhs, node_base, aabbs, o, l, m, t, n);
+    int rc;
+    if ((rc = s->f64.objects.upload(o)) || (rc = s->f64.lights.upload(l)) || (rc = s->f64.meshes.upload(m)) ||
+        (rc = s->f64.tris.upload(t)) || (rc = s->f64.normals.upload(n)))
+      return rc;
+  }
+  int rc = s->nodes.upload(all_nodes);
+  if (rc) return rc;
+  s->max_waves = s->num_cus * 8 * 4;  // 8 blocks of 4 waves per CU at most
+  if ((rc = s->partials.alloc((size_t)s->max_waves * kStatSlots))) return rc;
+  if ((rc = s->acc.alloc(kStatSlots))) return rc;
+  HIP_TRY(hipMemset(s->acc.p, 0, kStatSlots * sizeof(unsigned long long)));
+  HIP_TRY(hipDeviceSynchronize());
+  s->num_triangles = ntri;
+  s->num_nodes = nnodes;
+  s->max_depth = maxdepth;
+  s->build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  *out_scene = s.release();
+  return RT_OK;
+}
+
+extern "C" int rt_scene_destroy(rt_scene* s) {
+  if (!s) return fail(RT_E_INVALID, "null scene");
+  int prev = device_of_current();
+  if (prev != s->device) (void)hipSetDevice(s->device);
+  if (s->stream) (void)hipStreamSynchronize(s->stream);
+  delete s;
+  if (prev >= 0 && prev != -1) (void)hipSetDevice(prev);
+  return RT_OK;
+}
+
+extern "C" int rt_scene_get_info(const rt_scene* s, rt_scene_info* out) {
+  if (!s || !out) return fail(RT_E_INVALID, "null argument");
+  out->num_objects = s->nobj;
+  out->num_lights = s->nlight;
+  out->num_meshes = s->nmesh;
+  out->num_triangles = s->num_triangles;
+  out->num_bvh_nodes = s->num_nodes;
+  out->max_bvh_depth = s->max_depth;
+  out->device = s->device;
+  out->device_bytes = (int64_t)(s->f32.bytes() + s->f64.bytes() + s->nodes.bytes() + s->partials.bytes() +
+                                s->acc.bytes());
+  out->build_ms = s->build_ms;
+  return RT_OK;
+}
+
+namespace {
+
+struct Mapping {
+  int mode, y0, nrows, ncols, step, max_step, band_h, rank, world;
+};
+
+int check_options(const rt_scene* s, const rt_options* o) {
+  if (!o) return fail(RT_E_INVALID, "null options");
+  if (o->width <= 0 || o->height <= 0 || o->width > 65536 || o->height > 65536)
+    return fail(RT_E_INVALID, "bad image size %dx%d", o->width, o->height);
+  if (o->aa_kind == RT_AA_JITTERED || o->aa_kind == RT_AA_MULTI_JITTERED ||
+      o->aa_kind == RT_AA_CORRELATED_MULTI_JITTERED)
+    return fail(RT_E_UNSUPPORTED, "stochastic antialias kind %d is not implemented yet", o->aa_kind);
+  if (o->aa_kind != RT_AA_NONE && o->aa_kind != RT_AA_GRID) return fail(RT_E_INVALID, "bad aa_kind %d", o->aa_kind);
+  if (o->aa_kind == RT_AA_GRID && (o->grid_size < 1 || o->grid_size > 256))
+    return fail(RT_E_INVALID, "grid_size %d out of range [1, 256]", o->grid_size);
+  if (o->precision != RT_FP32 && o->precision != RT_FP64) return fail(RT_E_INVALID, "bad precision");
+  if (s->any_reflective && o->max_ray_depth > kMaxShadeLevels - 1)
+    return fail(RT_E_UNSUPPORTED, "max_ray_depth %d > %d with reflective materials", o->max_ray_depth,
+                kMaxShadeLevels - 1);
+  return RT_OK;
+}
+
+template <class R>
+void fill_params(rt_scene* s, const PrecisionData<R>& pd, const rt_options* o, const Mapping& mp, float* fb,
+                 RenderParams<R>& p, int* blocks) {
+  std::memset(&p, 0, sizeof p);
+  p.objects = pd.objects.p;
+  p.lights = pd.lights.p;
+  p.meshes = pd.meshes.p;
+  p.nodes = s->nodes.p;
+  p.tris = pd.tris.p;
+  p.normals = pd.normals.p;
+  p.fb = fb;
+  p.partials = s->partials.p;
+  for (int k = 0; k < 16; ++k) p.c2w[k] = (R)s->c2w[k];
+  for (int k = 0; k < 3; ++k) p.bg[k] = (R)s->bg[k];
+  // castPrimaryRay constants (renderer.nim:36-38), float64 on the host
+  p.f = (R)std::tan(s->fov * (3.14159265358979323846 / 180.0) / 2);
+  p.aspect = (R)((double)o->width / (double)o->height);
+  p.bias = (R)o->bias;
+  const int m = o->aa_kind == RT_AA_GRID ? o->grid_size : 1;
+  const int spp = m * m;
+  p.inv_len = (R)(1.0 / (double)spp);
+  const double xs = 1.0 / (double)m;  // grid(): xs = 1/n, ys = 1/m (m = n)
+  p.sample_step = (R)xs;
+  p.sample_off = (R)(xs * 0.5);
+  p.nobj = s->nobj;
+  p.nlight = s->nlight;
+  p.width = o->width;
+  p.height = o->height;
+  p.aa_kind = o->aa_kind;
+  p.grid_m = m;
+  p.spp = spp;
+  p.max_depth = o->max_ray_depth;
+  p.flags = (int32_t)o->flags;
+  p.max_iters = (int32_t)std::min<int64_t>(INT32_MAX, 2 * s->num_nodes + 16);
+  p.mode = mp.mode;
+  p.y0 = mp.y0;
+  p.nrows = mp.nrows;
+  p.ncols = mp.ncols;
+  p.step = mp.step;
+  p.max_step = mp.max_step;
+  p.band_h = mp.band_h;
+  p.rank = mp.rank;
+  p.world = mp.world;
+  // lanes per pixel: float64 parity mode keeps the reference's sequential
+  // sample sum (one lane per pixel); float32 spreads samples over lanes.
+  int L = 1;
+  if (o->precision == RT_FP32) {
+    while (L * 2 <= std::min(spp, 64)) L *= 2;
+  }
+  const int P = 64 / L;
+  int tx = 1, ty = 1;
+  switch (P) {
+    case 64: tx = 8; ty = 8; break;
+    case 32: tx = 8; ty = 4; break;
+    case 16: tx = 4; ty = 4; break;
+    case 8: tx = 4; ty = 2; break;
+    case 4: tx = 2; ty = 2; break;
+    case 2: tx = 2; ty = 1; break;
+    default: tx = 1; ty = 1; break;
+  }
+  p.lanes_per_px = L;
+  p.tile_x = tx;
+  p.tile_y = ty;
+  p.tiles_x = (mp.ncols + tx - 1) / tx;
+  const long long tiles_y = (mp.nrows + ty - 1) / ty;
+  p.ngroups = (long long)p.tiles_x * tiles_y;
+  const long long want = (p.ngroups + 3) / 4;
+  *blocks = (int)std::max(1LL, std::min<long long>(want, s->max_waves / 4));
+}
+
+int launch(rt_scene* s, const rt_options* o, const Mapping& mp, float* d_out, hipStream_t st) {
+  int blocks = 1;
+  if (o->precision == RT_FP64) {
+    RenderParams<double> p;
+    fill_params<double>(s, s->f64, o, mp, d_out, p, &blocks);
+    if (p.ngroups == 0) return RT_OK;
+    const int e = rtmi_launch_render_f64(&p, blocks, st);
+    if (e) return fail(RT_E_DEVICE, "render kernel launch failed: %s", hipGetErrorString((hipError_t)e));
+  } else {
+    RenderParams<float> p;
+    fill_params<float>(s, s->f32, o, mp, d_out, p, &blocks);
+    if (p.ngroups == 0) return RT_OK;
+    const int e = rtmi_launch_render_f32(&p, blocks, st);
+    if (e) return fail(RT_E_DEVICE, "render kernel launch failed: %s", hipGetErrorString((hipError_t)e));
+  }
+  const int e = rtmi_launch_reduce_stats(s->partials.p, blocks * 4, s->acc.p, st);
+  if (e) return fail(RT_E_DEVICE, "stats reduction launch failed: %s", hipGetErrorString((hipError_t)e));
+  return RT_OK;
+}
+
+int read_stats(rt_scene* s, hipStream_t st, rt_stats* out) {
+  unsigned long long h[kStatSlots];
+  HIP_TRY(hipMemcpyAsync(h, s->acc.p, sizeof h, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  out->num_primary_rays = h[STAT_PRIMARY];
+  out->num_intersection_tests = h[STAT_TESTS];
+  out->num_intersection_hits = h[STAT_HITS];
+  out->num_shadow_rays = h[STAT_SHADOW];
+  out->num_reflection_rays = h[STAT_REFL];
+  return RT_OK;
+}
+
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    prev = device_of_current();
+    if (prev != dev) (void)hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+// Common device-side body: order after the previous call, clear the
+// counters, launch, record completion.
+int render_device(rt_scene* s, const rt_options* o, const Mapping& mp, float* d_out, hipStream_t st,
+                  rt_stats* out) {
+  HIP_TRY(hipStreamWaitEvent(st, s->done, 0));
+  HIP_TRY(hipMemsetAsync(s->acc.p, 0, kStatSlots * sizeof(unsigned long long), st));
+  int rc = launch(s, o, mp, d_out, st);
+  if (rc) return rc;
+  HIP_TRY(hipEventRecord(s->done, st));
+  if (out) return read_stats(s, st, out);
+  return RT_OK;
+}
+
+int lines_mapping(const rt_options* o, int32_t y0, int32_t y1, int32_t step, int32_t max_step, Mapping* mp) {
+  if (!is_pow2(step) || !is_pow2(max_step) || max_step < step)
+    return fail(RT_E_INVALID, "step %d / maxStep %d must be powers of two with maxStep >= step", step, max_step);
+  if (y0 < 0 || y1 > o->height || y0 > y1) return fail(RT_E_INVALID, "rows [%d, %d) outside [0, %d)", y0, y1, o->height);
+  mp->mode = 0;
+  mp->y0 = y0;
+  mp->nrows = (y1 - y0 + step - 1) / step;
+  mp->ncols = (o->width + step - 1) / step;
+  mp->step = step;
+  mp->max_step = max_step;
+  mp->band_h = 1;
+  mp->rank = 0;
+  mp->world = 1;
+  return RT_OK;
+}
+
+}  // namespace
+
+extern "C" int rt_render_lines_device(rt_scene* s, const rt_options* o, float* d_fb, int32_t y0, int32_t y1,
+                                      int32_t step, int32_t max_step, void* stream, rt_stats* out) {
+  if (!s || !d_fb) return fail(RT_E_INVALID, "null argument");
+  int rc = check_options(s, o);
+  if (rc) return rc;
+  Mapping mp;
+  if ((rc = lines_mapping(o, y0, y1, step, max_step, &mp))) return rc;
+  std::lock_guard<std::mutex> lk(s->mu);
+  DeviceGuard g(s->device);
+  return render_device(s, o, mp, d_fb, stream ? (hipStream_t)stream : s->stream, out);
+}
+
+extern "C" int rt_render_lines(rt_scene* s, const rt_options* o, float* fb, int32_t fb_w, int32_t fb_h, int32_t y0,
+                               int32_t y1, int32_t step, int32_t max_step, rt_stats* out) {
+  if (!s || !fb) return fail(RT_E_INVALID, "null argument");
+  int rc = check_options(s, o);
+  if (rc) return rc;
+  if (fb_w != o->width || fb_h != o->height)
+    return fail(RT_E_INVALID, "framebuffer %dx%d does not match options %dx%d", fb_w, fb_h, o->width, o->height);
+  Mapping mp;
+  if ((rc = lines_mapping(o, y0, y1, step, max_step, &mp))) return rc;
+  rt_stats local{};
+  if (mp.nrows == 0) {
+    if (out) *out = local;
+    return RT_OK;
+  }
+  std::lock_guard<std::mutex> lk(s->mu);
+  DeviceGuard g(s->device);
+  const size_t need = (size_t)o->width * o->height * 3;
+  if (s->fb_scratch.n < need && (rc = s->fb_scratch.alloc(need))) return rc;
+  // rows the call may write: renderLine fills step x step blocks below y
+  const int32_t last_y = y0 + (mp.nrows - 1) * step;
+  const int32_t r0 = y0, r1 = std::min(last_y + step, o->height);
+  const size_t off = (size_t)r0 * o->width * 3, cnt = (size_t)(r1 - r0) * o->width * 3;
+  hipStream_t st = s->stream;
+  HIP_TRY(hipMemcpyAsync(s->fb_scratch.p + off, fb + off, cnt * sizeof(float), hipMemcpyHostToDevice, st));
+  if ((rc = render_device(s, o, mp, s->fb_scratch.p, st, nullptr))) return rc;
+  HIP_TRY(hipMemcpyAsync(fb + off, s->fb_scratch.p + off, cnt * sizeof(float), hipMemcpyDeviceToHost, st));
+  if ((rc = read_stats(s, st, &local))) return rc;
+  if (out) *out = local;
+  return RT_OK;
+}
+
+extern "C" int rt_render_bands_device(rt_scene* s, const rt_options* o, float* d_bands, int32_t band_h,
+                                      int32_t rank, int32_t world, void* stream, rt_stats* out) {
+  if (!s || !d_bands) return fail(RT_E_INVALID, "null argument");
+  int rc = check_options(s, o);
+  if (rc) return rc;
+  if (band_h <= 0 || world <= 0 || rank < 0 || rank >= world)
+    return fail(RT_E_INVALID, "bad band geometry band_h=%d rank=%d world=%d", band_h, rank, world);
+  int32_t rows = 0;
+  if ((rc = rt_band_rows(o->height, band_h, world, &rows))) return rc;
+  Mapping mp;
+  mp.mode = 1;
+  mp.y0 = 0;
+  mp.nrows = rows;
+  mp.ncols = o->width;
+  mp.step = 1;
+  mp.max_step = 1;
+  mp.band_h = band_h;
+  mp.rank = rank;
+  mp.world = world;
+  std::lock_guard<std::mutex> lk(s->mu);
+  DeviceGuard g(s->device);
+  return render_device(s, o, mp, d_bands, stream ? (hipStream_t)stream : s->stream, out);
+}
+
+extern "C" int rt_unshard_bands_device(const float* d_gathered, float* d_fb, int32_t width, int32_t height,
+                                       int32_t band_h, int32_t world, void* stream) {
+  if (!d_gathered || !d_fb || width <= 0 || height <= 0 || band_h <= 0 || world <= 0)
+    return fail(RT_E_INVALID, "bad arguments");
+  const int e = rtmi_launch_unshard(d_gathered, d_fb, width, height, band_h, world, stream);
+  if (e) return fail(RT_E_DEVICE, "unshard launch failed: %s", hipGetErrorString((hipError_t)e));
+  return RT_OK;
+}
+
+extern "C" int rt_scene_last_counters(rt_scene* s, rt_traversal_counters* out) {
+  if (!s || !out) return fail(RT_E_INVALID, "null argument");
+  std::lock_guard<std::mutex> lk(s->mu);
+  DeviceGuard g(s->device);
+  unsigned long long h[kStatSlots];
+  HIP_TRY(hipEventSynchronize(s->done));
+  HIP_TRY(hipMemcpy(h, s->acc.p, sizeof h, hipMemcpyDeviceToHost));
+  out->wave_node_fetches = h[STAT_NODE_FETCH];
+  out->wave_tri_fetches = h[STAT_TRI_FETCH];
+  out->lane_node_visits = h[STAT_LANE_NODES];
+  out->lane_tri_tests = h[STAT_LANE_TRIS];
+  return RT_OK;
+}

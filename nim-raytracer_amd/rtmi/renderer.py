@@ -1,0 +1,150 @@
+"""Renderer API over librtmi.so, mirroring src/renderer/renderer.nim.
+
+    initRenderer(device)                         renderer.nim:214-215
+    renderLine(scene, opts, fb, y, step, maxStep) -> Stats
+                                                 renderer.nim:162-211
+plus the whole-frame and multi-GPU forms that replace the scanline worker
+pool (src/raytracer.nim:25-109, src/concurrency/workerpool.nim) with one GPU
+dispatch. `scene` here is a DeviceScene: the reference's Scene flattened and
+uploaded once (BVH built) — the Nim shim in INTEGRATION.md does the same.
+"""
+import ctypes as C
+
+import numpy as np
+
+from . import abi
+from ._lib import RtmiError, check, lib
+from .scene import Options, Scene, Stats, flatten
+
+
+def initRenderer(device=0):
+    """Bind this thread to GPU `device` (must be gfx950)."""
+    check(lib().rt_init(int(device)))
+
+
+def device_count():
+    return int(lib().rt_device_count())
+
+
+class DeviceScene:
+    """A Scene resident in HBM on one GPU (objects, lights, BVH, triangles)."""
+
+    def __init__(self, scene: Scene, device=0):
+        initRenderer(device)
+        self.device = device
+        self.scene = scene
+        flat = flatten(scene)
+        h = C.c_void_p()
+        check(lib().rt_scene_create(C.byref(flat.desc), C.byref(h)))
+        self.h = h
+
+    def close(self):
+        if getattr(self, "h", None) and self.h.value:
+            lib().rt_scene_destroy(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def info(self):
+        i = abi.rt_scene_info()
+        check(lib().rt_scene_get_info(self.h, C.byref(i)))
+        return i.as_dict()
+
+    # -- host framebuffer (the pool-compatible path) ----------------------
+    def render_lines(self, opts: Options, fb, y0, y1, step=1, maxStep=1) -> Stats:
+        """renderLine for every y in countup(y0, y1-1, step); fb is a
+        C-contiguous float32 array of shape (h, w, 3) (framebuf.nim layout)."""
+        if not (isinstance(fb, np.ndarray) and fb.dtype == np.float32 and fb.flags.c_contiguous
+                and fb.shape == (opts.height, opts.width, 3)):
+            raise ValueError("fb must be a C-contiguous float32 array of shape (height, width, 3)")
+        o = opts.to_c()
+        st = abi.rt_stats()
+        check(lib().rt_render_lines(self.h, C.byref(o), fb.ctypes.data_as(C.POINTER(C.c_float)),
+                                    opts.width, opts.height, int(y0), int(y1), int(step),
+                                    int(maxStep), C.byref(st)))
+        return Stats.from_c(st)
+
+    # -- device framebuffer (the fast path) --------------------------------
+    def render_device(self, opts: Options, d_fb, y0=0, y1=None, step=1, maxStep=1, stream=None,
+                      stats=True):
+        """Render rows into a device buffer (int pointer or torch tensor of
+        height*width*3 float32). With stats=False nothing synchronises."""
+        ptr = _ptr(d_fb, opts.width * opts.height * 3)
+        o = opts.to_c()
+        st = abi.rt_stats()
+        check(lib().rt_render_lines_device(self.h, C.byref(o), C.c_void_p(ptr), int(y0),
+                                           int(opts.height if y1 is None else y1), int(step),
+                                           int(maxStep), _stream(stream),
+                                           C.byref(st) if stats else None))
+        return Stats.from_c(st) if stats else None
+
+    def render_bands_device(self, opts: Options, d_bands, band_h, rank, world, stream=None,
+                            stats=True):
+        rows = band_rows(opts.height, band_h, world)
+        ptr = _ptr(d_bands, rows * opts.width * 3)
+        o = opts.to_c()
+        st = abi.rt_stats()
+        check(lib().rt_render_bands_device(self.h, C.byref(o), C.c_void_p(ptr), int(band_h), int(rank),
+                                           int(world), _stream(stream), C.byref(st) if stats else None))
+        return Stats.from_c(st) if stats else None
+
+    def last_counters(self):
+        c = abi.rt_traversal_counters()
+        check(lib().rt_scene_last_counters(self.h, C.byref(c)))
+        return c.as_dict()
+
+
+def band_rows(height, band_h, world):
+    out = C.c_int32()
+    check(lib().rt_band_rows(int(height), int(band_h), int(world), C.byref(out)))
+    return out.value
+
+
+def unshard_bands_device(d_gathered, d_fb, width, height, band_h, world, stream=None):
+    rows = band_rows(height, band_h, world)
+    check(lib().rt_unshard_bands_device(C.c_void_p(_ptr(d_gathered, world * rows * width * 3)),
+                                        C.c_void_p(_ptr(d_fb, width * height * 3)), int(width),
+                                        int(height), int(band_h), int(world), _stream(stream)))
+
+
+def renderLine(scene: DeviceScene, opts: Options, fb, y, step=1, maxStep=1) -> Stats:
+    """renderer.nim:162-211 — one scanline (and its step x step blocks)."""
+    return scene.render_lines(opts, fb, y, y + 1, step, maxStep)
+
+
+def render_frame(scene: DeviceScene, opts: Options, fb=None):
+    """Whole frame through the host-framebuffer path. Returns (fb, Stats)."""
+    if fb is None:
+        fb = np.zeros((opts.height, opts.width, 3), dtype=np.float32)
+    st = scene.render_lines(opts, fb, 0, opts.height, 1, 1)
+    return fb, st
+
+
+def _ptr(buf, min_floats):
+    if isinstance(buf, int):
+        return buf
+    try:  # torch tensor
+        import torch  # noqa: F401
+        if not buf.is_cuda or buf.dtype.itemsize != 4 or not buf.is_contiguous():
+            raise ValueError("device buffer must be a contiguous 4-byte CUDA/HIP tensor")
+        if buf.numel() < min_floats:
+            raise ValueError(f"device buffer holds {buf.numel()} floats, need {min_floats}")
+        return int(buf.data_ptr())
+    except AttributeError:
+        raise TypeError("device buffer must be an int pointer or a torch tensor") from None
+
+
+def _stream(stream):
+    if stream is None:
+        return None
+    if isinstance(stream, int):
+        return C.c_void_p(stream)
+    return C.c_void_p(int(stream.cuda_stream))
+
+
+__all__ = ["DeviceScene", "RtmiError", "band_rows", "device_count", "initRenderer", "renderLine",
+           "render_frame", "unshard_bands_device"]

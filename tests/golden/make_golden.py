@@ -1,0 +1,45 @@
+"""Generate the committed golden fixtures with the oracle (fp64 restatement).
+
+    python tests/golden/make_golden.py
+
+Each .npz holds `fb` (h, w, 3 float32), `stats` (primary, tests, hits,
+shadow, reflection) and `meta` (scene/options as JSON). They pin the oracle
+against regressions; the GPU parity tests compare against the oracle itself.
+"""
+import json
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(REPO, "nim-raytracer_amd"))
+sys.path.insert(0, os.path.join(REPO, "oracle"))
+
+import oracle  # noqa: E402
+from rtmi import Antialias, Options, Precision, scenes  # noqa: E402
+
+CASES = {
+    "c1_spheres_warm3": dict(scene="spheres-warm-3", w=128, h=96, aa=0, m=1, bias=1e-4, depth=5),
+    "boxes2_grid2": dict(scene="boxes2", w=96, h=54, aa=1, m=2, bias=1e-4, depth=5),
+    "reflection": dict(scene="spheres-reflection", w=96, h=64, aa=0, m=1, bias=1e-4, depth=5),
+    "bunny": dict(scene="mesh-bunny", w=64, h=48, aa=0, m=1, bias=1e-4, depth=5),
+}
+
+
+def main():
+    oracle.build()
+    for name, c in CASES.items():
+        opts = Options(width=c["w"], height=c["h"], antialias=Antialias(c["aa"], c["m"]),
+                       bias=c["bias"], maxRayDepth=c["depth"], precision=Precision.fp64)
+        fb, st, _ = oracle.OracleScene(scenes.SCENES[c["scene"]]()).render(opts)
+        stats = np.array([st.numPrimaryRays, st.numIntersectionTests, st.numIntersectionHits,
+                          st.numShadowRays, st.numReflectionRays], dtype=np.int64)
+        np.savez_compressed(os.path.join(HERE, f"{name}.npz"), fb=fb, stats=stats,
+                            meta=np.array(json.dumps(c)))
+        print(name, st)
+
+
+if __name__ == "__main__":
+    main()
