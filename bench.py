@@ -1,0 +1,244 @@
+#!/usr/bin/env python3
+"""Benchmark: Mray/s (primary + shadow) on bunny.geom, 1920x1080, 256 spp.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+
+One step = one full frame of BASELINE config C3 (mesh-bunny layout: baked
+bunny.geom 69,451 triangles + ground plane, 2 distant lights, akGrid 16x16 =
+256 samples per pixel, fp32 performance mode) rendered from a scene resident
+in HBM into a device framebuffer. With N GPUs the SAME frame is cut into
+16-row bands dealt round-robin to the ranks, each rank renders its bands and
+one RCCL all-gather + an on-GPU un-interleave assembles the frame on rank 0
+(strong scaling; the gather is inside the timed region).
+
+Printed (rank 0, one JSON line): value = (primary + shadow rays of all ranks)
+x K / max-over-ranks wall time, plus
+  roofline     — the dominant kernel (k_render<float>): bytes its BVH
+                 traversal fetches (wave-level node + triangle records, counted
+                 on the GPU) / its average duration, timed live with HIP events
+                 on the stream it runs on, vs the 8 TB/s HBM peak; `traffic` is
+                 the PMC-measured HBM bytes per launch from the committed
+                 rocprofv3 summary (profiles/), or null;
+  cpu_baseline — the fp64 oracle (the reference algorithm: linear objects,
+                 brute-force mesh, scanline thread pool) on this host, 1 spp on
+                 a bounded row subsample of the same frame (rank 0, N = 1 only).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "nim-raytracer_amd"))
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md "Chip-level parameters")
+NODE_BYTES = 64        # one BvhNode record (two child boxes + refs)
+TRI_BYTES = 48         # one TriF32 record (v0, e1, e2, face id)
+BAND_H = 16
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--grid", type=int, default=16, help="akGrid m (spp = m*m)")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline sample time")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--flags", type=int, default=0, help="rt_options.flags (1 = any-hit shadows)")
+    return ap.parse_args()
+
+
+def cpu_baseline(scene, width, height, target_s):
+    """The oracle (reference algorithm, fp64, brute-force mesh) on a uniform
+    row subsample of the same frame at 1 spp, on this host's cores."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle
+    from rtmi import Antialias, Options, Precision, akGrid
+
+    try:
+        ncpu = len(os.sched_getaffinity(0))
+    except AttributeError:
+        ncpu = os.cpu_count() or 1
+    threads = max(1, min(16, ncpu))  # the GPU box's CPU share is 16 threads
+    opts = Options(width=width, height=height, antialias=Antialias(akGrid, 1), bias=1e-4,
+                   precision=Precision.fp64)
+    osc = oracle.OracleScene(scene)
+    # calibrate on a sparse probe, then size the sample to ~target_s
+    probe = list(range(7, height, max(1, height // 24)))
+    _, st, secs = osc.render(opts, rows=probe, nthreads=threads)
+    per_row = secs / len(probe)
+    n = int(max(len(probe), min(height, target_s / max(per_row, 1e-6))))
+    stride = max(1, height // n)
+    rows = list(range(stride // 2, height, stride))
+    _, st, secs = osc.render(opts, rows=rows, nthreads=threads)
+    rays = st.numPrimaryRays + st.numShadowRays
+    return {
+        "value": rays / secs / 1e6,
+        "unit": "Mray/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": (f"oracle/rt_oracle.c (fp64 restatement of the reference path: linear object loop, "
+                   f"brute-force TriangleMesh.intersect, scanline pool of {threads} threads), same "
+                   f"scene/camera at 1 spp (akGrid 1), {len(rows)} of {height} rows (every "
+                   f"{stride}th), {rays} rays in {secs:.2f} s"),
+    }
+
+
+def load_traffic(workload_key):
+    """HBM bytes per k_render launch from the committed PMC summary, if any."""
+    p = os.path.join(REPO, "profiles", "pmc_summary.json")
+    try:
+        with open(p) as f:
+            d = json.load(f)
+        e = d.get(workload_key)
+        return None if e is None else float(e["hbm_bytes_per_launch"])
+    except (OSError, ValueError, KeyError):
+        return None
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    from rtmi import Antialias, Options, Precision, akGrid, scenes
+    from rtmi.dist import band_rows, render_frame_distributed
+    from rtmi.renderer import DeviceScene
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    W, H, m = args.width, args.height, args.grid
+    scene = scenes.mesh_bunny()
+    t0 = time.time()
+    ds = DeviceScene(scene, device=local)
+    info = ds.info()
+    setup_s = time.time() - t0
+    opts = Options(width=W, height=H, antialias=Antialias(akGrid, m), bias=1e-4,
+                   precision=Precision.fp32, flags=args.flags)
+    stream = torch.cuda.current_stream()
+    rows = band_rows(H, BAND_H, world)
+    fb = torch.zeros(H * W * 3, dtype=torch.float32, device="cuda")
+    local_buf = torch.zeros(rows * W * 3, dtype=torch.float32, device="cuda")
+    gathered = torch.zeros(world * rows * W * 3, dtype=torch.float32, device="cuda")
+
+    from rtmi.renderer import unshard_bands_device
+
+    def step(time_kernel=None):
+        # render this rank's bands (world == 1: the whole frame, one band set)
+        if time_kernel is not None:
+            time_kernel[0].record(stream)
+        if world > 1:
+            ds.render_bands_device(opts, local_buf, BAND_H, rank, world, stream=stream, stats=False)
+        else:
+            ds.render_device(opts, fb, stream=stream, stats=False)
+        if time_kernel is not None:
+            time_kernel[1].record(stream)
+        if world > 1:
+            dist.all_gather_into_tensor(gathered, local_buf)
+            if rank == 0:
+                unshard_bands_device(gathered, fb, W, H, BAND_H, world, stream=stream)
+
+    # warmup (+ the deterministic per-frame ray counts)
+    st = ds.render_bands_device(opts, local_buf, BAND_H, rank, world, stream=stream, stats=True)
+    counters = ds.last_counters()
+    for _ in range(max(0, args.warmup)):
+        step()
+    rays_local = st.numPrimaryRays + st.numShadowRays
+    if world > 1:
+        t = torch.tensor([rays_local, st.numPrimaryRays, st.numShadowRays], dtype=torch.int64,
+                         device="cuda")
+        dist.all_reduce(t)
+        rays_frame, prim_frame, shadow_frame = [int(x) for x in t.tolist()]
+    else:
+        rays_frame, prim_frame, shadow_frame = rays_local, st.numPrimaryRays, st.numShadowRays
+
+    # timed region
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(evs[k])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        e = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = float(e.item())
+    kern_ms = sum(a.elapsed_time(b) for a, b in evs) / max(1, args.steps)
+
+    value = rays_frame * args.steps / elapsed / 1e6
+    # algorithmic traffic of one k_render launch on this rank (wave-level record fetches)
+    bytes_launch = (counters["wave_node_fetches"] * NODE_BYTES + counters["wave_tri_fetches"] * TRI_BYTES
+                    + rows * W * 12)
+    achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
+    workload_key = f"c3_{W}x{H}_m{m}_world{world}"
+    traffic = load_traffic(workload_key)
+
+    if rank == 0:
+        out = {
+            "metric": "Mray/s (primary+shadow) on bunny.geom 1080p/256spp; 1/2/4/8-GPU scaling",
+            "value": round(value, 2),
+            "unit": "Mray/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic rays over the reference's bunny.geom fixture (69,451 triangles)",
+            "config": {
+                "workload": ("C3: bunny.geom baked x30 + ground plane, mesh-bunny.nim lights/camera, "
+                             f"{W}x{H}, akGrid {m}x{m} = {m * m} spp, fp32, {BAND_H}-row bands "
+                             f"round-robin over {world} GPU(s) + RCCL all-gather"),
+                "width": W, "height": H, "spp": m * m, "triangles": info["num_triangles"],
+                "bvh_nodes": info["num_bvh_nodes"], "primary_rays_per_frame": prim_frame,
+                "shadow_rays_per_frame": shadow_frame, "parallelism": f"bands{world}",
+                "scene_setup_s": round(setup_s, 3), "bvh_build_ms": round(info["build_ms"], 1),
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": traffic,
+                "kernel": "k_render<float>",
+                "kernel_ms": round(kern_ms, 4),
+                "bytes_per_launch": int(bytes_launch),
+                "lane_node_visits": counters["lane_node_visits"],
+                "lane_tri_tests": counters["lane_tri_tests"],
+                "wave_node_fetches": counters["wave_node_fetches"],
+                "wave_tri_fetches": counters["wave_tri_fetches"],
+            },
+            "cpu_baseline": None,
+        }
+        if world == 1 and not args.no_cpu:
+            out["cpu_baseline"] = cpu_baseline(scene, W, H, args.cpu_seconds)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

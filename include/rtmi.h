@@ -11,8 +11,8 @@
  * This header is what a Nim `{.importc, dynlib: "librtmi.so".}` module binds
  * in its place. Plain C types only: pointers, sizes,
  * fixed-width integers and doubles. No torch/HIP types in any signature;
- * device streams are passed as opaque `void*` (a hipStream_t, NULL = the
- * scene's own stream).
+ * device streams are passed as opaque `void*` (a hipStream_t; NULL is HIP's
+ * null stream, exactly as in the HIP API).
  *
  * Conventions
  *  - Every entry point returns int: RT_OK (0) or a negative RT_E_* code.

@@ -5,23 +5,25 @@
 
 namespace rtmi {
 
-// Sum per-wave partial counters into acc (one block; acc accumulates across
-// launches until the host clears it).
+// Sum per-wave partial counters into acc (acc accumulates across launches
+// until the host clears it). Each block folds kWavesPerBlock waves in
+// registers, then one atomic per counter per block.
+constexpr int kWavesPerBlock = 256;
 __global__ __launch_bounds__(256) void k_reduce_stats(const unsigned long long* __restrict__ partials,
                                                       int num_waves, unsigned long long* __restrict__ acc) {
-  __shared__ unsigned long long red[256];
-  for (int k = 0; k < kStatSlots; ++k) {
-    unsigned long long s = 0;
-    for (int w = threadIdx.x; w < num_waves; w += blockDim.x) s += partials[(size_t)w * kStatSlots + k];
-    red[threadIdx.x] = s;
-    __syncthreads();
-    for (int off = blockDim.x / 2; off > 0; off >>= 1) {
-      if ((int)threadIdx.x < off) red[threadIdx.x] += red[threadIdx.x + off];
-      __syncthreads();
+  __shared__ unsigned long long red[kStatSlots][256];
+  const int w = blockIdx.x * kWavesPerBlock + threadIdx.x;
+#pragma unroll
+  for (int k = 0; k < kStatSlots; ++k) red[k][threadIdx.x] = w < num_waves ? partials[(size_t)w * kStatSlots + k] : 0ull;
+  __syncthreads();
+  for (int off = 128; off > 0; off >>= 1) {
+    if ((int)threadIdx.x < off) {
+#pragma unroll
+      for (int k = 0; k < kStatSlots; ++k) red[k][threadIdx.x] += red[k][threadIdx.x + off];
     }
-    if (threadIdx.x == 0) acc[k] += red[0];
     __syncthreads();
   }
+  if ((int)threadIdx.x < kStatSlots) atomicAdd(&acc[threadIdx.x], red[threadIdx.x][0]);
 }
 
 // Rank-0 epilogue of the framebuffer gather: gathered = world compact band
@@ -60,7 +62,8 @@ extern "C" int rtmi_launch_render_f32(const rtmi::RenderParams<float>* p, int bl
 
 extern "C" int rtmi_launch_reduce_stats(const unsigned long long* partials, int num_waves,
                                         unsigned long long* acc, void* stream) {
-  hipLaunchKernelGGL(rtmi::k_reduce_stats, dim3(1), dim3(256), 0, (hipStream_t)stream, partials, num_waves, acc);
+  const int blocks = (num_waves + rtmi::kWavesPerBlock - 1) / rtmi::kWavesPerBlock;
+  hipLaunchKernelGGL(rtmi::k_reduce_stats, dim3(blocks > 0 ? blocks : 1), dim3(256), 0, (hipStream_t)stream, partials, num_waves, acc);
   return (int)hipGetLastError();
 }
 

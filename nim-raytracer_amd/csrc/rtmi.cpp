@@ -672,7 +672,7 @@ extern "C" int rt_render_lines_device(rt_scene* s, const rt_options* o, float* d
   if ((rc = lines_mapping(o, y0, y1, step, max_step, &mp))) return rc;
   std::lock_guard<std::mutex> lk(s->mu);
   DeviceGuard g(s->device);
-  return render_device(s, o, mp, d_fb, stream ? (hipStream_t)stream : s->stream, out);
+  return render_device(s, o, mp, d_fb, (hipStream_t)stream, out);
 }
 
 extern "C" int rt_render_lines(rt_scene* s, const rt_options* o, float* fb, int32_t fb_w, int32_t fb_h, int32_t y0,
@@ -727,7 +727,7 @@ extern "C" int rt_render_bands_device(rt_scene* s, const rt_options* o, float* d
   mp.world = world;
   std::lock_guard<std::mutex> lk(s->mu);
   DeviceGuard g(s->device);
-  return render_device(s, o, mp, d_bands, stream ? (hipStream_t)stream : s->stream, out);
+  return render_device(s, o, mp, d_bands, (hipStream_t)stream, out);
 }
 
 extern "C" int rt_unshard_bands_device(const float* d_gathered, float* d_fb, int32_t width, int32_t height,

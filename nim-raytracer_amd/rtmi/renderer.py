@@ -139,11 +139,17 @@ def _ptr(buf, min_floats):
 
 
 def _stream(stream):
+    """hipStream_t for the C-ABI. None = the current torch stream when torch
+    is loaded (so torch ops and renders are ordered), else HIP's null stream."""
     if stream is None:
+        import sys
+        torch = sys.modules.get("torch")
+        if torch is not None and torch.cuda.is_available() and torch.cuda.is_initialized():
+            return C.c_void_p(int(torch.cuda.current_stream().cuda_stream) or None)
         return None
     if isinstance(stream, int):
-        return C.c_void_p(stream)
-    return C.c_void_p(int(stream.cuda_stream))
+        return C.c_void_p(stream or None)
+    return C.c_void_p(int(stream.cuda_stream) or None)
 
 
 __all__ = ["DeviceScene", "RtmiError", "band_rows", "device_count", "initRenderer", "renderLine",
