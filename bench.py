@@ -152,7 +152,11 @@ def main():
                 unshard_bands_device(gathered, fb, W, H, BAND_H, world, stream=stream)
 
     # warmup (+ the deterministic per-frame ray counts)
-    st = ds.render_bands_device(opts, local_buf, BAND_H, rank, world, stream=stream, stats=True)
+    # one instrumented launch (RT_FLAG_COUNT_TRAVERSAL) for the traversal record counts
+    from rtmi.abi import RT_FLAG_COUNT_TRAVERSAL
+    import dataclasses
+    copts = dataclasses.replace(opts, flags=opts.flags | RT_FLAG_COUNT_TRAVERSAL)
+    st = ds.render_bands_device(copts, local_buf, BAND_H, rank, world, stream=stream, stats=True)
     counters = ds.last_counters()
     for _ in range(max(0, args.warmup)):
         step()

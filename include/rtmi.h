@@ -137,6 +137,9 @@ typedef struct rt_options {
  * identical; num_intersection_hits can then differ from the reference's
  * closest-hit count on scenes where several objects overlap one shadow ray. */
 #define RT_FLAG_ANYHIT_SHADOWS 0x1u
+/* Run the instrumented kernel that also counts BVH node / triangle record
+ * fetches (rt_scene_last_counters). Slower; the image and Stats are the same. */
+#define RT_FLAG_COUNT_TRAVERSAL 0x2u
 
 /* Stats (src/renderer/stats.nim:4-13) plus ray counts for Mray/s. */
 typedef struct rt_stats {
@@ -238,8 +241,8 @@ int rt_unshard_bands_device(const float *d_gathered, float *d_fb,
 int rt_band_rows(int32_t height, int32_t band_h, int32_t world,
                  int32_t *out_rows);
 
-/* Traversal counters of the last render call on this scene (synchronises
- * the scene's stream). */
+/* Traversal counters of the last render call on this scene (waits for it).
+ * Zero unless that call set RT_FLAG_COUNT_TRAVERSAL. */
 int rt_scene_last_counters(rt_scene *scene, rt_traversal_counters *out);
 
 /* ---- helpers ----------------------------------------------------------- */

@@ -15,7 +15,7 @@
 namespace rtmi {
 
 struct BvhBuildParams {
-  int max_leaf = 4;         // triangles per leaf, SAH may stop earlier
+  int max_leaf = kLeafMax;  // triangles per leaf, SAH may stop earlier
   int bins = 32;            // SAH bins per axis
   float cost_node = 1.0f;   // relative cost of one node fetch (two boxes)
   float cost_tri = 1.0f;    // relative cost of one triangle test

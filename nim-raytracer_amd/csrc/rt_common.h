@@ -18,8 +18,13 @@ namespace rtmi {
 
 enum : int32_t { GEOM_SPHERE = 0, GEOM_PLANE = 1, GEOM_BOX = 2, GEOM_MESH = 3 };
 enum : int32_t { LIGHT_DISTANT = 0, LIGHT_POINT = 1 };
+// DevObject.xf: what world_to_object is (host-classified, float32 fast paths)
+enum : int32_t { XF_IDENTITY = 0, XF_TRANSLATE = 1, XF_GENERAL = 2 };
+// RenderParams.flags bits
+enum : int32_t { RT_DEV_FLAG_ANYHIT = 0x1, RT_DEV_FLAG_COUNT = 0x2 };
 
 constexpr int kMaxBvhDepth = 60;      // stack fits one 64-lane VGPR
+constexpr int kLeafMax = 4;           // triangles per BVH leaf (arrays padded by kLeafMax-1)
 constexpr int kMaxShadeLevels = 8;    // primary + 7 reflection bounces
 constexpr int kStatSlots = 10;        // per-wave partial counters
 
@@ -32,7 +37,8 @@ struct alignas(16) DevObject {
   R albedo[4];   // rgb, reflection
   int32_t type;
   int32_t mesh;
-  int32_t pad0, pad1;
+  int32_t xf;          // XF_* classification of world_to_object
+  int32_t pad1;
 };
 
 template <class R>
@@ -121,6 +127,67 @@ struct RenderParams {
   long long ngroups;               // tiles_x * tiles_y
 };
 
+// ---- float32 performance-kernel records (rt_fast.h) -------------------------
+// One 64-byte hot record per object: everything trace() needs, one s_load.
+struct alignas(16) FObj {
+  int32_t type, xf, mesh, pad0;
+  float t[3];     // world_to_object translation (XF_TRANSLATE)
+  float r;        // sphere radius
+  float lo[3];    // box vmin
+  float pad1;
+  float hi[3];    // box vmax
+  float pad2;
+};
+static_assert(sizeof(FObj) == 64, "FObj must be 64 bytes");
+
+// Shading data and the general transform, read only when needed.
+struct alignas(16) FObjX {
+  float w2o[12];     // world_to_object rows 0..2, column-major: w2o[c*3 + r]
+  float o2w[9];      // object_to_world 3x3 (normals, not re-normalised)
+  float albedo_pi[3];// albedo / PI (shader.nim:17)
+  float refl;        // Material.reflection
+  int32_t normal_base;
+  int32_t pad[6];
+};
+static_assert(sizeof(FObjX) == 128, "FObjX must be 128 bytes");
+
+struct alignas(16) FMesh {
+  float lo[3];
+  int32_t root;
+  float hi[3];
+  int32_t normal_base;
+};
+
+struct alignas(16) FLight {
+  int32_t type;
+  float ci[3];   // color * intensity
+  float v[3];    // dir (distant) / pos (point)
+  float pad;
+};
+
+struct FastParams {
+  const FObj* objs;
+  const FObjX* objx;
+  const FMesh* meshes;
+  const FLight* lights;
+  const BvhNode* nodes;
+  const TriF32* tris;
+  const float* normals;
+  float* fb;
+  unsigned long long* partials;
+  float cam[12];       // origin, C2W column 0, 1, 2 (xyz each)
+  float cam_a, cam_b;  // cx = (px - cam_b) * cam_a, cam_b = w/2   (renderer.nim:39)
+  float cam_c, cam_d;  // cy = (cam_d - py) * cam_c, cam_d = h/2   (renderer.nim:40)
+  float bg[3];
+  float bias;
+  float inv_len;
+  float sample_step, sample_off;
+  int32_t nobj, nlight, width, height;
+  int32_t aa_kind, grid_m, spp, max_depth, flags, max_iters;
+  int32_t mode, y0, nrows, ncols, step, max_step, band_h, rank, world;
+  int32_t lanes_per_px, log2_lanes, tile_x, tile_y, tiles_x, ngroups;
+};
+
 enum : int32_t {
   STAT_PRIMARY = 0, STAT_TESTS = 1, STAT_HITS = 2, STAT_SHADOW = 3, STAT_REFL = 4,
   STAT_NODE_FETCH = 5, STAT_TRI_FETCH = 6, STAT_LANE_NODES = 7, STAT_LANE_TRIS = 8
@@ -130,7 +197,7 @@ enum : int32_t {
 
 // Launchers implemented by the precision-specific translation units.
 extern "C" {
-int rtmi_launch_render_f32(const rtmi::RenderParams<float>* p, int blocks, void* stream);
+int rtmi_launch_render_f32(const rtmi::FastParams* p, int blocks, void* stream);
 int rtmi_launch_render_f64(const rtmi::RenderParams<double>* p, int blocks, void* stream);
 int rtmi_launch_reduce_stats(const unsigned long long* partials, int num_waves,
                              unsigned long long* acc, void* stream);

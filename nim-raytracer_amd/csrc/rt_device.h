@@ -23,7 +23,13 @@
 
 #include "rt_common.h"
 
-#define RT_CONST __attribute__((address_space(4)))
+#ifndef RT_CONST
+#if defined(__HIP_DEVICE_COMPILE__)
+#define RT_CONST __attribute__((address_space(4)))  // scalar (constant) loads
+#else
+#define RT_CONST
+#endif
+#endif
 
 namespace rtmi {
 
@@ -111,9 +117,13 @@ __device__ __forceinline__ unsigned long long popc(unsigned long long m) {
   return (unsigned long long)__popcll(m);
 }
 
+// Wave-uniform 32-bit counters (SGPRs), flushed per pixel group into a
+// per-lane 64-bit total (lane k holds slot k). Traversal counters (node /
+// triangle fetches) are only kept by the instrumented kernel (COUNT).
 struct WaveStats {
-  unsigned long long v[kStatSlots];
+  unsigned int v[kStatSlots];
 };
+__device__ __forceinline__ unsigned int popc32(unsigned long long m) { return (unsigned int)__popcll(m); }
 
 // ---- primitive intersections (object space) -------------------------------
 // Object-space ray as initRay builds it (geom.nim:41-48).
@@ -134,6 +144,16 @@ __device__ __forceinline__ ORay<R> init_oray(V3<R> o, V3<R> d) {
 // AABB.intersect (geom.nim:76-96), returns tmin or -inf.
 template <class R>
 __device__ __forceinline__ R aabb_ref(V3<R> lo, V3<R> hi, const ORay<R>& r) {
+  if constexpr (!Prec<R>::exact) {
+    // same test with IEEE min/max instead of the sign-indexed bounds (equal
+    // except for NaN slabs, whose Nim semantics only the float64 mode keeps)
+    const float ax = (lo.x - r.o.x) * r.inv.x, bx = (hi.x - r.o.x) * r.inv.x;
+    const float ay = (lo.y - r.o.y) * r.inv.y, by = (hi.y - r.o.y) * r.inv.y;
+    const float az = (lo.z - r.o.z) * r.inv.z, bz = (hi.z - r.o.z) * r.inv.z;
+    const float tmin = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
+    const float tmax = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz)) * Prec<R>::aabb_tmax_scale;
+    return tmin <= tmax ? tmin : -pinf<R>();
+  }
   const bool sx = r.inv.x < R(0), sy = r.inv.y < R(0), sz = r.inv.z < R(0);
   const R txmin = ((sx ? hi.x : lo.x) - r.o.x) * r.inv.x;
   const R txmax = ((sx ? lo.x : hi.x) - r.o.x) * r.inv.x;
@@ -237,14 +257,15 @@ __device__ __forceinline__ void slab2(const RT_CONST BvhNode& nd, V3<R> o, V3<R>
   }
 }
 
-template <class R>
+template <class R, bool COUNT>
 __device__ __forceinline__ void leaf(const RenderParams<R>& p, int first, int count, bool h,
                                      V3<R> o, V3<R> d, R& tbest, int& best_id, bool& active,
                                      bool anyhit, WaveStats& ws) {
   using Tri = typename TriOf<R>::type;
-  const unsigned long long m = ballot(h);
-  ws.v[STAT_TRI_FETCH] += (unsigned long long)count;
-  ws.v[STAT_LANE_TRIS] += popc(m) * (unsigned long long)count;
+  if constexpr (COUNT) {
+    ws.v[STAT_TRI_FETCH] += (unsigned int)count;
+    ws.v[STAT_LANE_TRIS] += popc32(ballot(h)) * (unsigned int)count;
+  }
   for (int k = 0; k < count; ++k) {
     const RT_CONST Tri& tri = cptr(p.tris)[first + k];
     const R t = tri_ref<R>(tri, o, d);
@@ -258,7 +279,7 @@ __device__ __forceinline__ void leaf(const RenderParams<R>& p, int first, int co
   if (anyhit) active = active && best_id < 0;
 }
 
-template <class R>
+template <class R, bool COUNT>
 __device__ __forceinline__ void traverse(const RenderParams<R>& p, int root, V3<R> o, V3<R> d,
                                          bool active, bool anyhit, R& tbest, int& best_id,
                                          WaveStats& ws) {
@@ -282,9 +303,10 @@ __device__ __forceinline__ void traverse(const RenderParams<R>& p, int root, V3<
   int node = root;
   for (int iter = 0; iter < p.max_iters; ++iter) {
     const RT_CONST BvhNode& nd = cptr(p.nodes)[node];
-    const unsigned long long live = ballot(active);
-    ws.v[STAT_NODE_FETCH] += 1ull;
-    ws.v[STAT_LANE_NODES] += popc(live);
+    if constexpr (COUNT) {
+      ws.v[STAT_NODE_FETCH] += 1u;
+      ws.v[STAT_LANE_NODES] += popc32(ballot(active));
+    }
     bool h0, h1;
     R tn0, tn1;
     slab2<R>(nd, o, ninv, oi, tbest, active, h0, h1, tn0, tn1);
@@ -293,11 +315,11 @@ __device__ __forceinline__ void traverse(const RenderParams<R>& p, int root, V3<
     unsigned long long m0 = (n0 > 0 || c0 >= 0) ? ballot(h0) : 0ull;
     unsigned long long m1 = (n1 > 0 || c1 >= 0) ? ballot(h1) : 0ull;
     if (n0 > 0 && m0) {
-      leaf<R>(p, c0, n0, h0, o, d, tbest, best_id, active, anyhit, ws);
+      leaf<R, COUNT>(p, c0, n0, h0, o, d, tbest, best_id, active, anyhit, ws);
       m0 = 0;
     }
     if (n1 > 0 && m1) {
-      leaf<R>(p, c1, n1, h1, o, d, tbest, best_id, active, anyhit, ws);
+      leaf<R, COUNT>(p, c1, n1, h1, o, d, tbest, best_id, active, anyhit, ws);
       m1 = 0;
     }
     if (anyhit && ballot(active) == 0ull) break;
@@ -330,27 +352,55 @@ struct Hit {
   R t;
 };
 
+// World -> object space for one object. float32 mode takes the identity /
+// translation shortcuts the host classified (DevObject.xf); float64 mode
+// always multiplies the full matrix so every rounding matches the oracle.
+template <class R>
+__device__ __forceinline__ void to_object(const RT_CONST DevObject<R>& ob, V3<R> o, V3<R> d, V3<R>& ro,
+                                          V3<R>& rd) {
+  if constexpr (!Prec<R>::exact) {
+    const int xf = ob.xf;
+    if (xf == XF_IDENTITY) {
+      ro = o;
+      rd = d;
+      return;
+    }
+    if (xf == XF_TRANSLATE) {
+      ro = V3<R>{o.x + ob.w2o[12], o.y + ob.w2o[13], o.z + ob.w2o[14]};
+      rd = d;
+      return;
+    }
+  }
+  ro = xform<R>(ob.w2o, o, R(1));
+  rd = xform<R>(ob.w2o, d, R(0));
+}
+
 // Linear closest hit over the scene's objects in order, for lanes with
 // `active`; tmin starts at t_near. Wave-uniform control flow only.
-template <class R>
+template <class R, bool COUNT>
 __device__ __forceinline__ Hit<R> trace(const RenderParams<R>& p, V3<R> o, V3<R> d, R t_near,
                                         bool active, bool anyhit, WaveStats& ws) {
   Hit<R> h{-1, -1, t_near};
-  const unsigned long long live = ballot(active);
-  ws.v[STAT_TESTS] += popc(live) * (unsigned long long)p.nobj;
+  ws.v[STAT_TESTS] += popc32(ballot(active)) * (unsigned int)p.nobj;
   for (int i = 0; i < p.nobj; ++i) {
     const RT_CONST DevObject<R>& ob = cptr(p.objects)[i];
     const int type = ob.type;
-    const ORay<R> r = init_oray<R>(xform<R>(ob.w2o, o, R(1)), xform<R>(ob.w2o, d, R(0)));
+    V3<R> ro, rd;
+    to_object<R>(ob, o, d, ro, rd);
+    ORay<R> r;
+    r.o = ro;
+    r.d = rd;
     R t;
     int tri = -1;
-    if (type == GEOM_SPHERE) {
-      t = sphere_ref<R>(ob.prm[0], r);
-    } else if (type == GEOM_PLANE) {
+    if (type == GEOM_PLANE) {
       t = plane_ref<R>(r);
+    } else if (type == GEOM_SPHERE) {
+      t = sphere_ref<R>(ob.prm[0], r);
     } else if (type == GEOM_BOX) {
+      r.inv = V3<R>{Prec<R>::rcp(rd.x), Prec<R>::rcp(rd.y), Prec<R>::rcp(rd.z)};
       t = aabb_ref<R>(V3<R>{ob.prm[0], ob.prm[1], ob.prm[2]}, V3<R>{ob.prm[4], ob.prm[5], ob.prm[6]}, r);
     } else if (type == GEOM_MESH) {
+      r.inv = V3<R>{Prec<R>::rcp(rd.x), Prec<R>::rcp(rd.y), Prec<R>::rcp(rd.z)};
       const RT_CONST DevMesh<R>& m = cptr(p.meshes)[ob.mesh];
       // TriangleMesh.intersect (geom.nim:339-358): AABB gate (tmin < 0 ->
       // miss, so rays starting inside the box miss), then closest face.
@@ -358,14 +408,14 @@ __device__ __forceinline__ Hit<R> trace(const RenderParams<R>& p, V3<R> o, V3<R>
       const bool in = active && gate >= R(0);
       R tb = h.t;
       int best = -1;
-      traverse<R>(p, m.root, r.o, r.d, in, anyhit, tb, best, ws);
+      traverse<R, COUNT>(p, m.root, r.o, r.d, in, anyhit, tb, best, ws);
       t = !(gate >= R(0)) ? -pinf<R>() : (best >= 0 ? tb : pinf<R>());
       tri = best;
     } else {
       t = -pinf<R>();
     }
     const bool upd = active && t >= R(0) && t < h.t;
-    ws.v[STAT_HITS] += popc(ballot(upd));
+    ws.v[STAT_HITS] += popc32(ballot(upd));
     if (upd) {
       h.t = t;
       h.obj = i;
@@ -376,8 +426,9 @@ __device__ __forceinline__ Hit<R> trace(const RenderParams<R>& p, V3<R> o, V3<R>
 }
 
 // ---- shade (renderer.nim:71-127) -------------------------------------------
+// normal(*) (geom.nim:361-379) for analytic geometry in object space.
 template <class R>
-__device__ __forceinline__ V3<R> object_normal(const DevObject<R>& ob, int type, V3<R> ho) {
+__device__ __forceinline__ V3<R> object_normal(const RT_CONST DevObject<R>& ob, int type, V3<R> ho) {
   if (type == GEOM_SPHERE) return normalize_dir<R>(ho);            // geom.nim:364-365
   if (type == GEOM_PLANE) return V3<R>{R(0), R(1), R(0)};          // geom.nim:367-368
   if (type == GEOM_BOX) {                                          // geom.nim:370-379
@@ -408,10 +459,10 @@ __device__ __forceinline__ V3<R> object_normal(const DevObject<R>& ob, int type,
 
 // One camera sample: trace + shade with the reflection recursion unrolled
 // into a loop of levels. Returns the sample colour (renderer.nim:71-127).
-template <class R>
+template <class R, bool COUNT>
 __device__ __forceinline__ V3<R> shade_path(const RenderParams<R>& p, V3<R> o, V3<R> d, bool active,
                                             WaveStats& ws) {
-  const bool anyhit_shadows = (p.flags & 0x1) != 0;
+  const bool anyhit_shadows = (p.flags & RT_DEV_FLAG_ANYHIT) != 0;
   constexpr R kPi = R(3.14159265358979323846);
   bool act = active;
   int depth = 1;
@@ -420,28 +471,52 @@ __device__ __forceinline__ V3<R> shade_path(const RenderParams<R>& p, V3<R> o, V
   // (1 - r)*L + r*inner folded from the innermost level outwards.
   V3<R> facc{R(0), R(0), R(0)};
   R fw = R(1);
-  V3<R> lvl_c[kMaxShadeLevels];
-  R lvl_r[kMaxShadeLevels];
+  V3<R> lvl_c[Prec<R>::exact ? kMaxShadeLevels : 1];
+  R lvl_r[Prec<R>::exact ? kMaxShadeLevels : 1];
   int nlev = 0;
   for (int lev = 0; lev < kMaxShadeLevels; ++lev) {
     if (ballot(act) == 0ull) break;
-    const Hit<R> hit = trace<R>(p, o, d, pinf<R>(), act, false, ws);
-    const bool miss = act && hit.obj < 0;
-    if (miss) terminal = V3<R>{p.bg[0], p.bg[1], p.bg[2]};
+    const Hit<R> hit = trace<R, COUNT>(p, o, d, pinf<R>(), act, false, ws);
+    if (act && hit.obj < 0) terminal = V3<R>{p.bg[0], p.bg[1], p.bg[2]};
     const bool lit = act && hit.obj >= 0;
-    const int oi = lit ? hit.obj : 0;
-    const DevObject<R>& ob = p.objects[oi];
-    const int type = ob.type;
     const V3<R> hw{o.x + d.x * hit.t, o.y + d.y * hit.t, o.z + d.z * hit.t};
-    const V3<R> ho = xform<R>(ob.w2o, hw, R(1));
-    V3<R> nrm;
-    if (hit.tri >= 0) {
-      const R* fn = p.normals + 3 * (size_t)(p.meshes[ob.mesh].normal_base + hit.tri);
-      nrm = V3<R>{fn[0], fn[1], fn[2]};
-    } else {
-      nrm = object_normal<R>(ob, type, ho);
+    // Gather the per-object shading inputs with one wave-uniform pass per
+    // distinct object hit by the wave (usually one), so the object record is
+    // read with scalar loads.
+    V3<R> N{R(0), R(0), R(0)};
+    V3<R> alb{R(0), R(0), R(0)};
+    R refl = R(0);
+    unsigned long long pending = ballot(lit);
+    while (pending) {
+      const int lead = (int)__builtin_ctzll(pending);
+      const int oi = __builtin_amdgcn_readlane(hit.obj, lead);
+      const bool mine = lit && hit.obj == oi;
+      pending &= ~ballot(mine);
+      const RT_CONST DevObject<R>& ob = cptr(p.objects)[oi];
+      if (mine) {
+        V3<R> nrm;
+        if (hit.tri >= 0) {
+          const R* fn = p.normals + 3 * (size_t)(cptr(p.meshes)[ob.mesh].normal_base + hit.tri);
+          nrm = V3<R>{fn[0], fn[1], fn[2]};
+        } else {
+          V3<R> ho;
+          if constexpr (!Prec<R>::exact) {
+            V3<R> dummy;
+            to_object<R>(ob, hw, V3<R>{R(0), R(0), R(0)}, ho, dummy);
+          } else {
+            ho = xform<R>(ob.w2o, hw, R(1));
+          }
+          nrm = object_normal<R>(ob, ob.type, ho);
+        }
+        if constexpr (!Prec<R>::exact) {
+          N = ob.xf == XF_GENERAL ? xform<R>(ob.o2w, nrm, R(0)) : nrm;
+        } else {
+          N = xform<R>(ob.o2w, nrm, R(0));
+        }
+        alb = V3<R>{ob.albedo[0], ob.albedo[1], ob.albedo[2]};
+        refl = ob.albedo[3];
+      }
     }
-    const V3<R> N = xform<R>(ob.o2w, nrm, R(0));
     V3<R> local{R(0), R(0), R(0)};
     for (int li = 0; li < p.nlight; ++li) {
       const RT_CONST DevLight<R>& L = cptr(p.lights)[li];
@@ -462,21 +537,20 @@ __device__ __forceinline__ V3<R> shade_path(const RenderParams<R>& p, V3<R> o, V
       }
       const V3<R> sd{ldir.x * R(-1), ldir.y * R(-1), ldir.z * R(-1)};
       const V3<R> so{hw.x + N.x * p.bias, hw.y + N.y * p.bias, hw.z + N.z * p.bias};
-      ws.v[STAT_SHADOW] += popc(ballot(lit));
-      const Hit<R> sh = trace<R>(p, so, sd, dist, lit, anyhit_shadows, ws);
+      ws.v[STAT_SHADOW] += popc32(ballot(lit));
+      const Hit<R> sh = trace<R, COUNT>(p, so, sd, dist, lit, anyhit_shadows, ws);
       if (lit && sh.obj < 0) {  // shadeDiffuse (shader.nim:12-17)
         const R ndl = nmax(R(0), dot4(N, R(0), sd, R(0) * R(-1)));
-        local.x = local.x + Prec<R>::div(ob.albedo[0], kPi) * I.x * ndl;
-        local.y = local.y + Prec<R>::div(ob.albedo[1], kPi) * I.y * ndl;
-        local.z = local.z + Prec<R>::div(ob.albedo[2], kPi) * I.z * ndl;
+        local.x = local.x + Prec<R>::div(alb.x, kPi) * I.x * ndl;
+        local.y = local.y + Prec<R>::div(alb.y, kPi) * I.y * ndl;
+        local.z = local.z + Prec<R>::div(alb.z, kPi) * I.z * ndl;
       }
     }
-    const R refl = ob.albedo[3];
     const bool reflect = lit && refl > R(0) && depth <= p.max_depth;
     if (lit && !reflect) terminal = local;
     if constexpr (Prec<R>::exact) {
       if (reflect) {
-        // shift-register push (static indices keep it in VGPRs)
+        // shift-register push (static indices keep it in registers)
 #pragma unroll
         for (int k = kMaxShadeLevels - 1; k > 0; --k) {
           lvl_c[k] = lvl_c[k - 1];
@@ -493,7 +567,7 @@ __device__ __forceinline__ V3<R> shade_path(const RenderParams<R>& p, V3<R> o, V
         fw = fw * refl;
       }
     }
-    ws.v[STAT_REFL] += popc(ballot(reflect));
+    ws.v[STAT_REFL] += popc32(ballot(reflect));
     if (reflect) {
       // renderer.nim:109-118
       const R ndi = R(2) * dot4(N, R(0), d, R(0));
@@ -516,13 +590,28 @@ __device__ __forceinline__ V3<R> shade_path(const RenderParams<R>& p, V3<R> o, V
     }
     return c;
   } else {
+    (void)lvl_c;
+    (void)lvl_r;
+    (void)nlev;
     return V3<R>{facc.x + fw * terminal.x, facc.y + fw * terminal.y, facc.z + fw * terminal.z};
   }
 }
 
+// Move the wave's 32-bit counters into the per-lane 64-bit totals.
+__device__ __forceinline__ void flush_stats(WaveStats& ws, unsigned long long& tot, int lane) {
+#pragma unroll
+  for (int k = 0; k < kStatSlots; ++k) {
+    tot += (lane == k) ? (unsigned long long)ws.v[k] : 0ull;
+    ws.v[k] = 0u;
+  }
+}
+
 // ---- the render kernel -----------------------------------------------------
-template <class R>
-__global__ __launch_bounds__(256) void k_render(const RenderParams<R> p) {
+#ifndef RTMI_MIN_WAVES
+#define RTMI_MIN_WAVES 1
+#endif
+template <class R, bool COUNT>
+__global__ __launch_bounds__(256, RTMI_MIN_WAVES) void k_render(const RenderParams<R> p) {
   const int lane = (int)__lane_id();
   const long long wave = (long long)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   const long long nwaves = (long long)gridDim.x * (blockDim.x >> 6);
@@ -534,7 +623,8 @@ __global__ __launch_bounds__(256) void k_render(const RenderParams<R> p) {
   const bool grid_aa = p.aa_kind != 0;
   WaveStats ws;
 #pragma unroll
-  for (int k = 0; k < kStatSlots; ++k) ws.v[k] = 0ull;
+  for (int k = 0; k < kStatSlots; ++k) ws.v[k] = 0u;
+  unsigned long long tot = 0ull;
 
   for (long long g = wave; g < p.ngroups; g += nwaves) {
     const int gx = (int)(g % p.tiles_x), gy = (int)(g / p.tiles_x);
@@ -572,8 +662,8 @@ __global__ __launch_bounds__(256) void k_render(const RenderParams<R> p) {
       const V3<R> dn = normalize_dir<R>(V3<R>{cx, cy, R(-1)});
       const V3<R> o = xform<R>(p.c2w, V3<R>{R(0), R(0), R(0)}, R(1));
       const V3<R> d = xform<R>(p.c2w, dn, R(0));
-      ws.v[STAT_PRIMARY] += popc(ballot(sv));
-      const V3<R> c = shade_path<R>(p, o, d, sv, ws);
+      ws.v[STAT_PRIMARY] += popc32(ballot(sv));
+      const V3<R> c = shade_path<R, COUNT>(p, o, d, sv, ws);
       if (sv) {
         if (grid_aa) {
           acc = V3<R>{acc.x + c.x, acc.y + c.y, acc.z + c.z};
@@ -581,7 +671,9 @@ __global__ __launch_bounds__(256) void k_render(const RenderParams<R> p) {
           acc = c;
         }
       }
+      if ((it & 63) == 63) flush_stats(ws, tot, lane);
     }
+    flush_stats(ws, tot, lane);
     // sum the L lanes of each pixel (exact mode launches with L = 1)
     for (int off = 1; off < L; off <<= 1) {
       acc.x += __shfl_xor(acc.x, off);
@@ -604,12 +696,7 @@ __global__ __launch_bounds__(256) void k_render(const RenderParams<R> p) {
       }
     }
   }
-  if (lane < kStatSlots) {
-    unsigned long long v = 0ull;
-#pragma unroll
-    for (int k = 0; k < kStatSlots; ++k) v = (lane == k) ? ws.v[k] : v;
-    p.partials[wave * kStatSlots + lane] = v;
-  }
+  if (lane < kStatSlots) p.partials[wave * kStatSlots + lane] = tot;
 }
 
 }  // namespace rtmi

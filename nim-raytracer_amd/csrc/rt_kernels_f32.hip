@@ -1,7 +1,7 @@
 // rt_kernels_f32.hip — float (performance mode) instantiation of the render
 // kernel, plus the precision-independent helper kernels (stats reduction,
 // multi-GPU band un-interleave). Built with FMA contraction on.
-#include "rt_device.h"
+#include "rt_fast.h"
 
 namespace rtmi {
 
@@ -51,12 +51,16 @@ __global__ __launch_bounds__(256) void k_unshard_scalar(const float* __restrict_
   for (int i = threadIdx.x; i < row_f; i += blockDim.x) fb[(size_t)y * row_f + i] = gathered[src_row * row_f + i];
 }
 
-template __global__ void k_render<float>(const RenderParams<float>);
+template __global__ void fast::k_render_fast<false>(const FastParams);
+template __global__ void fast::k_render_fast<true>(const FastParams);
 
 }  // namespace rtmi
 
-extern "C" int rtmi_launch_render_f32(const rtmi::RenderParams<float>* p, int blocks, void* stream) {
-  hipLaunchKernelGGL(rtmi::k_render<float>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, *p);
+extern "C" int rtmi_launch_render_f32(const rtmi::FastParams* p, int blocks, void* stream) {
+  if (p->flags & rtmi::RT_DEV_FLAG_COUNT)
+    hipLaunchKernelGGL((rtmi::fast::k_render_fast<true>), dim3(blocks), dim3(256), 0, (hipStream_t)stream, *p);
+  else
+    hipLaunchKernelGGL((rtmi::fast::k_render_fast<false>), dim3(blocks), dim3(256), 0, (hipStream_t)stream, *p);
   return (int)hipGetLastError();
 }
 

@@ -4,10 +4,14 @@
 #include "rt_device.h"
 
 namespace rtmi {
-template __global__ void k_render<double>(const RenderParams<double>);
+template __global__ void k_render<double, false>(const RenderParams<double>);
+template __global__ void k_render<double, true>(const RenderParams<double>);
 }
 
 extern "C" int rtmi_launch_render_f64(const rtmi::RenderParams<double>* p, int blocks, void* stream) {
-  hipLaunchKernelGGL(rtmi::k_render<double>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, *p);
+  if (p->flags & rtmi::RT_DEV_FLAG_COUNT)
+    hipLaunchKernelGGL((rtmi::k_render<double, true>), dim3(blocks), dim3(256), 0, (hipStream_t)stream, *p);
+  else
+    hipLaunchKernelGGL((rtmi::k_render<double, false>), dim3(blocks), dim3(256), 0, (hipStream_t)stream, *p);
   return (int)hipGetLastError();
 }

@@ -93,6 +93,26 @@ struct PrecisionData {
   }
 };
 
+struct FastData {
+  DevBuf<FObj> objs;
+  DevBuf<FObjX> objx;
+  DevBuf<FMesh> meshes;
+  DevBuf<FLight> lights;
+  DevBuf<TriF32> tris;
+  DevBuf<float> normals;
+  void release() {
+    objs.release();
+    objx.release();
+    meshes.release();
+    lights.release();
+    tris.release();
+    normals.release();
+  }
+  size_t bytes() const {
+    return objs.bytes() + objx.bytes() + meshes.bytes() + lights.bytes() + tris.bytes() + normals.bytes();
+  }
+};
+
 bool is_pow2(int v) { return v > 0 && (v & (v - 1)) == 0; }
 
 int device_of_current() {
@@ -114,7 +134,7 @@ struct rt_scene {
   double fov = 50.0;
   double c2w[16];
   double bg[3];
-  PrecisionData<float> f32;
+  FastData f32;
   PrecisionData<double> f64;
   DevBuf<BvhNode> nodes;
   DevBuf<unsigned long long> partials;
@@ -256,6 +276,21 @@ namespace {
 
 bool affine(const double* m) { return m[3] == 0.0 && m[7] == 0.0 && m[11] == 0.0 && m[15] == 1.0; }
 
+// Identity / pure translation / general (float32 fast paths, DevObject.xf).
+// Translation requires BOTH matrices to have an identity 3x3 block, so the
+// normal transform (object_to_world * n) is the identity too.
+int32_t classify_xf(const double* w2o, const double* o2w) {
+  bool lin_id = true;
+  for (int c = 0; c < 3; ++c)
+    for (int r = 0; r < 3; ++r) {
+      const double id = c == r ? 1.0 : 0.0;
+      if (w2o[c * 4 + r] != id || o2w[c * 4 + r] != id) lin_id = false;
+    }
+  if (!lin_id) return XF_GENERAL;
+  if (w2o[12] == 0.0 && w2o[13] == 0.0 && w2o[14] == 0.0) return XF_IDENTITY;
+  return XF_TRANSLATE;
+}
+
 template <class R>
 void fill_precision(const rt_scene_desc* d, const std::vector<std::vector<double>>& normals,
                     const std::vector<BvhResult>& bvhs, const std::vector<int32_t>& node_base,
@@ -280,6 +315,7 @@ void fill_precision(const rt_scene_desc* d, const std::vector<std::vector<double
     o.albedo[3] = (R)s.reflection;
     o.type = s.type;
     o.mesh = s.type == RT_MESH ? s.mesh : 0;
+    o.xf = classify_xf(s.world_to_object, s.object_to_world);
   }
   lights.assign((size_t)d->num_lights, DevLight<R>{});
   for (int i = 0; i < d->num_lights; ++i) {
@@ -322,6 +358,59 @@ void fill_precision(const rt_scene_desc* d, const std::vector<std::vector<double
     }
     for (double x : normals[(size_t)m]) nrm.push_back((R)x);
     normal_base += (int32_t)md.num_faces;
+  }
+  // pad so a kernel may read kLeafMax records from any leaf start
+  for (int k = 0; k < kLeafMax - 1; ++k) {
+    typename TriOf<R>::type t{};
+    t.id = -1;
+    tris.push_back(t);
+  }
+}
+
+// float32 kernel records (rt_common.h FObj/FObjX/FMesh/FLight).
+void fill_fast_records(const rt_scene_desc* d, const std::vector<DevMesh<float>>& dm, std::vector<FObj>& fo,
+                       std::vector<FObjX>& fx, std::vector<FMesh>& fm, std::vector<FLight>& fl) {
+  const double kPi = 3.14159265358979323846;
+  fo.assign((size_t)d->num_objects, FObj{});
+  fx.assign((size_t)d->num_objects, FObjX{});
+  for (int i = 0; i < d->num_objects; ++i) {
+    const rt_object_desc& s = d->objects[i];
+    FObj& o = fo[(size_t)i];
+    FObjX& x = fx[(size_t)i];
+    o.type = s.type;
+    o.xf = classify_xf(s.world_to_object, s.object_to_world);
+    o.mesh = s.type == RT_MESH ? s.mesh : 0;
+    for (int k = 0; k < 3; ++k) {
+      o.t[k] = (float)s.world_to_object[12 + k];
+      o.lo[k] = (float)s.box_min[k];
+      o.hi[k] = (float)s.box_max[k];
+    }
+    o.r = (float)s.radius;
+    for (int c = 0; c < 4; ++c)
+      for (int r = 0; r < 3; ++r) x.w2o[c * 3 + r] = (float)s.world_to_object[c * 4 + r];
+    for (int c = 0; c < 3; ++c)
+      for (int r = 0; r < 3; ++r) x.o2w[c * 3 + r] = (float)s.object_to_world[c * 4 + r];
+    for (int k = 0; k < 3; ++k) x.albedo_pi[k] = (float)(s.albedo[k] / kPi);
+    x.refl = (float)s.reflection;
+    x.normal_base = s.type == RT_MESH ? dm[(size_t)s.mesh].normal_base : 0;
+  }
+  fm.assign(dm.size(), FMesh{});
+  for (size_t m = 0; m < dm.size(); ++m) {
+    for (int k = 0; k < 3; ++k) {
+      fm[m].lo[k] = dm[m].lo[k];
+      fm[m].hi[k] = dm[m].hi[k];
+    }
+    fm[m].root = dm[m].root;
+    fm[m].normal_base = dm[m].normal_base;
+  }
+  fl.assign((size_t)d->num_lights, FLight{});
+  for (int i = 0; i < d->num_lights; ++i) {
+    const rt_light_desc& s = d->lights[i];
+    fl[(size_t)i].type = s.type == RT_POINT_LIGHT ? LIGHT_POINT : LIGHT_DISTANT;
+    for (int k = 0; k < 3; ++k) {
+      fl[(size_t)i].ci[k] = (float)(s.color[k] * s.intensity);
+      fl[(size_t)i].v[k] = (float)(s.type == RT_POINT_LIGHT ? s.pos[k] : s.dir[k]);
+    }
   }
 }
 
@@ -439,9 +528,14 @@ extern "C" int rt_scene_create(const rt_scene_desc* d, rt_scene** out_scene) {
     std::vector<TriF32> t;
     std::vector<float> n;
     fill_precision<float>(d, normals, bvhs, node_base, aabbs, o, l, m, t, n);
+    std::vector<FObj> fo;
+    std::vector<FObjX> fx;
+    std::vector<FMesh> fm;
+    std::vector<FLight> fl;
+    fill_fast_records(d, m, fo, fx, fm, fl);
     int rc;
-    if ((rc = s->f32.objects.upload(o)) || (rc = s->f32.lights.upload(l)) || (rc = s->f32.meshes.upload(m)) ||
-        (rc = s->f32.tris.upload(t)) || (rc = s->f32.normals.upload(n)))
+    if ((rc = s->f32.objs.upload(fo)) || (rc = s->f32.objx.upload(fx)) || (rc = s->f32.meshes.upload(fm)) ||
+        (rc = s->f32.lights.upload(fl)) || (rc = s->f32.tris.upload(t)) || (rc = s->f32.normals.upload(n)))
       return rc;
   }
   {
@@ -517,6 +611,106 @@ int check_options(const rt_scene* s, const rt_options* o) {
     return fail(RT_E_UNSUPPORTED, "max_ray_depth %d > %d with reflective materials", o->max_ray_depth,
                 kMaxShadeLevels - 1);
   return RT_OK;
+}
+
+// Lanes per pixel (L), pixels per wave tile, number of wave groups, grid.
+struct Plan {
+  int L, log2L, tx, ty, tiles_x, ngroups, blocks;
+};
+
+Plan plan_mapping(const rt_scene* s, const rt_options* o, const Mapping& mp, int spp) {
+  Plan pl{};
+  // float64 parity mode keeps the reference's sequential sample sum (one
+  // lane per pixel); float32 spreads a pixel's samples over up to 64 lanes.
+  int L = 1, lg = 0;
+  if (o->precision == RT_FP32) {
+    while (L * 2 <= std::min(spp, 64)) {
+      L *= 2;
+      ++lg;
+    }
+  }
+  const int P = 64 / L;
+  int tx = 1, ty = 1;
+  switch (P) {
+    case 64: tx = 8; ty = 8; break;
+    case 32: tx = 8; ty = 4; break;
+    case 16: tx = 4; ty = 4; break;
+    case 8: tx = 4; ty = 2; break;
+    case 4: tx = 2; ty = 2; break;
+    case 2: tx = 2; ty = 1; break;
+    default: tx = 1; ty = 1; break;
+  }
+  pl.L = L;
+  pl.log2L = lg;
+  pl.tx = tx;
+  pl.ty = ty;
+  pl.tiles_x = (mp.ncols + tx - 1) / tx;
+  const long long tiles_y = (mp.nrows + ty - 1) / ty;
+  const long long ng = (long long)pl.tiles_x * tiles_y;
+  pl.ngroups = (int)std::min<long long>(ng, INT32_MAX);
+  const long long want = (ng + 3) / 4;
+  pl.blocks = (int)std::max(1LL, std::min<long long>(want, s->max_waves / 4));
+  return pl;
+}
+
+void fill_fast(rt_scene* s, const rt_options* o, const Mapping& mp, float* fb, FastParams& p, int* blocks) {
+  std::memset(&p, 0, sizeof p);
+  p.objs = s->f32.objs.p;
+  p.objx = s->f32.objx.p;
+  p.meshes = s->f32.meshes.p;
+  p.lights = s->f32.lights.p;
+  p.nodes = s->nodes.p;
+  p.tris = s->f32.tris.p;
+  p.normals = s->f32.normals.p;
+  p.fb = fb;
+  p.partials = s->partials.p;
+  // camera: origin = C2W * (0,0,0,1) = column 3; dir = C2W * normalize(cx, cy, -1, 0)
+  for (int k = 0; k < 3; ++k) {
+    p.cam[k] = (float)s->c2w[12 + k];
+    p.cam[3 + k] = (float)s->c2w[0 + k];
+    p.cam[6 + k] = (float)s->c2w[4 + k];
+    p.cam[9 + k] = (float)s->c2w[8 + k];
+  }
+  const double f = std::tan(s->fov * (3.14159265358979323846 / 180.0) / 2);
+  const double r = (double)o->width / (double)o->height;
+  p.cam_a = (float)(2.0 * r * f / (double)o->width);  // cx = ((2 x r)/w - r) f = (x - w/2) 2rf/w
+  p.cam_b = (float)(0.5 * (double)o->width);
+  p.cam_c = (float)(2.0 * f / (double)o->height);     // cy = (1 - 2y/h) f = (h/2 - y) 2f/h
+  p.cam_d = (float)(0.5 * (double)o->height);
+  for (int k = 0; k < 3; ++k) p.bg[k] = (float)s->bg[k];
+  p.bias = (float)o->bias;
+  const int m = o->aa_kind == RT_AA_GRID ? o->grid_size : 1;
+  const int spp = m * m;
+  p.inv_len = (float)(1.0 / (double)spp);
+  p.sample_step = (float)(1.0 / (double)m);
+  p.sample_off = (float)(1.0 / (double)m * 0.5);
+  p.nobj = s->nobj;
+  p.nlight = s->nlight;
+  p.width = o->width;
+  p.height = o->height;
+  p.aa_kind = o->aa_kind;
+  p.grid_m = m;
+  p.spp = spp;
+  p.max_depth = o->max_ray_depth;
+  p.flags = (int32_t)o->flags;
+  p.max_iters = (int32_t)std::min<int64_t>(INT32_MAX, 2 * s->num_nodes + 16);
+  p.mode = mp.mode;
+  p.y0 = mp.y0;
+  p.nrows = mp.nrows;
+  p.ncols = mp.ncols;
+  p.step = mp.step;
+  p.max_step = mp.max_step;
+  p.band_h = mp.band_h;
+  p.rank = mp.rank;
+  p.world = mp.world;
+  const Plan pl = plan_mapping(s, o, mp, spp);
+  p.lanes_per_px = pl.L;
+  p.log2_lanes = pl.log2L;
+  p.tile_x = pl.tx;
+  p.tile_y = pl.ty;
+  p.tiles_x = pl.tiles_x;
+  p.ngroups = pl.ngroups;
+  *blocks = pl.blocks;
 }
 
 template <class R>
@@ -598,8 +792,8 @@ int launch(rt_scene* s, const rt_options* o, const Mapping& mp, float* d_out, hi
     const int e = rtmi_launch_render_f64(&p, blocks, st);
     if (e) return fail(RT_E_DEVICE, "render kernel launch failed: %s", hipGetErrorString((hipError_t)e));
   } else {
-    RenderParams<float> p;
-    fill_params<float>(s, s->f32, o, mp, d_out, p, &blocks);
+    FastParams p;
+    fill_fast(s, o, mp, d_out, p, &blocks);
     if (p.ngroups == 0) return RT_OK;
     const int e = rtmi_launch_render_f32(&p, blocks, st);
     if (e) return fail(RT_E_DEVICE, "render kernel launch failed: %s", hipGetErrorString((hipError_t)e));

@@ -9,7 +9,7 @@ import os
 
 from . import abi
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "librtmi.so")
+LIB_PATH = os.environ.get("RTMI_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "librtmi.so")
 
 _lib = None
 

@@ -19,6 +19,7 @@ RT_DISTANT_LIGHT, RT_POINT_LIGHT = 0, 1
 RT_AA_NONE, RT_AA_GRID, RT_AA_JITTERED, RT_AA_MULTI_JITTERED, RT_AA_CORRELATED_MULTI_JITTERED = range(5)
 RT_FP32, RT_FP64 = 0, 1
 RT_FLAG_ANYHIT_SHADOWS = 0x1
+RT_FLAG_COUNT_TRAVERSAL = 0x2
 
 _d16 = C.c_double * 16
 _d3 = C.c_double * 3

@@ -82,6 +82,16 @@ def test_fp32_within_tolerance(gpu, oracle_mod, name, w, h, aa, m):
     scene = scenes.SCENES[name]()
     ref, rst = _oracle_frame(oracle_mod, scene, _opts(w, h, Precision.fp64, aa, m))
     got, gst, _ = _gpu_frame(scene, _opts(w, h, Precision.fp32, aa, m))
+    if name == "boxtest":
+        # The reference's own NaN-slab case (test/boxtest.nim:31-41): on the
+        # centre column dir.x == 0 exactly and the camera sits exactly on the
+        # box's x = 1 face plane, so the hit depends on 0 * inf = NaN handling
+        # ("exclude or tolerate these pixels"). fp64 mode
+        # reproduces it bit for bit (test_fp64_bit_exact); fp32 is compared
+        # on every other column.
+        keep = np.ones(w, bool)
+        keep[w // 2] = False
+        got, ref = got[:, keep], ref[:, keep]
     _assert_fp32_close(got, ref)
     assert gst.numPrimaryRays == rst.numPrimaryRays
     assert gst.numIntersectionTests == pytest.approx(rst.numIntersectionTests, rel=1e-2)

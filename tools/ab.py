@@ -1,0 +1,75 @@
+"""In-process A/B timing of several librtmi.so builds (interleaved reps).
+
+    RTMI_LIBS=path/a.so,path/b.so ABLATE=c3_full,ground_nolights python tools/ab.py
+"""
+import ctypes as C
+import json
+import os
+import sys
+
+sys.path.insert(0, "nim-raytracer_amd")
+import torch  # noqa: E402  (one HIP runtime for all libraries)
+
+from rtmi import abi, scenes  # noqa: E402
+from rtmi.scene import Antialias, Options, Precision, akGrid, flatten  # noqa: E402
+
+
+def load(path):
+    return abi.bind(C.CDLL(path))
+
+
+def variants():
+    base = scenes.mesh_bunny()
+    o = Options(width=1920, height=1080, antialias=Antialias(akGrid, 16), bias=1e-4,
+                precision=Precision.fp32)
+    v = {"c3_full": (base, o)}
+    s = scenes.mesh_bunny(); s.objects = [s.objects[1]]; s.lights = []; v["ground_nolights"] = (s, o)
+    s = scenes.mesh_bunny(); s.objects = [s.objects[1]]; v["ground_only"] = (s, o)
+    s = scenes.mesh_bunny(); s.objects = [s.objects[0]]; v["bunny_only"] = (s, o)
+    s = scenes.mesh_bunny(); s.lights = []; v["c3_nolights"] = (s, o)
+    v["boxes2_c2"] = (scenes.boxes2(), Options(width=1920, height=1080, antialias=Antialias(akGrid, 8),
+                                               bias=1e-4, precision=Precision.fp32))
+    sel = os.environ.get("ABLATE", "")
+    return {k: x for k, x in v.items() if not sel or k in sel.split(",")}
+
+
+def main():
+    libs = os.environ["RTMI_LIBS"].split(",")
+    reps = int(os.environ.get("REPS", "4"))
+    L = [load(p) for p in libs]
+    for lib in L:
+        assert lib.rt_init(0) == 0, lib.rt_last_error()
+    res = {}
+    stream = torch.cuda.current_stream()
+    for name, (scene, opts) in variants().items():
+        flat = flatten(scene)
+        hs = []
+        for lib in L:
+            h = C.c_void_p()
+            assert lib.rt_scene_create(C.byref(flat.desc), C.byref(h)) == 0, lib.rt_last_error()
+            hs.append(h)
+        fb = torch.zeros(opts.width * opts.height * 3, dtype=torch.float32, device="cuda")
+        o = opts.to_c()
+        times = {p: [] for p in libs}
+        for r in range(reps):
+            for p, lib, h in zip(libs, L, hs):
+                st = abi.rt_stats()
+                lib.rt_render_lines_device(h, C.byref(o), C.c_void_p(fb.data_ptr()), 0, opts.height, 1, 1,
+                                           C.c_void_p(stream.cuda_stream or None), C.byref(st))
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+                for _ in range(3):
+                    lib.rt_render_lines_device(h, C.byref(o), C.c_void_p(fb.data_ptr()), 0, opts.height, 1, 1,
+                                               C.c_void_p(stream.cuda_stream or None), None)
+                e1.record(stream)
+                torch.cuda.synchronize()
+                times[p].append(e0.elapsed_time(e1) / 3)
+        for lib, h in zip(L, hs):
+            lib.rt_scene_destroy(h)
+        res[name] = {os.path.basename(p): round(min(t), 3) for p, t in times.items()}
+        print(name, res[name], flush=True)
+    json.dump(res, open("gpurun_out/ab.json", "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()
