@@ -1,0 +1,139 @@
+"""The C-ABI library (librtmi.so) without a GPU: it loads, exports every
+symbol include/rtmi.h declares with the struct layouts the header defines, and
+its host-side entry points validate input and fail with codes, not aborts."""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from rtmi import abi, glm, scenes
+from rtmi._lib import LIB_PATH, lib
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(REPO, "include", "rtmi.h")
+
+
+def header_functions():
+    txt = open(HEADER).read()
+    return set(re.findall(r"^\s*(?:const\s+)?\w+\s*\*?\s*(rt_\w+)\s*\(", txt, re.M))
+
+
+def test_header_symbols_exported():
+    names = header_functions()
+    assert len(names) >= 15
+    raw = C.CDLL(LIB_PATH)
+    missing = [n for n in names if not hasattr(raw, n)]
+    assert not missing, missing
+    assert names == set(abi.SIGNATURES), names ^ set(abi.SIGNATURES)
+
+
+def test_version_and_error_channel():
+    L = lib()
+    assert L.rt_version() == abi.RTMI_ABI_VERSION
+    assert L.rt_scene_destroy(None) == abi.RT_E_INVALID
+    assert b"null" in L.rt_last_error()
+
+
+def test_no_gpu_is_an_error_not_a_crash():
+    L = lib()
+    if L.rt_device_count() > 0:
+        pytest.skip("GPU present")
+    assert L.rt_init(0) == abi.RT_E_DEVICE
+    assert L.rt_last_error()
+
+
+_LAYOUT_C = r"""
+#include <stdio.h>
+#include <stddef.h>
+#include "rtmi.h"
+#define S(t) printf(#t " %zu\n", sizeof(t));
+#define O(t, f) printf(#t "." #f " %zu\n", offsetof(t, f));
+int main(void) {
+  S(rt_mesh_desc) S(rt_object_desc) S(rt_light_desc) S(rt_scene_desc) S(rt_options) S(rt_stats)
+  S(rt_traversal_counters) S(rt_scene_info)
+  O(rt_object_desc, world_to_object) O(rt_object_desc, radius) O(rt_object_desc, reflection)
+  O(rt_light_desc, pos) O(rt_scene_desc, lights) O(rt_scene_desc, fov) O(rt_scene_desc, bg_color)
+  O(rt_options, bias) O(rt_options, seed) O(rt_options, flags) O(rt_scene_info, build_ms)
+  return 0;
+}
+"""
+
+
+def test_struct_layouts_match_header(tmp_path):
+    src = tmp_path / "layout.c"
+    src.write_text(_LAYOUT_C)
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-std=c11", "-I", os.path.join(REPO, "include"), str(src), "-o", str(exe)],
+                   check=True)
+    out = dict(line.rsplit(" ", 1) for line in subprocess.check_output([str(exe)]).decode().split("\n")
+               if line)
+    for k, v in out.items():
+        if "." in k:
+            t, f = k.split(".")
+            assert getattr(getattr(abi, t), f).offset == int(v), k
+        else:
+            assert C.sizeof(getattr(abi, k)) == int(v), k
+
+
+def test_mat4_inverse_is_glm_inverse():
+    L = lib()
+    mats = [o.geometry.objectToWorld for o in scenes.boxes2().objects]
+    mats.append(scenes.spheres_warm().cameraToWorld)
+    for m in mats:
+        a = (C.c_double * 16)(*glm.flat(m))
+        out = (C.c_double * 16)()
+        assert L.rt_mat4_inverse(a, out) == abi.RT_OK
+        assert np.array_equal(np.array(out[:]), glm.flat(glm.inverse(m)))
+    z = (C.c_double * 16)()
+    assert L.rt_mat4_inverse(z, (C.c_double * 16)()) == abi.RT_E_INVALID
+
+
+def test_load_geom_matches_reader(tmp_path):
+    from rtmi.loaders import default_geom_path, readGeom
+    L = lib()
+    n = C.c_int64(0)
+    p = default_geom_path().encode()
+    assert L.rt_load_geom(p, C.byref(n), None) == abi.RT_OK
+    assert n.value == 69451
+    buf = np.zeros(n.value * 9, dtype=np.float64)
+    assert L.rt_load_geom(p, C.byref(n), buf.ctypes.data_as(C.POINTER(C.c_double))) == abi.RT_OK
+    assert np.array_equal(buf, readGeom(default_geom_path()).astype(np.float64).reshape(-1))
+    # errors
+    small = C.c_int64(10)
+    assert L.rt_load_geom(p, C.byref(small), buf.ctypes.data_as(C.POINTER(C.c_double))) == abi.RT_E_INVALID
+    assert L.rt_load_geom(str(tmp_path / "missing.geom").encode(), C.byref(n), None) == abi.RT_E_IO
+    bad = tmp_path / "trunc.geom"
+    bad.write_bytes(np.int32(5).tobytes() + b"\0" * 17)
+    m = C.c_int64(5)
+    assert L.rt_load_geom(str(bad).encode(), C.byref(m), buf.ctypes.data_as(C.POINTER(C.c_double))) == abi.RT_E_IO
+
+
+def test_band_rows_matches_host_mapping():
+    from rtmi.dist import band_rows
+    L = lib()
+    out = C.c_int32()
+    for h, b, w in [(1080, 16, 1), (1080, 16, 8), (131, 7, 3), (1, 1, 8), (2160, 32, 4)]:
+        assert L.rt_band_rows(h, b, w, C.byref(out)) == abi.RT_OK
+        assert out.value == band_rows(h, b, w)
+    assert L.rt_band_rows(0, 16, 1, C.byref(out)) == abi.RT_E_INVALID
+
+
+def test_scene_create_validates_before_touching_a_device():
+    from rtmi.scene import flatten
+    L = lib()
+    h = C.c_void_p()
+    assert L.rt_scene_create(None, C.byref(h)) == abi.RT_E_INVALID
+    s = scenes.spheres_warm(3)
+    flat = flatten(s)
+    flat._objs[0].type = 7
+    assert L.rt_scene_create(C.byref(flat.desc), C.byref(h)) == abi.RT_E_INVALID
+    flat = flatten(scenes.mesh_bunny())
+    flat._objs[0].mesh = 3
+    assert L.rt_scene_create(C.byref(flat.desc), C.byref(h)) == abi.RT_E_INVALID
+    flat = flatten(scenes.spheres_warm(3))
+    flat._objs[1].object_to_world[3] = 0.5  # projective row: unsupported
+    assert L.rt_scene_create(C.byref(flat.desc), C.byref(h)) == abi.RT_E_UNSUPPORTED
+    assert not h.value

@@ -1,0 +1,69 @@
+"""The N > 1 path on CPU: world_size-2 torch.distributed (gloo). Each rank
+renders its round-robin image bands (with the oracle, standing in for the
+GPU's rt_render_bands_device), one all-gather assembles them, rank 0
+un-interleaves (the host statement of rt_unshard_bands_device), and Stats are
+all-reduced — checked against a whole-frame render."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+BAND_H = 16
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, out_path):
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(repo, "nim-raytracer_amd"))
+    sys.path.insert(0, os.path.join(repo, "oracle"))
+    import torch
+    import torch.distributed as dist
+
+    import oracle
+    from rtmi import Antialias, Options, Precision, akGrid, scenes
+    from rtmi.dist import band_rows, rank_rows, unshard_host
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    opts = Options(width=64, height=45, antialias=Antialias(akGrid, 2), bias=1e-4,
+                   precision=Precision.fp64)
+    o = oracle.OracleScene(scenes.spheres_warm())
+    rows = band_rows(opts.height, BAND_H, world)
+    ys = rank_rows(opts.height, BAND_H, rank, world)
+    full = np.zeros((opts.height, opts.width, 3), np.float32)
+    _, st, _ = o.render(opts, rows=[int(y) for y in ys if y >= 0], fb=full, nthreads=2)
+    local = np.zeros((rows, opts.width, 3), np.float32)
+    local[ys >= 0] = full[ys[ys >= 0]]
+    gathered = torch.zeros((world * rows, opts.width, 3), dtype=torch.float32)
+    dist.all_gather_into_tensor(gathered, torch.from_numpy(local))
+    counts = torch.tensor([st.numPrimaryRays, st.numIntersectionTests, st.numIntersectionHits,
+                           st.numShadowRays], dtype=torch.int64)
+    dist.all_reduce(counts)
+    if rank == 0:
+        fb = unshard_host(gathered.numpy().reshape(world, rows, opts.width, 3), opts.height, BAND_H)
+        np.savez(out_path, fb=fb, counts=counts.numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2])
+def test_band_shard_gather_matches_whole_frame(tmp_path, oracle_mod, world):
+    import torch.multiprocessing as mp
+
+    from rtmi import Antialias, Options, Precision, akGrid, scenes
+    out = str(tmp_path / "frame.npz")
+    mp.spawn(_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    z = np.load(out)
+    opts = Options(width=64, height=45, antialias=Antialias(akGrid, 2), bias=1e-4, precision=Precision.fp64)
+    ref, st, _ = oracle_mod.OracleScene(scenes.spheres_warm()).render(opts)
+    assert np.array_equal(z["fb"], ref)
+    assert z["counts"].tolist() == [st.numPrimaryRays, st.numIntersectionTests, st.numIntersectionHits,
+                                    st.numShadowRays]
