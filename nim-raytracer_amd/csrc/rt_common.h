@@ -69,6 +69,18 @@ struct alignas(16) BvhNode {
 };
 static_assert(sizeof(BvhNode) == 64, "BvhNode must be 64 bytes");
 
+// BVH4 node for the float32 kernel (collapsed from the SAH BVH2, same
+// conservative fp32 boxes): four child boxes in SoA form, 128 bytes = two
+// s_load_dwordx16. count[k] > 0: leaf with triangles [child[k], +count[k]);
+// count[k] == 0: internal node child[k]; count[k] < 0: empty slot.
+struct alignas(16) Bvh4Node {
+  float lo[3][4];   // lo[axis][child]
+  float hi[3][4];
+  int32_t child[4];
+  int32_t count[4];
+};
+static_assert(sizeof(Bvh4Node) == 128, "Bvh4Node must be 128 bytes");
+
 struct alignas(16) TriF32 {
   float v0[3];
   int32_t id;    // original face index (tie-break + normal lookup)
@@ -153,9 +165,11 @@ static_assert(sizeof(FObjX) == 128, "FObjX must be 128 bytes");
 
 struct alignas(16) FMesh {
   float lo[3];
-  int32_t root;
+  int32_t root;        // BVH4 root (index into nodes4), -1 for an empty mesh
   float hi[3];
   int32_t normal_base;
+  int32_t root2;       // BVH2 root (index into nodes), -1 for an empty mesh
+  int32_t pad[3];
 };
 
 struct alignas(16) FLight {
@@ -171,6 +185,7 @@ struct FastParams {
   const FMesh* meshes;
   const FLight* lights;
   const BvhNode* nodes;
+  const Bvh4Node* nodes4;
   const TriF32* tris;
   const float* normals;
   float* fb;

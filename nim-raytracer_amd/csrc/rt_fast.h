@@ -28,6 +28,9 @@
 #endif
 #endif
 
+#ifndef RTMI_BVH4
+#define RTMI_BVH4 0
+#endif
 #ifndef RTMI_LEAF_BATCH
 #define RTMI_LEAF_BATCH 0
 #endif
@@ -56,6 +59,23 @@ __device__ __forceinline__ float dot3(F3 a, F3 b) { return __builtin_fmaf(a.x, b
 struct Stats32 {
   unsigned int v[kStatSlots];
 };
+
+#ifdef RTMI_STAMPS
+// Diagnostic build only (never the measured kernel): shader-clock stamps
+// accumulated into the traversal counter slots 5..8.
+__device__ __forceinline__ unsigned long long stamp() {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+#define RT_STAMP(var) const unsigned long long var = stamp()
+#define RT_ACC(slot, a, b) ws.v[slot] += (unsigned int)((b) - (a))
+#else
+#define RT_STAMP(var)
+#define RT_ACC(slot, a, b)
+#endif
 
 struct Hit {
   int obj;
@@ -132,11 +152,27 @@ __device__ __forceinline__ float triangle(const TriF32& tri, F3 o, F3 d) {
   return ok ? t : -finf();
 }
 
-// Wave-coherent closest/any hit over one mesh BVH (see rt_device.h).
+// Leaf: closest/any hit over `n` triangles starting at `first` for lanes `h`.
+__device__ __forceinline__ void leaf(const FastParams& p, int first, int n, bool h, F3 o, F3 d, float& tbest,
+                                     int& best_id) {
+  for (int k = 0; k < n; ++k) {
+    const TriF32 tri = cp(p.tris)[first + k];
+    const float t = triangle(tri, o, d);
+    const int id = tri.id;
+    if (h && t >= 0.0f && (t < tbest || (t == tbest && id < best_id))) {
+      tbest = t;
+      best_id = id;
+    }
+  }
+}
+
+// Wave-coherent closest/any hit over one mesh BVH2 (64-B nodes, both child
+// boxes per fetch). Selected with -DRTMI_BVH4=0.
 template <bool COUNT>
-__device__ __forceinline__ void traverse(const FastParams& p, int root, F3 o, F3 d, bool active, bool anyhit,
-                                         float& tbest, int& best_id, Stats32& ws) {
+__device__ __forceinline__ void traverse2(const FastParams& p, int root, F3 o, F3 d, bool active, bool anyhit,
+                                          float& tbest, int& best_id, Stats32& ws) {
   if (bal(active) == 0ull) return;
+  RT_STAMP(t_enter);
   const float e = 1e-20f;
   const float dx = fabsf(d.x) < e ? __builtin_copysignf(e, d.x) : d.x;
   const float dy = fabsf(d.y) < e ? __builtin_copysignf(e, d.y) : d.y;
@@ -167,46 +203,23 @@ __device__ __forceinline__ void traverse(const FastParams& p, int root, F3 o, F3
     const bool h1 = active && tn1 <= tf1 * 1.0000004f;
     unsigned long long m0 = (nd.n0 > 0 || nd.c0 >= 0) ? bal(h0) : 0ull;
     unsigned long long m1 = (nd.n1 > 0 || nd.c1 >= 0) ? bal(h1) : 0ull;
-    for (int c = 0; c < 2; ++c) {
-      const int n = c == 0 ? nd.n0 : nd.n1;
-      const unsigned long long m = c == 0 ? m0 : m1;
-      if (n > 0 && m) {
-        const int first = c == 0 ? nd.c0 : nd.c1;
-        const bool h = c == 0 ? h0 : h1;
-        if constexpr (COUNT) {
-          ws.v[STAT_TRI_FETCH] += (unsigned int)n;
-          ws.v[STAT_LANE_TRIS] += pc(m) * (unsigned int)n;
-        }
-        // Leaves hold at most kLeafMax triangles and the array is padded, so
-        // all of a leaf's records are requested at once (one scalar-load
-        // round trip per leaf instead of one per triangle).
-#if RTMI_LEAF_BATCH
-        TriF32 tr[kLeafMax];
-#pragma unroll
-        for (int k = 0; k < kLeafMax; ++k) tr[k] = cp(p.tris)[first + k];
-#pragma unroll
-        for (int k = 0; k < kLeafMax; ++k) {
-          const float t = triangle(tr[k], o, d);
-          const int id = tr[k].id;
-          if (k < n && h && t >= 0.0f && (t < tbest || (t == tbest && id < best_id))) {
-            tbest = t;
-            best_id = id;
-          }
-        }
-#else
-        for (int k = 0; k < n; ++k) {
-          const TriF32 tri = cp(p.tris)[first + k];
-          const float t = triangle(tri, o, d);
-          const int id = tri.id;
-          if (h && t >= 0.0f && (t < tbest || (t == tbest && id < best_id))) {
-            tbest = t;
-            best_id = id;
-          }
-        }
-#endif
-        if (anyhit) active = active && best_id < 0;
-        if (c == 0) m0 = 0ull; else m1 = 0ull;
+    if (nd.n0 > 0 && m0) {
+      if constexpr (COUNT) {
+        ws.v[STAT_TRI_FETCH] += (unsigned int)nd.n0;
+        ws.v[STAT_LANE_TRIS] += pc(m0) * (unsigned int)nd.n0;
       }
+      leaf(p, nd.c0, nd.n0, h0, o, d, tbest, best_id);
+      if (anyhit) active = active && best_id < 0;
+      m0 = 0ull;
+    }
+    if (nd.n1 > 0 && m1) {
+      if constexpr (COUNT) {
+        ws.v[STAT_TRI_FETCH] += (unsigned int)nd.n1;
+        ws.v[STAT_LANE_TRIS] += pc(m1) * (unsigned int)nd.n1;
+      }
+      leaf(p, nd.c1, nd.n1, h1, o, d, tbest, best_id);
+      if (anyhit) active = active && best_id < 0;
+      m1 = 0ull;
     }
     if (anyhit && bal(active) == 0ull) break;
     if (m0 && m1) {
@@ -227,6 +240,118 @@ __device__ __forceinline__ void traverse(const FastParams& p, int root, F3 o, F3
       node = __builtin_amdgcn_readlane(stack, sp);
     }
   }
+#ifdef RTMI_STAMPS
+  { RT_STAMP(t_exit); RT_ACC(5, t_enter, t_exit); }
+#endif
+}
+
+__device__ __forceinline__ void cswap(unsigned& ka, int& ca, unsigned& kb, int& cb) {
+  const bool sw = kb < ka;
+  const unsigned k = sw ? kb : ka;
+  const int c = sw ? cb : ca;
+  kb = sw ? ka : kb;
+  cb = sw ? ca : cb;
+  ka = k;
+  ca = c;
+}
+
+// Wave-coherent closest/any hit over one mesh's BVH4 (rt_common.h Bvh4Node).
+// The node index and the stack are wave-uniform: one 128-B node is fetched
+// with scalar loads, every lane tests the four child boxes against its own
+// ray (four independent slab tests: ILP), ballots decide which children the
+// wave visits, leaves are tested immediately, internal children are ordered
+// by the lead lane's entry distance (a scalar sorting network on the float
+// bits; entry distances are >= 0) and all but the nearest are pushed onto
+// the 64-lane VGPR stack. Must be called from wave-uniform control flow.
+template <bool COUNT>
+__device__ __forceinline__ void traverse4(const FastParams& p, int root, F3 o, F3 d, bool active, bool anyhit,
+                                          float& tbest, int& best_id, Stats32& ws) {
+  if (bal(active) == 0ull) return;
+  RT_STAMP(t_enter);
+  const float e = 1e-20f;
+  const float dx = fabsf(d.x) < e ? __builtin_copysignf(e, d.x) : d.x;
+  const float dy = fabsf(d.y) < e ? __builtin_copysignf(e, d.y) : d.y;
+  const float dz = fabsf(d.z) < e ? __builtin_copysignf(e, d.z) : d.z;
+  const F3 ni = f3(rcp(dx), rcp(dy), rcp(dz));
+  const F3 oi = f3(o.x * ni.x, o.y * ni.y, o.z * ni.z);
+  const int lane = (int)__lane_id();
+  int stack = 0;
+  int sp = 0;
+  int node = root;
+  for (int iter = 0; iter < p.max_iters; ++iter) {
+    RT_STAMP(t_node);
+    const Bvh4Node nd = cp(p.nodes4)[node];
+    if constexpr (COUNT) {
+      ws.v[STAT_NODE_FETCH] += 1u;
+      ws.v[STAT_LANE_NODES] += pc(bal(active));
+    }
+    float tn[4];
+    bool h[4];
+    unsigned long long m[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float ax = __builtin_fmaf(nd.lo[0][k], ni.x, -oi.x), bx = __builtin_fmaf(nd.hi[0][k], ni.x, -oi.x);
+      const float ay = __builtin_fmaf(nd.lo[1][k], ni.y, -oi.y), by = __builtin_fmaf(nd.hi[1][k], ni.y, -oi.y);
+      const float az = __builtin_fmaf(nd.lo[2][k], ni.z, -oi.z), bz = __builtin_fmaf(nd.hi[2][k], ni.z, -oi.z);
+      tn[k] = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fmaxf(fminf(az, bz), 0.0f));
+      const float tf = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fminf(fmaxf(az, bz), tbest));
+      h[k] = active && tn[k] <= tf * 1.0000004f;
+      m[k] = nd.count[k] >= 0 ? bal(h[k]) : 0ull;
+    }
+#ifdef RTMI_STAMPS
+    { RT_STAMP(t_slab); RT_ACC(8, t_node, t_slab); }
+#endif
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (nd.count[k] > 0 && m[k]) {
+        RT_STAMP(t_leaf);
+        if constexpr (COUNT) {
+          ws.v[STAT_TRI_FETCH] += (unsigned int)nd.count[k];
+          ws.v[STAT_LANE_TRIS] += pc(m[k]) * (unsigned int)nd.count[k];
+        }
+        leaf(p, nd.child[k], nd.count[k], h[k], o, d, tbest, best_id);
+        if (anyhit) active = active && best_id < 0;
+        m[k] = 0ull;
+#ifdef RTMI_STAMPS
+        { RT_STAMP(t_leaf_end); RT_ACC(6, t_leaf, t_leaf_end); }
+#endif
+      }
+    }
+    if (anyhit && bal(active) == 0ull) break;
+    // order the internal children hit by any lane
+    const unsigned long long live = bal(active);
+    const int lead = live ? (int)__builtin_ctzll(live) : 0;
+    unsigned key[4];
+    int cn[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const unsigned tk = (unsigned)__builtin_amdgcn_readlane(__float_as_int(tn[k]), lead);
+      key[k] = m[k] ? (((m[k] >> lead) & 1ull) ? tk : 0x7f000000u) : 0xffffffffu;
+      cn[k] = nd.child[k];
+    }
+    cswap(key[0], cn[0], key[1], cn[1]);
+    cswap(key[2], cn[2], key[3], cn[3]);
+    cswap(key[0], cn[0], key[2], cn[2]);
+    cswap(key[1], cn[1], key[3], cn[3]);
+    cswap(key[1], cn[1], key[2], cn[2]);
+    if (key[0] == 0xffffffffu) {
+      if (sp == 0) break;
+      --sp;
+      node = __builtin_amdgcn_readlane(stack, sp);
+    } else {
+      node = cn[0];
+#pragma unroll
+      for (int k = 3; k >= 1; --k) {
+        if (key[k] != 0xffffffffu) {
+          stack = (lane == sp) ? cn[k] : stack;
+          ++sp;
+        }
+      }
+    }
+  }
+#ifdef RTMI_STAMPS
+  { RT_STAMP(t_exit); RT_ACC(5, t_enter, t_exit); }
+#endif
 }
 
 // trace (renderer.nim:47-67): linear closest hit over the objects in order.
@@ -255,7 +380,11 @@ __device__ __forceinline__ Hit trace(const FastParams& p, F3 o, F3 d, float tmax
       const bool in = gate >= 0.0f;
       float tb = h.t;
       int best = -1;
-      if (m.root >= 0) traverse<COUNT>(p, m.root, ro, rd, active && in, anyhit, tb, best, ws);
+#if RTMI_BVH4
+      if (m.root >= 0) traverse4<COUNT>(p, m.root, ro, rd, active && in, anyhit, tb, best, ws);
+#else
+      if (m.root2 >= 0) traverse2<COUNT>(p, m.root2, ro, rd, active && in, anyhit, tb, best, ws);
+#endif
       t = !in ? -finf() : (best >= 0 ? tb : finf());
       tri = best;
     }
@@ -309,6 +438,9 @@ __device__ __forceinline__ F3 shade_path(const FastParams& p, F3 o, F3 d, bool a
   for (int lev = 0; lev < kMaxShadeLevels; ++lev) {
     if (bal(act) == 0ull) break;
     const Hit hit = trace<COUNT>(p, o, d, finf(), act, false, ws);
+#ifdef RTMI_EXP_PRIMARY_ONLY
+    return f3(hit.t, (float)hit.obj, (float)hit.tri);
+#endif
     if (act && hit.obj < 0) acc = f3(acc.x + w * p.bg[0], acc.y + w * p.bg[1], acc.z + w * p.bg[2]);
     const bool lit = act && hit.obj >= 0;
     const F3 hw = f3(__builtin_fmaf(d.x, hit.t, o.x), __builtin_fmaf(d.y, hit.t, o.y), __builtin_fmaf(d.z, hit.t, o.z));
@@ -462,7 +594,11 @@ __global__ __launch_bounds__(256) void k_render_fast(const FastParams p) {
                       (cx * p.cam[5] + cy * p.cam[8] - p.cam[11]) * rl);
       const F3 o = f3(p.cam[0], p.cam[1], p.cam[2]);
       ws.v[STAT_PRIMARY] += pc(bal(sv));
+      RT_STAMP(t_s0);
       const F3 c = shade_path<COUNT>(p, o, d, sv, ws);
+#ifdef RTMI_STAMPS
+      { RT_STAMP(t_s1); RT_ACC(7, t_s0, t_s1); }
+#endif
       if (sv) acc = grid_aa ? f3(acc.x + c.x, acc.y + c.y, acc.z + c.z) : c;
       bi += dli;
       bj += dlj;

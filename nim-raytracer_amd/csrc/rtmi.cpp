@@ -137,6 +137,7 @@ struct rt_scene {
   FastData f32;
   PrecisionData<double> f64;
   DevBuf<BvhNode> nodes;
+  DevBuf<Bvh4Node> nodes4;
   DevBuf<unsigned long long> partials;
   DevBuf<unsigned long long> acc;
   DevBuf<float> fb_scratch;
@@ -149,6 +150,7 @@ struct rt_scene {
     f32.release();
     f64.release();
     nodes.release();
+    nodes4.release();
     partials.release();
     acc.release();
     fb_scratch.release();
@@ -401,6 +403,7 @@ void fill_fast_records(const rt_scene_desc* d, const std::vector<DevMesh<float>>
       fm[m].hi[k] = dm[m].hi[k];
     }
     fm[m].root = dm[m].root;
+    fm[m].root2 = dm[m].root;
     fm[m].normal_base = dm[m].normal_base;
   }
   fl.assign((size_t)d->num_lights, FLight{});
@@ -445,6 +448,8 @@ extern "C" int rt_scene_create(const rt_scene_desc* d, rt_scene** out_scene) {
   int64_t ntri = 0, nnodes = 0;
   int maxdepth = 0;
   std::vector<BvhNode> all_nodes;
+  std::vector<Bvh4Node> all_nodes4;
+  std::vector<int32_t> node4_base((size_t)d->num_meshes, -1);
   for (int m = 0; m < d->num_meshes; ++m) {
     const rt_mesh_desc& md = d->meshes[m];
     if (md.num_faces < 0 || md.num_vertices < 0 || (md.num_faces > 0 && (!md.faces || !md.vertices)))
@@ -496,6 +501,21 @@ extern "C" int rt_scene_create(const rt_scene_desc* d, rt_scene** out_scene) {
       if (nd.n1 > 0) nd.c1 += (int32_t)ntri;
       all_nodes.push_back(nd);
     }
+    {  // BVH4 for the float32 kernel
+      std::vector<Bvh4Node> n4;
+      int d4 = 0;
+      const char* err4 = "BVH4 collapse failed";
+      if (!collapse_bvh4(bvhs[(size_t)m], &n4, &d4, &err4)) return fail(RT_E_INVALID, "mesh %d: %s", m, err4);
+      node4_base[(size_t)m] = n4.empty() ? -1 : (int32_t)all_nodes4.size();
+      const int32_t b4 = (int32_t)all_nodes4.size();
+      for (Bvh4Node nd : n4) {
+        for (int k = 0; k < 4; ++k) {
+          if (nd.count[k] == 0) nd.child[k] += b4;
+          else if (nd.count[k] > 0) nd.child[k] += (int32_t)ntri;
+        }
+        all_nodes4.push_back(nd);
+      }
+    }
     ntri += md.num_faces;
     nnodes += (int64_t)bvhs[(size_t)m].nodes.size();
     maxdepth = std::max(maxdepth, bvhs[(size_t)m].max_depth);
@@ -533,6 +553,7 @@ extern "C" int rt_scene_create(const rt_scene_desc* d, rt_scene** out_scene) {
     std::vector<FMesh> fm;
     std::vector<FLight> fl;
     fill_fast_records(d, m, fo, fx, fm, fl);
+    for (size_t k = 0; k < fm.size(); ++k) fm[k].root = node4_base[k];  // BVH4 roots
     int rc;
     if ((rc = s->f32.objs.upload(fo)) || (rc = s->f32.objx.upload(fx)) || (rc = s->f32.meshes.upload(fm)) ||
         (rc = s->f32.lights.upload(fl)) || (rc = s->f32.tris.upload(t)) || (rc = s->f32.normals.upload(n)))
@@ -552,6 +573,7 @@ extern "C" int rt_scene_create(const rt_scene_desc* d, rt_scene** out_scene) {
   }
   int rc = s->nodes.upload(all_nodes);
   if (rc) return rc;
+  if ((rc = s->nodes4.upload(all_nodes4))) return rc;
   s->max_waves = s->num_cus * 8 * 4;  // 8 blocks of 4 waves per CU at most
   if ((rc = s->partials.alloc((size_t)s->max_waves * kStatSlots))) return rc;
   if ((rc = s->acc.alloc(kStatSlots))) return rc;
@@ -584,7 +606,8 @@ extern "C" int rt_scene_get_info(const rt_scene* s, rt_scene_info* out) {
   out->num_bvh_nodes = s->num_nodes;
   out->max_bvh_depth = s->max_depth;
   out->device = s->device;
-  out->device_bytes = (int64_t)(s->f32.bytes() + s->f64.bytes() + s->nodes.bytes() + s->partials.bytes() +
+  out->device_bytes = (int64_t)(s->f32.bytes() + s->f64.bytes() + s->nodes.bytes() + s->nodes4.bytes() +
+                                s->partials.bytes() +
                                 s->acc.bytes());
   out->build_ms = s->build_ms;
   return RT_OK;
@@ -660,6 +683,7 @@ void fill_fast(rt_scene* s, const rt_options* o, const Mapping& mp, float* fb, F
   p.meshes = s->f32.meshes.p;
   p.lights = s->f32.lights.p;
   p.nodes = s->nodes.p;
+  p.nodes4 = s->nodes4.p;
   p.tris = s->f32.tris.p;
   p.normals = s->f32.normals.p;
   p.fb = fb;
