@@ -74,16 +74,9 @@ struct Builder {
   void set_child(BvhNode& nd, int which, const ChildRef& r) const {
     float* lo = which == 0 ? nd.lo0 : nd.lo1;
     float* hi = which == 0 ? nd.hi0 : nd.hi1;
-    if (r.n == 0 && r.c < 0) {  // empty child: never visited (kernel checks c/n)
-      for (int a = 0; a < 3; ++a) {
-        lo[a] = std::numeric_limits<float>::quiet_NaN();
-        hi[a] = std::numeric_limits<float>::quiet_NaN();
-      }
-    } else {
-      for (int a = 0; a < 3; ++a) {
-        lo[a] = lo32(r.box.lo[a]);
-        hi[a] = hi32(r.box.hi[a]);
-      }
+    for (int a = 0; a < 3; ++a) {
+      lo[a] = lo32(r.box.lo[a]);
+      hi[a] = hi32(r.box.hi[a]);
     }
     if (which == 0) {
       nd.c0 = r.c;
@@ -259,9 +252,11 @@ bool build_bvh(const double* v, const int32_t* f, int64_t nf, const BvhBuildPara
   const int s = B.split(0, (int)nf, 1, bb);
   ChildRef l, r;
   if (s < 0) {
+    // a single leaf: the root's second slot repeats it, so every child of
+    // every node is valid (the kernels skip no-child checks); a repeated
+    // triangle can only tie with itself and never changes the closest hit
     l = B.make_leaf(0, (int)nf, bb);
-    r.c = -1;
-    r.n = 0;
+    r = l;
   } else {
     l = B.build(0, s, 2);
     r = B.build(s, (int)nf, 2);
@@ -283,117 +278,12 @@ bool build_bvh(const double* v, const int32_t* f, int64_t nf, const BvhBuildPara
           *err = "BVH leaf out of range";
           return false;
         }
-      } else if (cs[k] >= nn || (cs[k] < 0 && cs[k] != -1)) {
+      } else if (cs[k] >= nn || cs[k] <= 0) {  // internal: never the root, never empty
         *err = "BVH child out of range";
         return false;
       }
     }
   }
-  return true;
-}
-
-namespace {
-
-struct Ref2 {
-  int32_t c, n;   // BVH2 child reference (n == 0: internal node c; c < 0: empty)
-  float lo[3], hi[3];
-};
-
-float area(const Ref2& r) {
-  const float dx = r.hi[0] - r.lo[0], dy = r.hi[1] - r.lo[1], dz = r.hi[2] - r.lo[2];
-  return 2.0f * (dx * dy + dy * dz + dz * dx);
-}
-
-Ref2 child_ref(const BvhNode& nd, int k) {
-  Ref2 r;
-  r.c = k == 0 ? nd.c0 : nd.c1;
-  r.n = k == 0 ? nd.n0 : nd.n1;
-  for (int a = 0; a < 3; ++a) {
-    r.lo[a] = k == 0 ? nd.lo0[a] : nd.lo1[a];
-    r.hi[a] = k == 0 ? nd.hi0[a] : nd.hi1[a];
-  }
-  return r;
-}
-
-struct Collapser {
-  const std::vector<BvhNode>& n2;
-  std::vector<Bvh4Node>& n4;
-  int max_depth = 0;
-
-  // Emit the BVH4 node whose children come from expanding BVH2 node `b2`.
-  int32_t emit(int32_t b2, int depth) {
-    std::vector<Ref2> kids;
-    for (int k = 0; k < 2; ++k) {
-      const Ref2 r = child_ref(n2[(size_t)b2], k);
-      if (r.n > 0 || r.c >= 0) kids.push_back(r);
-    }
-    while (kids.size() < 4) {
-      int best = -1;
-      float best_area = -1.0f;
-      for (size_t i = 0; i < kids.size(); ++i)
-        if (kids[i].n == 0 && kids[i].c >= 0 && area(kids[i]) > best_area) {
-          best_area = area(kids[i]);
-          best = (int)i;
-        }
-      if (best < 0) break;
-      const int32_t src = kids[(size_t)best].c;
-      kids.erase(kids.begin() + best);
-      for (int k = 0; k < 2; ++k) {
-        const Ref2 r = child_ref(n2[(size_t)src], k);
-        if (r.n > 0 || r.c >= 0) kids.push_back(r);
-      }
-    }
-    const int32_t me = (int32_t)n4.size();
-    n4.emplace_back();
-    max_depth = std::max(max_depth, depth);
-    Bvh4Node nd;
-    for (int k = 0; k < 4; ++k) {
-      for (int a = 0; a < 3; ++a) {
-        nd.lo[a][k] = 0.0f;
-        nd.hi[a][k] = 0.0f;
-      }
-      nd.child[k] = -1;
-      nd.count[k] = -1;
-    }
-    for (size_t k = 0; k < kids.size(); ++k) {
-      const Ref2& r = kids[k];
-      for (int a = 0; a < 3; ++a) {
-        nd.lo[a][k] = r.lo[a];
-        nd.hi[a][k] = r.hi[a];
-      }
-      if (r.n > 0) {
-        nd.child[k] = r.c;
-        nd.count[k] = r.n;
-      } else {
-        nd.child[k] = emit(r.c, depth + 1);
-        nd.count[k] = 0;
-      }
-    }
-    n4[(size_t)me] = nd;
-    return me;
-  }
-};
-
-}  // namespace
-
-bool collapse_bvh4(const BvhResult& b2, std::vector<Bvh4Node>* out, int* max_depth, const char** err) {
-  out->clear();
-  *max_depth = 0;
-  if (b2.nodes.empty()) return true;
-  Collapser c{b2.nodes, *out};
-  c.emit(0, 1);
-  *max_depth = c.max_depth;
-  // each level pushes at most 3 entries: keep the stack within one VGPR
-  if (3 * c.max_depth + 1 > 64) {
-    *err = "BVH4 too deep for the traversal stack";
-    return false;
-  }
-  for (const Bvh4Node& nd : *out)
-    for (int k = 0; k < 4; ++k)
-      if (nd.count[k] == 0 && (nd.child[k] <= 0 || nd.child[k] >= (int32_t)out->size())) {
-        *err = "BVH4 child out of range";
-        return false;
-      }
   return true;
 }
 

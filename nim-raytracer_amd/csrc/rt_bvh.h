@@ -27,10 +27,6 @@ struct BvhResult {
   int max_depth = 0;
 };
 
-// Collapse a BVH2 into a BVH4 (greedy: expand the internal child with the
-// largest surface area until four slots are used). Leaves keep their triangle
-// ranges; boxes are copied from the BVH2 (already conservative fp32).
-bool collapse_bvh4(const BvhResult& b2, std::vector<Bvh4Node>* out, int* max_depth, const char** err);
 
 // vertices: nv*3 doubles; faces: nf*3 indices (validated by the caller).
 bool build_bvh(const double* vertices, const int32_t* faces, int64_t nf, const BvhBuildParams& prm,

@@ -69,18 +69,6 @@ struct alignas(16) BvhNode {
 };
 static_assert(sizeof(BvhNode) == 64, "BvhNode must be 64 bytes");
 
-// BVH4 node for the float32 kernel (collapsed from the SAH BVH2, same
-// conservative fp32 boxes): four child boxes in SoA form, 128 bytes = two
-// s_load_dwordx16. count[k] > 0: leaf with triangles [child[k], +count[k]);
-// count[k] == 0: internal node child[k]; count[k] < 0: empty slot.
-struct alignas(16) Bvh4Node {
-  float lo[3][4];   // lo[axis][child]
-  float hi[3][4];
-  int32_t child[4];
-  int32_t count[4];
-};
-static_assert(sizeof(Bvh4Node) == 128, "Bvh4Node must be 128 bytes");
-
 struct alignas(16) TriF32 {
   float v0[3];
   int32_t id;    // original face index (tie-break + normal lookup)
@@ -90,6 +78,21 @@ struct alignas(16) TriF32 {
   float pad2;
 };
 static_assert(sizeof(TriF32) == 48, "TriF32 must be 48 bytes");
+
+// float32 kernel triangle (rt_fast.h tri_test): 64 bytes = ONE
+// s_load_dwordx16. e2 = v2 - v0, e1n = -(v1 - v0), nn = -(e1 x e2), the
+// cross product formed in float64 from the float64 edges, then rounded.
+struct alignas(16) TriFast {
+  float v0[3];
+  int32_t id;    // original face index (tie-break + normal lookup)
+  float e2[3];
+  float pad0;
+  float e1n[3];
+  float pad1;
+  float nn[3];
+  float pad2;
+};
+static_assert(sizeof(TriFast) == 64, "TriFast must be 64 bytes");
 
 struct alignas(16) TriF64 {
   double v0[3];
@@ -165,11 +168,9 @@ static_assert(sizeof(FObjX) == 128, "FObjX must be 128 bytes");
 
 struct alignas(16) FMesh {
   float lo[3];
-  int32_t root;        // BVH4 root (index into nodes4), -1 for an empty mesh
+  int32_t root;        // BVH2 root (index into nodes), -1 for an empty mesh
   float hi[3];
   int32_t normal_base;
-  int32_t root2;       // BVH2 root (index into nodes), -1 for an empty mesh
-  int32_t pad[3];
 };
 
 struct alignas(16) FLight {
@@ -185,8 +186,7 @@ struct FastParams {
   const FMesh* meshes;
   const FLight* lights;
   const BvhNode* nodes;
-  const Bvh4Node* nodes4;
-  const TriF32* tris;
+  const TriFast* tris;
   const float* normals;
   float* fb;
   unsigned long long* partials;
@@ -198,7 +198,7 @@ struct FastParams {
   float inv_len;
   float sample_step, sample_off;
   int32_t nobj, nlight, width, height;
-  int32_t aa_kind, grid_m, spp, max_depth, flags, max_iters;
+  int32_t aa_kind, grid_m, spp, max_depth, flags, shadow_mesh;
   int32_t mode, y0, nrows, ncols, step, max_step, band_h, rank, world;
   int32_t lanes_per_px, log2_lanes, tile_x, tile_y, tiles_x, ngroups;
 };

@@ -28,12 +28,6 @@
 #endif
 #endif
 
-#ifndef RTMI_BVH4
-#define RTMI_BVH4 0
-#endif
-#ifndef RTMI_LEAF_BATCH
-#define RTMI_LEAF_BATCH 0
-#endif
 
 namespace rtmi {
 namespace fast {
@@ -132,45 +126,68 @@ __device__ __forceinline__ float plane(F3 o, F3 d) {
   return fabsf(d.y) > 1e-6f ? -o.y * rcp(d.y) : -finf();
 }
 
-// rayTriangleIntersectFast (geom.nim:283-336), single-sided.
-__device__ __forceinline__ float triangle(const TriF32& tri, F3 o, F3 d) {
-  const float e1x = tri.e1[0], e1y = tri.e1[1], e1z = tri.e1[2];
-  const float e2x = tri.e2[0], e2y = tri.e2[1], e2z = tri.e2[2];
-  const float px = d.y * e2z - d.z * e2y;
-  const float py = d.z * e2x - d.x * e2z;
-  const float pz = d.x * e2y - d.y * e2x;
-  const float det = __builtin_fmaf(e1x, px, __builtin_fmaf(e1y, py, e1z * pz));
-  const float inv_det = rcp(det);
-  const float tx = o.x - tri.v0[0], ty = o.y - tri.v0[1], tz = o.z - tri.v0[2];
-  const float u = __builtin_fmaf(tx, px, __builtin_fmaf(ty, py, tz * pz)) * inv_det;
-  const float qx = ty * e1z - tz * e1y;
-  const float qy = tz * e1x - tx * e1z;
-  const float qz = tx * e1y - ty * e1x;
-  const float v = __builtin_fmaf(d.x, qx, __builtin_fmaf(d.y, qy, d.z * qz)) * inv_det;
-  const float t = __builtin_fmaf(e2x, qx, __builtin_fmaf(e2y, qy, e2z * qz)) * inv_det;
-  const bool ok = det >= 0.000001f && u >= 0.0f && u <= 1.0f && v >= 0.0f && u + v <= 1.0f;
-  return ok ? t : -finf();
+// Closest hit as ONE 64-bit key: float bits of t in the high word, the
+// triangle's face index in the low word. For t >= 0 the float bits order like
+// unsigned integers, so key order is the reference's "smaller t, then lower
+// face index" order (geom.nim:339-358 keeps the first, i.e. lowest-index,
+// face on a tie); a negative or NaN t sorts above +inf and is never accepted.
+// One v_cmp_lt_u64 + three v_cndmask replace the compare/tie-break mask
+// algebra (which cost SALU s_and/s_or per triangle).
+__device__ __forceinline__ unsigned long long tkey(float t, unsigned int lo) {
+  return ((unsigned long long)__float_as_uint(t) << 32) | lo;
 }
 
-// Leaf: closest/any hit over `n` triangles starting at `first` for lanes `h`.
-__device__ __forceinline__ void leaf(const FastParams& p, int first, int n, bool h, F3 o, F3 d, float& tbest,
-                                     int& best_id) {
-  for (int k = 0; k < n; ++k) {
-    const TriF32 tri = cp(p.tris)[first + k];
-    const float t = triangle(tri, o, d);
-    const int id = tri.id;
-    if (h && t >= 0.0f && (t < tbest || (t == tbest && id < best_id))) {
-      tbest = t;
-      best_id = id;
-    }
+// rayTriangleIntersectFast (geom.nim:283-336), single-sided, on the TriFast
+// record (rt_common.h): with c = (o - v0) x d and nn = -(e1 x e2),
+//   det = d.nn, u*det = e2.c, v*det = (-e1).c, t = (o - v0).nn / (-det)
+// (scalar triple-product identities of the reference's p = d x e2,
+// q = tvec x e1 form). The barycentric range is tested unscaled in one min:
+// u >= 0, v >= 0, u + v <= 1 (u <= 1 is implied), det >= 1e-6.
+__device__ __forceinline__ void tri_test(const RT_CONST TriFast& T, F3 o, F3 d, unsigned long long& key,
+                                         float& tc) {
+  const float tx = o.x - T.v0[0], ty = o.y - T.v0[1], tz = o.z - T.v0[2];
+  const float cx = __builtin_fmaf(ty, d.z, -tz * d.y);
+  const float cy = __builtin_fmaf(tz, d.x, -tx * d.z);
+  const float cz = __builtin_fmaf(tx, d.y, -ty * d.x);
+  const float u = __builtin_fmaf(T.e2[0], cx, __builtin_fmaf(T.e2[1], cy, T.e2[2] * cz));
+  const float v = __builtin_fmaf(T.e1n[0], cx, __builtin_fmaf(T.e1n[1], cy, T.e1n[2] * cz));
+  const float det = __builtin_fmaf(T.nn[0], d.x, __builtin_fmaf(T.nn[1], d.y, T.nn[2] * d.z));
+  const float tt = __builtin_fmaf(T.nn[0], tx, __builtin_fmaf(T.nn[1], ty, T.nn[2] * tz));
+  const float t = tt * rcp(-det);
+  const float g = fminf(fminf(fminf(u, v), det - (u + v)), det - 0.000001f);
+  const float ts = g >= 0.0f ? t : -1.0f;
+  const unsigned long long k = tkey(ts, (unsigned int)T.id);
+  const bool acc = k < key;
+  key = acc ? k : key;
+  tc = acc ? ts : tc;
+}
+
+// Leaf: the n (1..kLeafMax, wave-uniform) triangles starting at `first`.
+__device__ __forceinline__ void leaf(const FastParams& p, int first, int n, F3 o, F3 d, unsigned long long& key,
+                                     float& tc) {
+  const RT_CONST TriFast* t = cp(p.tris) + first;
+  tri_test(t[0], o, d, key, tc);
+#pragma unroll
+  for (int k = 1; k < kLeafMax; ++k) {
+    if (k >= n) break;
+    tri_test(t[k], o, d, key, tc);
   }
 }
 
-// Wave-coherent closest/any hit over one mesh BVH2 (64-B nodes, both child
-// boxes per fetch). Selected with -DRTMI_BVH4=0.
+// Wave-coherent closest hit over one mesh BVH2 (64-B nodes, both child boxes
+// per scalar fetch). Per lane: `tc` is the box-culling limit (the current
+// best t; -1 for lanes that take no part, so `active` never enters a lane
+// mask) and `key` the best (t, face) so far. Lanes step through the same node
+// sequence: a child is visited when any lane's ray hits its box; both hit ->
+// the nearer (majority vote) first, the other onto a 64-entry stack held one
+// entry per lane in a single VGPR. Every child reference is valid (the
+// builder never emits an empty child), and no iteration guard is needed: a
+// traversal visits each node at most once.
+// early/stop: exact early exit for shadow rays (trace()): a lane
+// retires once its best t <= stop.
 template <bool COUNT>
-__device__ __forceinline__ void traverse2(const FastParams& p, int root, F3 o, F3 d, bool active, bool anyhit,
-                                          float& tbest, int& best_id, Stats32& ws) {
+__device__ __forceinline__ void traverse(const FastParams& p, int root, F3 o, F3 d, bool active, bool early,
+                                         float stop, float& tbest, int& best_id, Stats32& ws) {
   if (bal(active) == 0ull) return;
   RT_STAMP(t_enter);
   const float e = 1e-20f;
@@ -180,14 +197,21 @@ __device__ __forceinline__ void traverse2(const FastParams& p, int root, F3 o, F
   const F3 ni = f3(rcp(dx), rcp(dy), rcp(dz));
   const F3 oi = f3(o.x * ni.x, o.y * ni.y, o.z * ni.z);
   const int lane = (int)__lane_id();
+  float tc = active ? tbest : -1.0f;
+  // Retire only on a FOUND hit: accepted t are < the initial limit tbest, so
+  // clamp stop to the float just below it (tbest > 0; for tbest == 0 the
+  // bit pattern wraps to NaN, fminf keeps stop, and nothing is acceptable).
+  stop = fminf(stop, __uint_as_float(__float_as_uint(tbest) - 1u));
+  const unsigned long long key0 = active ? tkey(tbest, 0u) : 0ull;
+  unsigned long long key = key0;
   int stack = 0;
   int sp = 0;
   int node = root;
-  for (int iter = 0; iter < p.max_iters; ++iter) {
+  for (;;) {
     const BvhNode nd = cp(p.nodes)[node];
     if constexpr (COUNT) {
       ws.v[STAT_NODE_FETCH] += 1u;
-      ws.v[STAT_LANE_NODES] += pc(bal(active));
+      ws.v[STAT_LANE_NODES] += pc(bal(tc >= 0.0f));
     }
     const float ax0 = __builtin_fmaf(nd.lo0[0], ni.x, -oi.x), bx0 = __builtin_fmaf(nd.hi0[0], ni.x, -oi.x);
     const float ay0 = __builtin_fmaf(nd.lo0[1], ni.y, -oi.y), by0 = __builtin_fmaf(nd.hi0[1], ni.y, -oi.y);
@@ -196,35 +220,36 @@ __device__ __forceinline__ void traverse2(const FastParams& p, int root, F3 o, F
     const float ay1 = __builtin_fmaf(nd.lo1[1], ni.y, -oi.y), by1 = __builtin_fmaf(nd.hi1[1], ni.y, -oi.y);
     const float az1 = __builtin_fmaf(nd.lo1[2], ni.z, -oi.z), bz1 = __builtin_fmaf(nd.hi1[2], ni.z, -oi.z);
     const float tn0 = fmaxf(fmaxf(fminf(ax0, bx0), fminf(ay0, by0)), fmaxf(fminf(az0, bz0), 0.0f));
-    const float tf0 = fminf(fminf(fmaxf(ax0, bx0), fmaxf(ay0, by0)), fminf(fmaxf(az0, bz0), tbest));
+    const float tf0 = fminf(fminf(fmaxf(ax0, bx0), fmaxf(ay0, by0)), fminf(fmaxf(az0, bz0), tc));
     const float tn1 = fmaxf(fmaxf(fminf(ax1, bx1), fminf(ay1, by1)), fmaxf(fminf(az1, bz1), 0.0f));
-    const float tf1 = fminf(fminf(fmaxf(ax1, bx1), fmaxf(ay1, by1)), fminf(fmaxf(az1, bz1), tbest));
-    const bool h0 = active && tn0 <= tf0 * 1.0000004f;
-    const bool h1 = active && tn1 <= tf1 * 1.0000004f;
-    unsigned long long m0 = (nd.n0 > 0 || nd.c0 >= 0) ? bal(h0) : 0ull;
-    unsigned long long m1 = (nd.n1 > 0 || nd.c1 >= 0) ? bal(h1) : 0ull;
-    if (nd.n0 > 0 && m0) {
-      if constexpr (COUNT) {
-        ws.v[STAT_TRI_FETCH] += (unsigned int)nd.n0;
-        ws.v[STAT_LANE_TRIS] += pc(m0) * (unsigned int)nd.n0;
+    const float tf1 = fminf(fminf(fmaxf(ax1, bx1), fmaxf(ay1, by1)), fminf(fmaxf(az1, bz1), tc));
+    unsigned long long m0 = bal(tn0 <= tf0 * 1.0000004f);
+    unsigned long long m1 = bal(tn1 <= tf1 * 1.0000004f);
+    if (nd.n0 > 0) {
+      if (m0) {
+        if constexpr (COUNT) {
+          ws.v[STAT_TRI_FETCH] += (unsigned int)nd.n0;
+          ws.v[STAT_LANE_TRIS] += pc(m0) * (unsigned int)nd.n0;
+        }
+        leaf(p, nd.c0, nd.n0, o, d, key, tc);
+        if (early) tc = tc <= stop ? -1.0f : tc;
       }
-      leaf(p, nd.c0, nd.n0, h0, o, d, tbest, best_id);
-      if (anyhit) active = active && best_id < 0;
       m0 = 0ull;
     }
-    if (nd.n1 > 0 && m1) {
-      if constexpr (COUNT) {
-        ws.v[STAT_TRI_FETCH] += (unsigned int)nd.n1;
-        ws.v[STAT_LANE_TRIS] += pc(m1) * (unsigned int)nd.n1;
+    if (nd.n1 > 0) {
+      if (m1) {
+        if constexpr (COUNT) {
+          ws.v[STAT_TRI_FETCH] += (unsigned int)nd.n1;
+          ws.v[STAT_LANE_TRIS] += pc(m1) * (unsigned int)nd.n1;
+        }
+        leaf(p, nd.c1, nd.n1, o, d, key, tc);
+        if (early) tc = tc <= stop ? -1.0f : tc;
       }
-      leaf(p, nd.c1, nd.n1, h1, o, d, tbest, best_id);
-      if (anyhit) active = active && best_id < 0;
       m1 = 0ull;
     }
-    if (anyhit && bal(active) == 0ull) break;
     if (m0 && m1) {
-      const unsigned long long near0 = bal(h0 && h1 && tn0 <= tn1);
-      const bool first0 = pc(near0) * 2u >= pc(m0 & m1);
+      const unsigned long long both = m0 & m1;
+      const bool first0 = pc(bal(tn0 <= tn1) & both) * 2u >= pc(both);
       const int near = first0 ? nd.c0 : nd.c1;
       const int far = first0 ? nd.c1 : nd.c0;
       stack = (lane == sp) ? far : stack;
@@ -236,143 +261,61 @@ __device__ __forceinline__ void traverse2(const FastParams& p, int root, F3 o, F
       node = nd.c1;
     } else {
       if (sp == 0) break;
+      if (early && bal(tc >= 0.0f) == 0ull) break;
       --sp;
       node = __builtin_amdgcn_readlane(stack, sp);
     }
+  }
+  if (key != key0) {
+    tbest = __uint_as_float((unsigned int)(key >> 32));
+    best_id = (int)(unsigned int)key;
   }
 #ifdef RTMI_STAMPS
   { RT_STAMP(t_exit); RT_ACC(5, t_enter, t_exit); }
 #endif
 }
 
-__device__ __forceinline__ void cswap(unsigned& ka, int& ca, unsigned& kb, int& cb) {
-  const bool sw = kb < ka;
-  const unsigned k = sw ? kb : ka;
-  const int c = sw ? cb : ca;
-  kb = sw ? ka : kb;
-  cb = sw ? ca : cb;
-  ka = k;
-  ca = c;
+// t of analytic object i in world space, -inf on a miss (Sphere / Plane /
+// Box .intersect, geom.nim:215-248, 76-96).
+__device__ __forceinline__ float analytic_t(const FastParams& p, const FObj& ob, int i, F3 o, F3 d) {
+  F3 ro, rd;
+  to_object(p, ob, i, o, d, ro, rd);
+  if (ob.type == GEOM_PLANE) return plane(ro, rd);
+  if (ob.type == GEOM_SPHERE) return sphere(ob.r, ro, rd);
+  return aabb(ob.lo, ob.hi, ro, f3(rcp(rd.x), rcp(rd.y), rcp(rd.z)));
 }
 
-// Wave-coherent closest/any hit over one mesh's BVH4 (rt_common.h Bvh4Node).
-// The node index and the stack are wave-uniform: one 128-B node is fetched
-// with scalar loads, every lane tests the four child boxes against its own
-// ray (four independent slab tests: ILP), ballots decide which children the
-// wave visits, leaves are tested immediately, internal children are ordered
-// by the lead lane's entry distance (a scalar sorting network on the float
-// bits; entry distances are >= 0) and all but the nearest are pushed onto
-// the 64-lane VGPR stack. Must be called from wave-uniform control flow.
+// trace (renderer.nim:47-67): linear closest hit over the objects in order;
+// an object counts as a hit only when it beats the running minimum.
+//
+// Shadow rays only need (a) whether any object is hit below tmax and (b) the
+// reference's hit count, in which an object after the mesh is counted only if
+// its t beats the mesh's closest t. So once a lane has found a mesh hit at
+// t <= stop = min t of the analytic objects after the mesh, every later
+// comparison is decided and the lane retires: exact, not an approximation.
+// Applied when the scene has exactly one mesh object (p.shadow_mesh).
 template <bool COUNT>
-__device__ __forceinline__ void traverse4(const FastParams& p, int root, F3 o, F3 d, bool active, bool anyhit,
-                                          float& tbest, int& best_id, Stats32& ws) {
-  if (bal(active) == 0ull) return;
-  RT_STAMP(t_enter);
-  const float e = 1e-20f;
-  const float dx = fabsf(d.x) < e ? __builtin_copysignf(e, d.x) : d.x;
-  const float dy = fabsf(d.y) < e ? __builtin_copysignf(e, d.y) : d.y;
-  const float dz = fabsf(d.z) < e ? __builtin_copysignf(e, d.z) : d.z;
-  const F3 ni = f3(rcp(dx), rcp(dy), rcp(dz));
-  const F3 oi = f3(o.x * ni.x, o.y * ni.y, o.z * ni.z);
-  const int lane = (int)__lane_id();
-  int stack = 0;
-  int sp = 0;
-  int node = root;
-  for (int iter = 0; iter < p.max_iters; ++iter) {
-    RT_STAMP(t_node);
-    const Bvh4Node nd = cp(p.nodes4)[node];
-    if constexpr (COUNT) {
-      ws.v[STAT_NODE_FETCH] += 1u;
-      ws.v[STAT_LANE_NODES] += pc(bal(active));
-    }
-    float tn[4];
-    bool h[4];
-    unsigned long long m[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const float ax = __builtin_fmaf(nd.lo[0][k], ni.x, -oi.x), bx = __builtin_fmaf(nd.hi[0][k], ni.x, -oi.x);
-      const float ay = __builtin_fmaf(nd.lo[1][k], ni.y, -oi.y), by = __builtin_fmaf(nd.hi[1][k], ni.y, -oi.y);
-      const float az = __builtin_fmaf(nd.lo[2][k], ni.z, -oi.z), bz = __builtin_fmaf(nd.hi[2][k], ni.z, -oi.z);
-      tn[k] = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fmaxf(fminf(az, bz), 0.0f));
-      const float tf = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fminf(fmaxf(az, bz), tbest));
-      h[k] = active && tn[k] <= tf * 1.0000004f;
-      m[k] = nd.count[k] >= 0 ? bal(h[k]) : 0ull;
-    }
-#ifdef RTMI_STAMPS
-    { RT_STAMP(t_slab); RT_ACC(8, t_node, t_slab); }
-#endif
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      if (nd.count[k] > 0 && m[k]) {
-        RT_STAMP(t_leaf);
-        if constexpr (COUNT) {
-          ws.v[STAT_TRI_FETCH] += (unsigned int)nd.count[k];
-          ws.v[STAT_LANE_TRIS] += pc(m[k]) * (unsigned int)nd.count[k];
-        }
-        leaf(p, nd.child[k], nd.count[k], h[k], o, d, tbest, best_id);
-        if (anyhit) active = active && best_id < 0;
-        m[k] = 0ull;
-#ifdef RTMI_STAMPS
-        { RT_STAMP(t_leaf_end); RT_ACC(6, t_leaf, t_leaf_end); }
-#endif
-      }
-    }
-    if (anyhit && bal(active) == 0ull) break;
-    // order the internal children hit by any lane
-    const unsigned long long live = bal(active);
-    const int lead = live ? (int)__builtin_ctzll(live) : 0;
-    unsigned key[4];
-    int cn[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const unsigned tk = (unsigned)__builtin_amdgcn_readlane(__float_as_int(tn[k]), lead);
-      key[k] = m[k] ? (((m[k] >> lead) & 1ull) ? tk : 0x7f000000u) : 0xffffffffu;
-      cn[k] = nd.child[k];
-    }
-    cswap(key[0], cn[0], key[1], cn[1]);
-    cswap(key[2], cn[2], key[3], cn[3]);
-    cswap(key[0], cn[0], key[2], cn[2]);
-    cswap(key[1], cn[1], key[3], cn[3]);
-    cswap(key[1], cn[1], key[2], cn[2]);
-    if (key[0] == 0xffffffffu) {
-      if (sp == 0) break;
-      --sp;
-      node = __builtin_amdgcn_readlane(stack, sp);
-    } else {
-      node = cn[0];
-#pragma unroll
-      for (int k = 3; k >= 1; --k) {
-        if (key[k] != 0xffffffffu) {
-          stack = (lane == sp) ? cn[k] : stack;
-          ++sp;
-        }
-      }
-    }
-  }
-#ifdef RTMI_STAMPS
-  { RT_STAMP(t_exit); RT_ACC(5, t_enter, t_exit); }
-#endif
-}
-
-// trace (renderer.nim:47-67): linear closest hit over the objects in order.
-template <bool COUNT>
-__device__ __forceinline__ Hit trace(const FastParams& p, F3 o, F3 d, float tmax, bool active, bool anyhit,
+__device__ __forceinline__ Hit trace(const FastParams& p, F3 o, F3 d, float tmax, bool active, bool shadow,
                                      Stats32& ws) {
   Hit h{-1, -1, tmax};
-  ws.v[STAT_TESTS] += pc(bal(active)) * (unsigned int)p.nobj;
+  const bool early = shadow && p.shadow_mesh >= 0;
+  float stop = -1.0f;
+  if (early) {
+    stop = finf();
+    for (int i = p.shadow_mesh + 1; i < p.nobj; ++i) {
+      const float t = analytic_t(p, cp(p.objs)[i], i, o, d);
+      stop = t >= 0.0f ? fminf(stop, t) : stop;
+    }
+  }
   for (int i = 0; i < p.nobj; ++i) {
     const FObj ob = cp(p.objs)[i];
-    F3 ro, rd;
-    to_object(p, ob, i, o, d, ro, rd);
     float t;
     int tri = -1;
-    if (ob.type == GEOM_PLANE) {
-      t = plane(ro, rd);
-    } else if (ob.type == GEOM_SPHERE) {
-      t = sphere(ob.r, ro, rd);
-    } else if (ob.type == GEOM_BOX) {
-      t = aabb(ob.lo, ob.hi, ro, f3(rcp(rd.x), rcp(rd.y), rcp(rd.z)));
+    if (ob.type != GEOM_MESH) {
+      t = analytic_t(p, ob, i, o, d);
     } else {
+      F3 ro, rd;
+      to_object(p, ob, i, o, d, ro, rd);
       const FMesh m = cp(p.meshes)[ob.mesh];
       // TriangleMesh.intersect (geom.nim:339-358): a ray starting inside
       // the mesh AABB misses; otherwise the closest face.
@@ -380,11 +323,7 @@ __device__ __forceinline__ Hit trace(const FastParams& p, F3 o, F3 d, float tmax
       const bool in = gate >= 0.0f;
       float tb = h.t;
       int best = -1;
-#if RTMI_BVH4
-      if (m.root >= 0) traverse4<COUNT>(p, m.root, ro, rd, active && in, anyhit, tb, best, ws);
-#else
-      if (m.root2 >= 0) traverse2<COUNT>(p, m.root2, ro, rd, active && in, anyhit, tb, best, ws);
-#endif
+      if (m.root >= 0) traverse<COUNT>(p, m.root, ro, rd, active && in, early && i == p.shadow_mesh, stop, tb, best, ws);
       t = !in ? -finf() : (best >= 0 ? tb : finf());
       tri = best;
     }
@@ -430,7 +369,6 @@ __device__ __forceinline__ F3 analytic_normal(const FObj& ob, F3 ho) {
 // loop of levels with forward weights.
 template <bool COUNT>
 __device__ __forceinline__ F3 shade_path(const FastParams& p, F3 o, F3 d, bool active, Stats32& ws) {
-  const bool anyhit_shadows = (p.flags & RT_DEV_FLAG_ANYHIT) != 0;
   bool act = active;
   int depth = 1;
   F3 acc = f3(0.0f, 0.0f, 0.0f);
@@ -438,9 +376,6 @@ __device__ __forceinline__ F3 shade_path(const FastParams& p, F3 o, F3 d, bool a
   for (int lev = 0; lev < kMaxShadeLevels; ++lev) {
     if (bal(act) == 0ull) break;
     const Hit hit = trace<COUNT>(p, o, d, finf(), act, false, ws);
-#ifdef RTMI_EXP_PRIMARY_ONLY
-    return f3(hit.t, (float)hit.obj, (float)hit.tri);
-#endif
     if (act && hit.obj < 0) acc = f3(acc.x + w * p.bg[0], acc.y + w * p.bg[1], acc.z + w * p.bg[2]);
     const bool lit = act && hit.obj >= 0;
     const F3 hw = f3(__builtin_fmaf(d.x, hit.t, o.x), __builtin_fmaf(d.y, hit.t, o.y), __builtin_fmaf(d.z, hit.t, o.z));
@@ -498,7 +433,7 @@ __device__ __forceinline__ F3 shade_path(const FastParams& p, F3 o, F3 d, bool a
         dist = finf();
       }
       ws.v[STAT_SHADOW] += pc(bal(lit));
-      const Hit sh = trace<COUNT>(p, so, sd, dist, lit, anyhit_shadows, ws);
+      const Hit sh = trace<COUNT>(p, so, sd, dist, lit, true, ws);
       if (lit && sh.obj < 0) {  // shadeDiffuse (shader.nim:12-17)
         const float ndl = fmaxf(dot3(N, sd), 0.0f);
         local = f3(__builtin_fmaf(alb.x * I.x, ndl, local.x), __builtin_fmaf(alb.y * I.y, ndl, local.y),

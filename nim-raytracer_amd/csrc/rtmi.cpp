@@ -98,7 +98,7 @@ struct FastData {
   DevBuf<FObjX> objx;
   DevBuf<FMesh> meshes;
   DevBuf<FLight> lights;
-  DevBuf<TriF32> tris;
+  DevBuf<TriFast> tris;
   DevBuf<float> normals;
   void release() {
     objs.release();
@@ -130,6 +130,7 @@ struct rt_scene {
   hipStream_t stream = nullptr;
   hipEvent_t done = nullptr;
   int32_t nobj = 0, nlight = 0, nmesh = 0;
+  int32_t shadow_mesh = -1;  // the only mesh object, or -1 (FastParams.shadow_mesh)
   bool any_reflective = false;
   double fov = 50.0;
   double c2w[16];
@@ -137,7 +138,6 @@ struct rt_scene {
   FastData f32;
   PrecisionData<double> f64;
   DevBuf<BvhNode> nodes;
-  DevBuf<Bvh4Node> nodes4;
   DevBuf<unsigned long long> partials;
   DevBuf<unsigned long long> acc;
   DevBuf<float> fb_scratch;
@@ -150,7 +150,6 @@ struct rt_scene {
     f32.release();
     f64.release();
     nodes.release();
-    nodes4.release();
     partials.release();
     acc.release();
     fb_scratch.release();
@@ -369,6 +368,37 @@ void fill_precision(const rt_scene_desc* d, const std::vector<std::vector<double
   }
 }
 
+// float32 kernel triangles (rt_common.h TriFast) in BVH leaf order; edges and
+// the negated face normal formed in float64, then rounded once.
+void fill_fast_tris(const rt_scene_desc* d, const std::vector<BvhResult>& bvhs, std::vector<TriFast>& tris) {
+  tris.clear();
+  for (int m = 0; m < d->num_meshes; ++m) {
+    const rt_mesh_desc& md = d->meshes[m];
+    for (int32_t face : bvhs[(size_t)m].order) {
+      TriFast t{};
+      const int32_t* fi = &md.faces[3 * (size_t)face];
+      const double* v0 = &md.vertices[3 * (size_t)fi[0]];
+      const double* v1 = &md.vertices[3 * (size_t)fi[1]];
+      const double* v2 = &md.vertices[3 * (size_t)fi[2]];
+      double e1[3], e2[3];
+      for (int k = 0; k < 3; ++k) {
+        e1[k] = v1[k] - v0[k];
+        e2[k] = v2[k] - v0[k];
+      }
+      const double n[3] = {e1[1] * e2[2] - e1[2] * e2[1], e1[2] * e2[0] - e1[0] * e2[2],
+                           e1[0] * e2[1] - e1[1] * e2[0]};
+      for (int k = 0; k < 3; ++k) {
+        t.v0[k] = (float)v0[k];
+        t.e2[k] = (float)e2[k];
+        t.e1n[k] = (float)-e1[k];
+        t.nn[k] = (float)-n[k];
+      }
+      t.id = face;
+      tris.push_back(t);
+    }
+  }
+}
+
 // float32 kernel records (rt_common.h FObj/FObjX/FMesh/FLight).
 void fill_fast_records(const rt_scene_desc* d, const std::vector<DevMesh<float>>& dm, std::vector<FObj>& fo,
                        std::vector<FObjX>& fx, std::vector<FMesh>& fm, std::vector<FLight>& fl) {
@@ -403,7 +433,6 @@ void fill_fast_records(const rt_scene_desc* d, const std::vector<DevMesh<float>>
       fm[m].hi[k] = dm[m].hi[k];
     }
     fm[m].root = dm[m].root;
-    fm[m].root2 = dm[m].root;
     fm[m].normal_base = dm[m].normal_base;
   }
   fl.assign((size_t)d->num_lights, FLight{});
@@ -448,8 +477,6 @@ extern "C" int rt_scene_create(const rt_scene_desc* d, rt_scene** out_scene) {
   int64_t ntri = 0, nnodes = 0;
   int maxdepth = 0;
   std::vector<BvhNode> all_nodes;
-  std::vector<Bvh4Node> all_nodes4;
-  std::vector<int32_t> node4_base((size_t)d->num_meshes, -1);
   for (int m = 0; m < d->num_meshes; ++m) {
     const rt_mesh_desc& md = d->meshes[m];
     if (md.num_faces < 0 || md.num_vertices < 0 || (md.num_faces > 0 && (!md.faces || !md.vertices)))
@@ -501,21 +528,6 @@ extern "C" int rt_scene_create(const rt_scene_desc* d, rt_scene** out_scene) {
       if (nd.n1 > 0) nd.c1 += (int32_t)ntri;
       all_nodes.push_back(nd);
     }
-    {  // BVH4 for the float32 kernel
-      std::vector<Bvh4Node> n4;
-      int d4 = 0;
-      const char* err4 = "BVH4 collapse failed";
-      if (!collapse_bvh4(bvhs[(size_t)m], &n4, &d4, &err4)) return fail(RT_E_INVALID, "mesh %d: %s", m, err4);
-      node4_base[(size_t)m] = n4.empty() ? -1 : (int32_t)all_nodes4.size();
-      const int32_t b4 = (int32_t)all_nodes4.size();
-      for (Bvh4Node nd : n4) {
-        for (int k = 0; k < 4; ++k) {
-          if (nd.count[k] == 0) nd.child[k] += b4;
-          else if (nd.count[k] > 0) nd.child[k] += (int32_t)ntri;
-        }
-        all_nodes4.push_back(nd);
-      }
-    }
     ntri += md.num_faces;
     nnodes += (int64_t)bvhs[(size_t)m].nodes.size();
     maxdepth = std::max(maxdepth, bvhs[(size_t)m].max_depth);
@@ -533,6 +545,15 @@ extern "C" int rt_scene_create(const rt_scene_desc* d, rt_scene** out_scene) {
   s->device = dev;
   s->num_cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
   s->nobj = d->num_objects;
+  {
+    int n_mesh_obj = 0;
+    for (int i = 0; i < d->num_objects; ++i)
+      if (d->objects[i].type == RT_MESH) {
+        ++n_mesh_obj;
+        s->shadow_mesh = i;
+      }
+    if (n_mesh_obj != 1) s->shadow_mesh = -1;
+  }
   s->nlight = d->num_lights;
   s->nmesh = d->num_meshes;
   s->any_reflective = any_reflective;
@@ -545,15 +566,16 @@ extern "C" int rt_scene_create(const rt_scene_desc* d, rt_scene** out_scene) {
     std::vector<DevObject<float>> o;
     std::vector<DevLight<float>> l;
     std::vector<DevMesh<float>> m;
-    std::vector<TriF32> t;
+    std::vector<TriF32> t32;
     std::vector<float> n;
-    fill_precision<float>(d, normals, bvhs, node_base, aabbs, o, l, m, t, n);
+    fill_precision<float>(d, normals, bvhs, node_base, aabbs, o, l, m, t32, n);
+    std::vector<TriFast> t;
+    fill_fast_tris(d, bvhs, t);
     std::vector<FObj> fo;
     std::vector<FObjX> fx;
     std::vector<FMesh> fm;
     std::vector<FLight> fl;
     fill_fast_records(d, m, fo, fx, fm, fl);
-    for (size_t k = 0; k < fm.size(); ++k) fm[k].root = node4_base[k];  // BVH4 roots
     int rc;
     if ((rc = s->f32.objs.upload(fo)) || (rc = s->f32.objx.upload(fx)) || (rc = s->f32.meshes.upload(fm)) ||
         (rc = s->f32.lights.upload(fl)) || (rc = s->f32.tris.upload(t)) || (rc = s->f32.normals.upload(n)))
@@ -573,7 +595,6 @@ extern "C" int rt_scene_create(const rt_scene_desc* d, rt_scene** out_scene) {
   }
   int rc = s->nodes.upload(all_nodes);
   if (rc) return rc;
-  if ((rc = s->nodes4.upload(all_nodes4))) return rc;
   s->max_waves = s->num_cus * 8 * 4;  // 8 blocks of 4 waves per CU at most
   if ((rc = s->partials.alloc((size_t)s->max_waves * kStatSlots))) return rc;
   if ((rc = s->acc.alloc(kStatSlots))) return rc;
@@ -606,7 +627,7 @@ extern "C" int rt_scene_get_info(const rt_scene* s, rt_scene_info* out) {
   out->num_bvh_nodes = s->num_nodes;
   out->max_bvh_depth = s->max_depth;
   out->device = s->device;
-  out->device_bytes = (int64_t)(s->f32.bytes() + s->f64.bytes() + s->nodes.bytes() + s->nodes4.bytes() +
+  out->device_bytes = (int64_t)(s->f32.bytes() + s->f64.bytes() + s->nodes.bytes() +
                                 s->partials.bytes() +
                                 s->acc.bytes());
   out->build_ms = s->build_ms;
@@ -683,7 +704,6 @@ void fill_fast(rt_scene* s, const rt_options* o, const Mapping& mp, float* fb, F
   p.meshes = s->f32.meshes.p;
   p.lights = s->f32.lights.p;
   p.nodes = s->nodes.p;
-  p.nodes4 = s->nodes4.p;
   p.tris = s->f32.tris.p;
   p.normals = s->f32.normals.p;
   p.fb = fb;
@@ -717,7 +737,7 @@ void fill_fast(rt_scene* s, const rt_options* o, const Mapping& mp, float* fb, F
   p.spp = spp;
   p.max_depth = o->max_ray_depth;
   p.flags = (int32_t)o->flags;
-  p.max_iters = (int32_t)std::min<int64_t>(INT32_MAX, 2 * s->num_nodes + 16);
+  p.shadow_mesh = s->shadow_mesh;
   p.mode = mp.mode;
   p.y0 = mp.y0;
   p.nrows = mp.nrows;
@@ -832,7 +852,15 @@ int read_stats(rt_scene* s, hipStream_t st, rt_stats* out) {
   HIP_TRY(hipMemcpyAsync(h, s->acc.p, sizeof h, hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
   out->num_primary_rays = h[STAT_PRIMARY];
-  out->num_intersection_tests = h[STAT_TESTS];
+  // renderer.nim:54-56 counts one test per object per trace call, and every
+  // trace call is a primary, shadow or reflection ray: the float32 kernel
+  // leaves the slot at 0 and the count is derived; the float64 kernel still
+  // counts it, which is checked here.
+  const unsigned long long rays = h[STAT_PRIMARY] + h[STAT_SHADOW] + h[STAT_REFL];
+  const unsigned long long tests = (unsigned long long)s->nobj * rays;
+  if (h[STAT_TESTS] != 0 && h[STAT_TESTS] != tests)
+    return fail(RT_E_DEVICE, "inconsistent intersection-test count (%llu vs %llu)", h[STAT_TESTS], tests);
+  out->num_intersection_tests = tests;
   out->num_intersection_hits = h[STAT_HITS];
   out->num_shadow_rays = h[STAT_SHADOW];
   out->num_reflection_rays = h[STAT_REFL];

@@ -51,6 +51,19 @@ def main():
         fb = torch.zeros(opts.width * opts.height * 3, dtype=torch.float32, device="cuda")
         o = opts.to_c()
         times = {p: [] for p in libs}
+        ref_img = None
+        for p, lib, h in zip(libs, L, hs):  # Stats + image agreement across builds
+            st = abi.rt_stats()
+            assert lib.rt_render_lines_device(h, C.byref(o), C.c_void_p(fb.data_ptr()), 0, opts.height, 1, 1,
+                                              C.c_void_p(stream.cuda_stream or None), C.byref(st)) == 0
+            torch.cuda.synchronize()
+            img = fb.cpu()
+            if ref_img is None:
+                ref_img = img
+            d = (img - ref_img).abs()
+            print(f"  {os.path.basename(p)}: stats=({st.num_primary_rays},{st.num_intersection_tests},"
+                  f"{st.num_intersection_hits},{st.num_shadow_rays},{st.num_reflection_rays}) "
+                  f"maxdiff={d.max().item():.3g} frac>2e-3={(d > 2e-3).float().mean().item():.2e}", flush=True)
         for r in range(reps):
             for p, lib, h in zip(libs, L, hs):
                 st = abi.rt_stats()
