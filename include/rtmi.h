@@ -133,9 +133,9 @@ typedef struct rt_options {
   uint32_t reserved;
 } rt_options;
 
-/* Shadow rays may stop at the first occluder (any-hit). The image is
- * identical; num_intersection_hits can then differ from the reference's
- * closest-hit count on scenes where several objects overlap one shadow ray. */
+/* Accepted for compatibility and ignored: shadow rays always stop searching
+ * a mesh once the reference's outcome and hit count are decided (an exact
+ * early exit: image and Stats identical to the closest-hit reference). */
 #define RT_FLAG_ANYHIT_SHADOWS 0x1u
 /* Run the instrumented kernel that also counts BVH node / triangle record
  * fetches (rt_scene_last_counters). Slower; the image and Stats are the same. */

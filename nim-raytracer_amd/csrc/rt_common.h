@@ -21,7 +21,7 @@ enum : int32_t { LIGHT_DISTANT = 0, LIGHT_POINT = 1 };
 // DevObject.xf: what world_to_object is (host-classified, float32 fast paths)
 enum : int32_t { XF_IDENTITY = 0, XF_TRANSLATE = 1, XF_GENERAL = 2 };
 // RenderParams.flags bits
-enum : int32_t { RT_DEV_FLAG_ANYHIT = 0x1, RT_DEV_FLAG_COUNT = 0x2 };
+enum : int32_t { RT_DEV_FLAG_COUNT = 0x2 };
 
 constexpr int kMaxBvhDepth = 60;      // stack fits one 64-lane VGPR
 constexpr int kLeafMax = 4;           // triangles per BVH leaf (arrays padded by kLeafMax-1)
@@ -132,6 +132,7 @@ struct RenderParams {
   int32_t max_depth;
   int32_t flags;
   int32_t max_iters;               // traversal bound: each node entered at most once
+  int32_t shadow_mesh;             // the scene's only mesh object, or -1 (trace early exit)
   // work mapping: rows k in [0, nrows), columns j in [0, ncols), x = j*step.
   int32_t mode;                    // 0: y = y0 + k*step into full image; 1: bands
   int32_t y0, nrows, ncols, step, max_step;

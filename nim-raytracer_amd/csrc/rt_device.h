@@ -260,7 +260,7 @@ __device__ __forceinline__ void slab2(const RT_CONST BvhNode& nd, V3<R> o, V3<R>
 template <class R, bool COUNT>
 __device__ __forceinline__ void leaf(const RenderParams<R>& p, int first, int count, bool h,
                                      V3<R> o, V3<R> d, R& tbest, int& best_id, bool& active,
-                                     bool anyhit, WaveStats& ws) {
+                                     bool early, R stop, WaveStats& ws) {
   using Tri = typename TriOf<R>::type;
   if constexpr (COUNT) {
     ws.v[STAT_TRI_FETCH] += (unsigned int)count;
@@ -276,12 +276,13 @@ __device__ __forceinline__ void leaf(const RenderParams<R>& p, int first, int co
       best_id = id;
     }
   }
-  if (anyhit) active = active && best_id < 0;
+  // exact shadow early exit (see trace): retire on a found hit at t <= stop
+  if (early) active = active && !(best_id >= 0 && tbest <= stop);
 }
 
 template <class R, bool COUNT>
 __device__ __forceinline__ void traverse(const RenderParams<R>& p, int root, V3<R> o, V3<R> d,
-                                         bool active, bool anyhit, R& tbest, int& best_id,
+                                         bool active, bool early, R stop, R& tbest, int& best_id,
                                          WaveStats& ws) {
   if (ballot(active) == 0ull || root < 0) return;
   V3<R> ninv, oi;
@@ -315,14 +316,14 @@ __device__ __forceinline__ void traverse(const RenderParams<R>& p, int root, V3<
     unsigned long long m0 = (n0 > 0 || c0 >= 0) ? ballot(h0) : 0ull;
     unsigned long long m1 = (n1 > 0 || c1 >= 0) ? ballot(h1) : 0ull;
     if (n0 > 0 && m0) {
-      leaf<R, COUNT>(p, c0, n0, h0, o, d, tbest, best_id, active, anyhit, ws);
+      leaf<R, COUNT>(p, c0, n0, h0, o, d, tbest, best_id, active, early, stop, ws);
       m0 = 0;
     }
     if (n1 > 0 && m1) {
-      leaf<R, COUNT>(p, c1, n1, h1, o, d, tbest, best_id, active, anyhit, ws);
+      leaf<R, COUNT>(p, c1, n1, h1, o, d, tbest, best_id, active, early, stop, ws);
       m1 = 0;
     }
-    if (anyhit && ballot(active) == 0ull) break;
+    if (early && ballot(active) == 0ull) break;
     if (m0 && m1) {
       const unsigned long long both = m0 & m1;
       const unsigned long long near0 = ballot(h0 && h1 && tn0 <= tn1);
@@ -375,13 +376,47 @@ __device__ __forceinline__ void to_object(const RT_CONST DevObject<R>& ob, V3<R>
   rd = xform<R>(ob.w2o, d, R(0));
 }
 
+// t of an analytic object (plane / sphere / box) in its object space.
+template <class R>
+__device__ __forceinline__ R analytic_t(const RT_CONST DevObject<R>& ob, int type, ORay<R>& r) {
+  if (type == GEOM_PLANE) return plane_ref<R>(r);
+  if (type == GEOM_SPHERE) return sphere_ref<R>(ob.prm[0], r);
+  if (type == GEOM_BOX) {
+    r.inv = V3<R>{Prec<R>::rcp(r.d.x), Prec<R>::rcp(r.d.y), Prec<R>::rcp(r.d.z)};
+    return aabb_ref<R>(V3<R>{ob.prm[0], ob.prm[1], ob.prm[2]}, V3<R>{ob.prm[4], ob.prm[5], ob.prm[6]}, r);
+  }
+  return -pinf<R>();
+}
+
 // Linear closest hit over the scene's objects in order, for lanes with
 // `active`; tmin starts at t_near. Wave-uniform control flow only.
+//
+// Shadow rays (`shadow`) use an EXACT early exit when the scene has one mesh
+// object (p.shadow_mesh): the caller needs only whether anything is hit and
+// the reference's hit count, in which an object after the mesh counts only
+// if its t beats the mesh's closest t. Once a lane holds a mesh hit at
+// t <= stop = min t (>= 0) over the analytic objects after the mesh, every
+// later comparison is decided, so the lane stops searching for a closer face.
 template <class R, bool COUNT>
 __device__ __forceinline__ Hit<R> trace(const RenderParams<R>& p, V3<R> o, V3<R> d, R t_near,
-                                        bool active, bool anyhit, WaveStats& ws) {
+                                        bool active, bool shadow, WaveStats& ws) {
   Hit<R> h{-1, -1, t_near};
   ws.v[STAT_TESTS] += popc32(ballot(active)) * (unsigned int)p.nobj;
+  const bool early = shadow && p.shadow_mesh >= 0;
+  R stop = -pinf<R>();
+  if (early) {
+    stop = pinf<R>();
+    for (int i = p.shadow_mesh + 1; i < p.nobj; ++i) {
+      const RT_CONST DevObject<R>& ob = cptr(p.objects)[i];
+      V3<R> ro, rd;
+      to_object<R>(ob, o, d, ro, rd);
+      ORay<R> r;
+      r.o = ro;
+      r.d = rd;
+      const R t = analytic_t<R>(ob, ob.type, r);
+      if (t >= R(0) && t < stop) stop = t;
+    }
+  }
   for (int i = 0; i < p.nobj; ++i) {
     const RT_CONST DevObject<R>& ob = cptr(p.objects)[i];
     const int type = ob.type;
@@ -392,14 +427,9 @@ __device__ __forceinline__ Hit<R> trace(const RenderParams<R>& p, V3<R> o, V3<R>
     r.d = rd;
     R t;
     int tri = -1;
-    if (type == GEOM_PLANE) {
-      t = plane_ref<R>(r);
-    } else if (type == GEOM_SPHERE) {
-      t = sphere_ref<R>(ob.prm[0], r);
-    } else if (type == GEOM_BOX) {
-      r.inv = V3<R>{Prec<R>::rcp(rd.x), Prec<R>::rcp(rd.y), Prec<R>::rcp(rd.z)};
-      t = aabb_ref<R>(V3<R>{ob.prm[0], ob.prm[1], ob.prm[2]}, V3<R>{ob.prm[4], ob.prm[5], ob.prm[6]}, r);
-    } else if (type == GEOM_MESH) {
+    if (type != GEOM_MESH) {
+      t = analytic_t<R>(ob, type, r);
+    } else {
       r.inv = V3<R>{Prec<R>::rcp(rd.x), Prec<R>::rcp(rd.y), Prec<R>::rcp(rd.z)};
       const RT_CONST DevMesh<R>& m = cptr(p.meshes)[ob.mesh];
       // TriangleMesh.intersect (geom.nim:339-358): AABB gate (tmin < 0 ->
@@ -408,11 +438,9 @@ __device__ __forceinline__ Hit<R> trace(const RenderParams<R>& p, V3<R> o, V3<R>
       const bool in = active && gate >= R(0);
       R tb = h.t;
       int best = -1;
-      traverse<R, COUNT>(p, m.root, r.o, r.d, in, anyhit, tb, best, ws);
+      traverse<R, COUNT>(p, m.root, r.o, r.d, in, early && i == p.shadow_mesh, stop, tb, best, ws);
       t = !(gate >= R(0)) ? -pinf<R>() : (best >= 0 ? tb : pinf<R>());
       tri = best;
-    } else {
-      t = -pinf<R>();
     }
     const bool upd = active && t >= R(0) && t < h.t;
     ws.v[STAT_HITS] += popc32(ballot(upd));
@@ -462,7 +490,6 @@ __device__ __forceinline__ V3<R> object_normal(const RT_CONST DevObject<R>& ob, 
 template <class R, bool COUNT>
 __device__ __forceinline__ V3<R> shade_path(const RenderParams<R>& p, V3<R> o, V3<R> d, bool active,
                                             WaveStats& ws) {
-  const bool anyhit_shadows = (p.flags & RT_DEV_FLAG_ANYHIT) != 0;
   constexpr R kPi = R(3.14159265358979323846);
   bool act = active;
   int depth = 1;
@@ -538,7 +565,7 @@ __device__ __forceinline__ V3<R> shade_path(const RenderParams<R>& p, V3<R> o, V
       const V3<R> sd{ldir.x * R(-1), ldir.y * R(-1), ldir.z * R(-1)};
       const V3<R> so{hw.x + N.x * p.bias, hw.y + N.y * p.bias, hw.z + N.z * p.bias};
       ws.v[STAT_SHADOW] += popc32(ballot(lit));
-      const Hit<R> sh = trace<R, COUNT>(p, so, sd, dist, lit, anyhit_shadows, ws);
+      const Hit<R> sh = trace<R, COUNT>(p, so, sd, dist, lit, true, ws);
       if (lit && sh.obj < 0) {  // shadeDiffuse (shader.nim:12-17)
         const R ndl = nmax(R(0), dot4(N, R(0), sd, R(0) * R(-1)));
         local.x = local.x + Prec<R>::div(alb.x, kPi) * I.x * ndl;

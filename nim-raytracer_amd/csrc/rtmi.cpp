@@ -790,6 +790,7 @@ void fill_params(rt_scene* s, const PrecisionData<R>& pd, const rt_options* o, c
   p.spp = spp;
   p.max_depth = o->max_ray_depth;
   p.flags = (int32_t)o->flags;
+  p.shadow_mesh = s->shadow_mesh;
   p.max_iters = (int32_t)std::min<int64_t>(INT32_MAX, 2 * s->num_nodes + 16);
   p.mode = mp.mode;
   p.y0 = mp.y0;

@@ -210,6 +210,55 @@ def torus_scene(U=1000, V=500):
     return _mesh_scene(torus_mesh(U, V), "torus", (0.9, 0.5, 0.2))
 
 
+def _placed(mesh, t):
+    from .glm import inverse
+    mesh.objectToWorld = translate(mat4(1.0), vec3(*t))
+    mesh.worldToObject = inverse(mesh.objectToWorld)
+    return mesh
+
+
+def mesh_mix():
+    """Test scene (not one of the reference's): a small reflective mesh with
+    analytic objects before AND after it in object order, lit by a point light
+    above and a distant light. Shadow rays cross the mesh and then a later
+    sphere (or a later sphere first), which exercises the exact shadow early
+    exit's stop distance (rt_fast.h / rt_device.h trace) against the oracle's
+    plain closest-hit loop."""
+    objects = [
+        Object("ballA", initSphere(r=1.0, objectToWorld=translate(mat4(1.0), vec3(-4.0, 1.0, -9.0))),
+               Material(albedo=vec3(0.9, 0.3, 0.2))),
+        Object("torus", _placed(torus_mesh(24, 12), (0.0, 0.0001, -12.0)),
+               Material(albedo=vec3(0.9, 0.5, 0.2), reflection=0.5)),
+        Object("ballB", initSphere(r=1.0, objectToWorld=translate(mat4(1.0), vec3(0.0, 9.0, -12.0))),
+               Material(albedo=vec3(0.2, 0.5, 0.9))),
+        Object("ballD", initSphere(r=0.8, objectToWorld=translate(mat4(1.0), vec3(2.5, 0.8, -10.0))),
+               Material(albedo=vec3(0.6, 0.9, 0.2))),
+        Object("boxC", initBox(objectToWorld=translate(mat4(1.0), vec3(4.0, 0.0, -13.0)),
+                               vmin=vec(-1.0, 0.0, -1.0), vmax=vec(1.0, 2.0, 1.0)),
+               Material(albedo=vec3(0.5))),
+        Object("ground", initPlane(objectToWorld=mat4(1.0)), Material(albedo=vec3(0.4))),
+    ]
+    lights = [
+        PointLight(color=vec3(1.0, 1.0, 1.0), intensity=4000.0, pos=point(0.5, 14.0, -12.0)),
+        _warm_lights()[0],
+    ]
+    return Scene(objects=objects, lights=lights, fov=50.0, cameraToWorld=_std_camera(0.0, 5.5, 1.5),
+                 bgColor=vec3(0.01, 0.03, 0.05))
+
+
+def two_meshes():
+    """Test scene: two mesh objects (the shadow early exit is off: with a
+    second mesh later in object order its closest t is not known in advance)."""
+    objects = [
+        Object("torus1", _placed(torus_mesh(24, 12), (1.5, 0.0001, -12.0)), Material(albedo=vec3(0.9, 0.5, 0.2))),
+        Object("torus2", _placed(torus_mesh(16, 8, R=1.5, r=0.5), (-3.0, 0.0001, -9.0)),
+               Material(albedo=vec3(0.2, 0.5, 0.9))),
+        Object("ground", initPlane(objectToWorld=mat4(1.0)), Material(albedo=vec3(0.4))),
+    ]
+    return Scene(objects=objects, lights=_warm_lights(), fov=50.0, cameraToWorld=_std_camera(0.0, 5.5, 1.5),
+                 bgColor=vec3(0.01, 0.03, 0.05))
+
+
 SCENES = {
     "spheres-warm": spheres_warm,
     "spheres-warm-3": lambda: spheres_warm(3),
@@ -219,4 +268,6 @@ SCENES = {
     "spheres-pointlight1": spheres_pointlight1,
     "mesh-bunny": mesh_bunny,
     "torus": torus_scene,
+    "mesh-mix": mesh_mix,
+    "two-meshes": two_meshes,
 }

@@ -54,6 +54,8 @@ CASES = [
     ("spheres-reflection", 160, 120, akNone, 1),
     ("spheres-pointlight1", 96, 64, akNone, 1),
     ("boxtest", 120, 80, akNone, 1),
+    ("mesh-mix", 96, 64, akNone, 1),           # shadow early exit with later objects
+    ("two-meshes", 96, 64, akGrid, 2),         # early exit disabled (two meshes)
 ]
 
 

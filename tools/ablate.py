@@ -3,7 +3,7 @@ import sys, os, json, dataclasses
 sys.path.insert(0, 'nim-raytracer_amd')
 import torch
 from rtmi import Antialias, Options, Precision, akGrid, scenes
-from rtmi.abi import RT_FLAG_ANYHIT_SHADOWS, RT_FLAG_COUNT_TRAVERSAL
+from rtmi.abi import RT_FLAG_COUNT_TRAVERSAL
 from rtmi.renderer import DeviceScene
 
 def timeit(ds, opts, n=5):
@@ -26,7 +26,6 @@ base = scenes.mesh_bunny()
 opts = Options(width=1920, height=1080, antialias=Antialias(akGrid, 16), bias=1e-4, precision=Precision.fp32)
 variants = {}
 variants['c3_full'] = (base, opts)
-variants['c3_anyhit'] = (base, dataclasses.replace(opts, flags=RT_FLAG_ANYHIT_SHADOWS))
 s = scenes.mesh_bunny(); s.lights = []; variants['c3_nolights'] = (s, opts)
 s = scenes.mesh_bunny(); s.lights = s.lights[:1]; variants['c3_1light'] = (s, opts)
 s = scenes.mesh_bunny(); s.objects = [s.objects[1]]; variants['ground_only'] = (s, opts)
