@@ -35,7 +35,7 @@ sys.path.insert(0, os.path.join(REPO, "nim-raytracer_amd"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md "Chip-level parameters")
 NODE_BYTES = 64        # one BvhNode record (two child boxes + refs)
-TRI_BYTES = 48         # one TriF32 record (v0, e1, e2, face id)
+TRI_BYTES = 64         # one TriFast record (v0, e2, -e1, -n, face id)
 BAND_H = 16
 
 

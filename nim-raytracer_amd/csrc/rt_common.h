@@ -191,6 +191,7 @@ struct FastParams {
   const float* normals;
   float* fb;
   unsigned long long* partials;
+  unsigned int* queue;             // kQueueShards heads (atomicAdd), zeroed at launch
   float cam[12];       // origin, C2W column 0, 1, 2 (xyz each)
   float cam_a, cam_b;  // cx = (px - cam_b) * cam_a, cam_b = w/2   (renderer.nim:39)
   float cam_c, cam_d;  // cy = (cam_d - py) * cam_c, cam_d = h/2   (renderer.nim:40)
@@ -199,7 +200,7 @@ struct FastParams {
   float inv_len;
   float sample_step, sample_off;
   int32_t nobj, nlight, width, height;
-  int32_t aa_kind, grid_m, spp, max_depth, flags, shadow_mesh;
+  int32_t aa_kind, grid_m, spp, max_depth, flags, shadow_mesh, chunk, shards;
   int32_t mode, y0, nrows, ncols, step, max_step, band_h, rank, world;
   int32_t lanes_per_px, log2_lanes, tile_x, tile_y, tiles_x, ngroups;
 };
@@ -208,6 +209,8 @@ enum : int32_t {
   STAT_PRIMARY = 0, STAT_TESTS = 1, STAT_HITS = 2, STAT_SHADOW = 3, STAT_REFL = 4,
   STAT_NODE_FETCH = 5, STAT_TRI_FETCH = 6, STAT_LANE_NODES = 7, STAT_LANE_TRIS = 8
 };
+// float32 kernel work queue: 8 head words, 128 B apart, zeroed per launch
+constexpr int kQueueShards = 8, kQueueStride = 32;
 
 }  // namespace rtmi
 
@@ -215,6 +218,7 @@ enum : int32_t {
 extern "C" {
 int rtmi_launch_render_f32(const rtmi::FastParams* p, int blocks, void* stream);
 int rtmi_launch_render_f64(const rtmi::RenderParams<double>* p, int blocks, void* stream);
+int rtmi_render_f32_blocks_per_cu(int count);
 int rtmi_launch_reduce_stats(const unsigned long long* partials, int num_waves,
                              unsigned long long* acc, void* stream);
 int rtmi_launch_unshard(const float* gathered, float* fb, int width, int height, int band_h,

@@ -470,7 +470,6 @@ template <bool COUNT>
 __global__ __launch_bounds__(256) void k_render_fast(const FastParams p) {
   const int lane = (int)__lane_id();
   const int wave = (int)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
-  const int nwaves = (int)(gridDim.x * (blockDim.x >> 6));
   const int L = p.lanes_per_px;
   const int sub = lane & (L - 1);
   const int pix = lane >> p.log2_lanes;
@@ -485,7 +484,25 @@ __global__ __launch_bounds__(256) void k_render_fast(const FastParams p) {
   for (int k = 0; k < kStatSlots; ++k) ws.v[k] = 0u;
   unsigned long long tot = 0ull;
 
-  for (int g = wave; g < p.ngroups; g += nwaves) {
+  // Work queue: the grid is exactly the resident waves (host: occupancy
+  // query) and each wave pulls chunks of p.chunk pixel groups. One head word
+  // saturates near 90 dequeues/us, so the heads are sharded 8 ways, one per
+  // blockIdx % 8 label (blocks sharing an XCD; fewer shards when the grid
+  // has fewer than 8 blocks, so every shard has pullers), each on its own 128-B line;
+  // shard k hands out chunks k, k+8, k+16, ... so every shard's work is
+  // spread over the whole image. The next chunk's index is fetched one chunk
+  // ahead, hiding the atomic's latency behind the samples.
+  const int shard = (int)(blockIdx.x % (unsigned int)p.shards);
+  unsigned int* head = p.queue + shard * kQueueStride;
+  const int C = p.chunk;
+  int qj = 0;
+  if (lane == 0) qj = (int)atomicAdd(head, 1u);
+  qj = __builtin_amdgcn_readfirstlane(qj);
+  int qj_next = 0;
+  if (lane == 0) qj_next = (int)atomicAdd(head, 1u);
+  int g = (qj * p.shards + shard) * C;
+  int in_chunk = 0;
+  while (g < p.ngroups) {
     const int gx = g % p.tiles_x, gy = g / p.tiles_x;
     const int j = gx * p.tile_x + tpx;
     const int k = gy * p.tile_y + tpy;
@@ -561,6 +578,14 @@ __global__ __launch_bounds__(256) void k_render_fast(const FastParams p) {
         float* q = p.fb + ((size_t)out_row * p.width + x) * 3;
         q[0] = acc.x; q[1] = acc.y; q[2] = acc.z;
       }
+    }
+    if (++in_chunk < C && g + 1 < p.ngroups) {
+      ++g;
+    } else {
+      in_chunk = 0;
+      qj = __builtin_amdgcn_readfirstlane(qj_next);
+      if (lane == 0) qj_next = (int)atomicAdd(head, 1u);
+      g = (qj * p.shards + shard) * C;
     }
   }
   if (lane < kStatSlots) p.partials[(size_t)wave * kStatSlots + lane] = tot;

@@ -64,6 +64,15 @@ extern "C" int rtmi_launch_render_f32(const rtmi::FastParams* p, int blocks, voi
   return (int)hipGetLastError();
 }
 
+// Resident 256-thread blocks per CU of the render kernel (grid sizing for the
+// work-queue loop: launch exactly what fits, waves pull pixel groups).
+extern "C" int rtmi_render_f32_blocks_per_cu(int count) {
+  int nb = 0;
+  hipError_t e = count ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, rtmi::fast::k_render_fast<true>, 256, 0)
+                       : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, rtmi::fast::k_render_fast<false>, 256, 0);
+  return e == hipSuccess && nb > 0 ? nb : 1;
+}
+
 extern "C" int rtmi_launch_reduce_stats(const unsigned long long* partials, int num_waves,
                                         unsigned long long* acc, void* stream) {
   const int blocks = (num_waves + rtmi::kWavesPerBlock - 1) / rtmi::kWavesPerBlock;

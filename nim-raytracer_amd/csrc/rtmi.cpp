@@ -140,6 +140,7 @@ struct rt_scene {
   DevBuf<BvhNode> nodes;
   DevBuf<unsigned long long> partials;
   DevBuf<unsigned long long> acc;
+  DevBuf<unsigned int> queue;      // float32 work-queue heads (kQueueShards * kQueueStride)
   DevBuf<float> fb_scratch;
   int max_waves = 0;
   int64_t num_triangles = 0, num_nodes = 0;
@@ -151,6 +152,7 @@ struct rt_scene {
     f64.release();
     nodes.release();
     partials.release();
+    queue.release();
     acc.release();
     fb_scratch.release();
     if (done) (void)hipEventDestroy(done);
@@ -598,6 +600,7 @@ extern "C" int rt_scene_create(const rt_scene_desc* d, rt_scene** out_scene) {
   s->max_waves = s->num_cus * 8 * 4;  // 8 blocks of 4 waves per CU at most
   if ((rc = s->partials.alloc((size_t)s->max_waves * kStatSlots))) return rc;
   if ((rc = s->acc.alloc(kStatSlots))) return rc;
+  if ((rc = s->queue.alloc((size_t)kQueueShards * kQueueStride))) return rc;
   HIP_TRY(hipMemset(s->acc.p, 0, kStatSlots * sizeof(unsigned long long)));
   HIP_TRY(hipDeviceSynchronize());
   s->num_triangles = ntri;
@@ -693,7 +696,12 @@ Plan plan_mapping(const rt_scene* s, const rt_options* o, const Mapping& mp, int
   const long long ng = (long long)pl.tiles_x * tiles_y;
   pl.ngroups = (int)std::min<long long>(ng, INT32_MAX);
   const long long want = (ng + 3) / 4;
-  pl.blocks = (int)std::max(1LL, std::min<long long>(want, s->max_waves / 4));
+  long long cap = s->max_waves / 4;
+  if (o->precision == RT_FP32) {  // work-queue kernel: launch what is resident
+    const int per_cu = rtmi_render_f32_blocks_per_cu((o->flags & RT_FLAG_COUNT_TRAVERSAL) ? 1 : 0);
+    cap = std::min<long long>(cap, (long long)per_cu * s->num_cus);
+  }
+  pl.blocks = (int)std::max(1LL, std::min<long long>(want, cap));
   return pl;
 }
 
@@ -708,6 +716,7 @@ void fill_fast(rt_scene* s, const rt_options* o, const Mapping& mp, float* fb, F
   p.normals = s->f32.normals.p;
   p.fb = fb;
   p.partials = s->partials.p;
+  p.queue = s->queue.p;
   // camera: origin = C2W * (0,0,0,1) = column 3; dir = C2W * normalize(cx, cy, -1, 0)
   for (int k = 0; k < 3; ++k) {
     p.cam[k] = (float)s->c2w[12 + k];
@@ -754,6 +763,10 @@ void fill_fast(rt_scene* s, const rt_options* o, const Mapping& mp, float* fb, F
   p.tile_y = pl.ty;
   p.tiles_x = pl.tiles_x;
   p.ngroups = pl.ngroups;
+  // 4 groups per dequeue once every wave gets many chunks (tail <= 4 groups);
+  // 1 for small launches
+  p.chunk = (long long)pl.ngroups >= (long long)pl.blocks * 4 * 64 ? 4 : 1;
+  p.shards = std::min(kQueueShards, pl.blocks);
   *blocks = pl.blocks;
 }
 
@@ -885,6 +898,8 @@ int render_device(rt_scene* s, const rt_options* o, const Mapping& mp, float* d_
                   rt_stats* out) {
   HIP_TRY(hipStreamWaitEvent(st, s->done, 0));
   HIP_TRY(hipMemsetAsync(s->acc.p, 0, kStatSlots * sizeof(unsigned long long), st));
+  if (o->precision == RT_FP32)
+    HIP_TRY(hipMemsetAsync(s->queue.p, 0, (size_t)kQueueShards * kQueueStride * sizeof(unsigned int), st));
   int rc = launch(s, o, mp, d_out, st);
   if (rc) return rc;
   HIP_TRY(hipEventRecord(s->done, st));

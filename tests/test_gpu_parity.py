@@ -209,3 +209,15 @@ def test_full_size_c3_properties(gpu, oracle_mod):
     _assert_fp32_close(g1[rows], ref[rows])
 
 
+
+
+@pytest.mark.parametrize("w,h,m", [(1, 1, 1), (3, 2, 4), (7, 1, 16), (5, 3, 2)])
+def test_fp32_tiny_launches(gpu, oracle_mod, w, h, m):
+    """Launches with fewer pixel groups than work-queue shards / blocks: every
+    pixel is rendered exactly once (ray count) and matches the oracle."""
+    scene = scenes.spheres_warm(3)
+    aa = akGrid if m > 1 else akNone
+    ref, rst = _oracle_frame(oracle_mod, scene, _opts(w, h, Precision.fp64, aa, m))
+    got, gst, _ = _gpu_frame(scene, _opts(w, h, Precision.fp32, aa, m))
+    assert gst.numPrimaryRays == rst.numPrimaryRays == w * h * m * m
+    assert np.abs(got - ref).max() <= 2e-3
