@@ -44,6 +44,20 @@ __device__ __forceinline__ float rsq(float x) { return __builtin_amdgcn_rsqf(x);
 __device__ __forceinline__ float fsqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
 __device__ __forceinline__ float finf() { return __builtin_huge_valf(); }
 
+// Kernel parameters are read through this pointer into the kernarg segment,
+// re-laundered (opaque to the optimizer) once per pixel group, sample and
+// light: each field is then re-read with a scalar load near its use instead
+// of being hoisted to the kernel entry and pinned in SGPRs for the whole
+// kernel (which spilled ~100 SGPRs into VGPR lanes and cost a v_readlane per
+// use). Inside traverse() the pointer is invariant, so the node / triangle
+// base addresses stay hoisted off the fetch chain.
+using KP = const RT_CONST FastParams*;
+__device__ __forceinline__ KP params() {
+  KP q = (KP)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(q));
+  return q;
+}
+
 struct F3 {
   float x, y, z;
 };
@@ -78,7 +92,7 @@ struct Hit {
 };
 
 // World -> object space (FObj.xf classification).
-__device__ __forceinline__ void to_object(const FastParams& p, const FObj& ob, int i, F3 o, F3 d, F3& ro,
+__device__ __forceinline__ void to_object(KP p, const FObj& ob, int i, F3 o, F3 d, F3& ro,
                                           F3& rd) {
   if (ob.xf == XF_IDENTITY) {
     ro = o;
@@ -87,7 +101,7 @@ __device__ __forceinline__ void to_object(const FastParams& p, const FObj& ob, i
     ro = f3(o.x + ob.t[0], o.y + ob.t[1], o.z + ob.t[2]);
     rd = d;
   } else {
-    const RT_CONST FObjX& x = cp(p.objx)[i];
+    const RT_CONST FObjX& x = cp(p->objx)[i];
     const float* m = x.w2o;  // m[c*3 + r], c = 0..3
     ro = f3(__builtin_fmaf(m[0], o.x, __builtin_fmaf(m[3], o.y, __builtin_fmaf(m[6], o.z, m[9]))),
             __builtin_fmaf(m[1], o.x, __builtin_fmaf(m[4], o.y, __builtin_fmaf(m[7], o.z, m[10]))),
@@ -163,9 +177,9 @@ __device__ __forceinline__ void tri_test(const RT_CONST TriFast& T, F3 o, F3 d, 
 }
 
 // Leaf: the n (1..kLeafMax, wave-uniform) triangles starting at `first`.
-__device__ __forceinline__ void leaf(const FastParams& p, int first, int n, F3 o, F3 d, unsigned long long& key,
+__device__ __forceinline__ void leaf(KP p, int first, int n, F3 o, F3 d, unsigned long long& key,
                                      float& tc) {
-  const RT_CONST TriFast* t = cp(p.tris) + first;
+  const RT_CONST TriFast* t = cp(p->tris) + first;
   tri_test(t[0], o, d, key, tc);
 #pragma unroll
   for (int k = 1; k < kLeafMax; ++k) {
@@ -186,7 +200,7 @@ __device__ __forceinline__ void leaf(const FastParams& p, int first, int n, F3 o
 // early/stop: exact early exit for shadow rays (trace()): a lane
 // retires once its best t <= stop.
 template <bool COUNT>
-__device__ __forceinline__ void traverse(const FastParams& p, int root, F3 o, F3 d, bool active, bool early,
+__device__ __forceinline__ void traverse(KP p, int root, F3 o, F3 d, bool active, bool early,
                                          float stop, float& tbest, int& best_id, Stats32& ws) {
   if (bal(active) == 0ull) return;
   RT_STAMP(t_enter);
@@ -208,7 +222,7 @@ __device__ __forceinline__ void traverse(const FastParams& p, int root, F3 o, F3
   int sp = 0;
   int node = root;
   for (;;) {
-    const BvhNode nd = cp(p.nodes)[node];
+    const BvhNode nd = cp(p->nodes)[node];
     if constexpr (COUNT) {
       ws.v[STAT_NODE_FETCH] += 1u;
       ws.v[STAT_LANE_NODES] += pc(bal(tc >= 0.0f));
@@ -277,7 +291,7 @@ __device__ __forceinline__ void traverse(const FastParams& p, int root, F3 o, F3
 
 // t of analytic object i in world space, -inf on a miss (Sphere / Plane /
 // Box .intersect, geom.nim:215-248, 76-96).
-__device__ __forceinline__ float analytic_t(const FastParams& p, const FObj& ob, int i, F3 o, F3 d) {
+__device__ __forceinline__ float analytic_t(KP p, const FObj& ob, int i, F3 o, F3 d) {
   F3 ro, rd;
   to_object(p, ob, i, o, d, ro, rd);
   if (ob.type == GEOM_PLANE) return plane(ro, rd);
@@ -293,22 +307,22 @@ __device__ __forceinline__ float analytic_t(const FastParams& p, const FObj& ob,
 // its t beats the mesh's closest t. So once a lane has found a mesh hit at
 // t <= stop = min t of the analytic objects after the mesh, every later
 // comparison is decided and the lane retires: exact, not an approximation.
-// Applied when the scene has exactly one mesh object (p.shadow_mesh).
+// Applied when the scene has exactly one mesh object (p->shadow_mesh).
 template <bool COUNT>
-__device__ __forceinline__ Hit trace(const FastParams& p, F3 o, F3 d, float tmax, bool active, bool shadow,
+__device__ __forceinline__ Hit trace(KP p, F3 o, F3 d, float tmax, bool active, bool shadow,
                                      Stats32& ws) {
   Hit h{-1, -1, tmax};
-  const bool early = shadow && p.shadow_mesh >= 0;
+  const bool early = shadow && p->shadow_mesh >= 0;
   float stop = -1.0f;
   if (early) {
     stop = finf();
-    for (int i = p.shadow_mesh + 1; i < p.nobj; ++i) {
-      const float t = analytic_t(p, cp(p.objs)[i], i, o, d);
+    for (int i = p->shadow_mesh + 1; i < p->nobj; ++i) {
+      const float t = analytic_t(p, cp(p->objs)[i], i, o, d);
       stop = t >= 0.0f ? fminf(stop, t) : stop;
     }
   }
-  for (int i = 0; i < p.nobj; ++i) {
-    const FObj ob = cp(p.objs)[i];
+  for (int i = 0; i < p->nobj; ++i) {
+    const FObj ob = cp(p->objs)[i];
     float t;
     int tri = -1;
     if (ob.type != GEOM_MESH) {
@@ -316,14 +330,14 @@ __device__ __forceinline__ Hit trace(const FastParams& p, F3 o, F3 d, float tmax
     } else {
       F3 ro, rd;
       to_object(p, ob, i, o, d, ro, rd);
-      const FMesh m = cp(p.meshes)[ob.mesh];
+      const FMesh m = cp(p->meshes)[ob.mesh];
       // TriangleMesh.intersect (geom.nim:339-358): a ray starting inside
       // the mesh AABB misses; otherwise the closest face.
       const float gate = aabb(m.lo, m.hi, ro, f3(rcp(rd.x), rcp(rd.y), rcp(rd.z)));
       const bool in = gate >= 0.0f;
       float tb = h.t;
       int best = -1;
-      if (m.root >= 0) traverse<COUNT>(p, m.root, ro, rd, active && in, early && i == p.shadow_mesh, stop, tb, best, ws);
+      if (m.root >= 0) traverse<COUNT>(p, m.root, ro, rd, active && in, early && i == p->shadow_mesh, stop, tb, best, ws);
       t = !in ? -finf() : (best >= 0 ? tb : finf());
       tri = best;
     }
@@ -368,15 +382,16 @@ __device__ __forceinline__ F3 analytic_normal(const FObj& ob, F3 ho) {
 // One camera sample: trace + shade (renderer.nim:71-127), reflections as a
 // loop of levels with forward weights.
 template <bool COUNT>
-__device__ __forceinline__ F3 shade_path(const FastParams& p, F3 o, F3 d, bool active, Stats32& ws) {
+__device__ __forceinline__ F3 shade_path(KP p, F3 o, F3 d, bool active, Stats32& ws) {
   bool act = active;
   int depth = 1;
   F3 acc = f3(0.0f, 0.0f, 0.0f);
   float w = 1.0f;
   for (int lev = 0; lev < kMaxShadeLevels; ++lev) {
+    p = params();
     if (bal(act) == 0ull) break;
     const Hit hit = trace<COUNT>(p, o, d, finf(), act, false, ws);
-    if (act && hit.obj < 0) acc = f3(acc.x + w * p.bg[0], acc.y + w * p.bg[1], acc.z + w * p.bg[2]);
+    if (act && hit.obj < 0) acc = f3(acc.x + w * p->bg[0], acc.y + w * p->bg[1], acc.z + w * p->bg[2]);
     const bool lit = act && hit.obj >= 0;
     const F3 hw = f3(__builtin_fmaf(d.x, hit.t, o.x), __builtin_fmaf(d.y, hit.t, o.y), __builtin_fmaf(d.z, hit.t, o.z));
     F3 N = f3(0.0f, 0.0f, 0.0f);
@@ -388,12 +403,12 @@ __device__ __forceinline__ F3 shade_path(const FastParams& p, F3 o, F3 d, bool a
       const int oi = __builtin_amdgcn_readlane(hit.obj, lead);
       const bool mine = lit && hit.obj == oi;
       pending &= ~bal(mine);
-      const FObj ob = cp(p.objs)[oi];
-      const RT_CONST FObjX& ox = cp(p.objx)[oi];
+      const FObj ob = cp(p->objs)[oi];
+      const RT_CONST FObjX& ox = cp(p->objx)[oi];
       if (mine) {
         F3 n;
         if (ob.type == GEOM_MESH) {
-          const float* fn = p.normals + 3 * (size_t)(ox.normal_base + hit.tri);
+          const float* fn = p->normals + 3 * (size_t)(ox.normal_base + hit.tri);
           n = f3(fn[0], fn[1], fn[2]);
         } else {
           F3 ho, unused;
@@ -413,10 +428,11 @@ __device__ __forceinline__ F3 shade_path(const FastParams& p, F3 o, F3 d, bool a
       }
     }
     F3 local = f3(0.0f, 0.0f, 0.0f);
-    const F3 so = f3(__builtin_fmaf(N.x, p.bias, hw.x), __builtin_fmaf(N.y, p.bias, hw.y),
-                     __builtin_fmaf(N.z, p.bias, hw.z));
-    for (int li = 0; li < p.nlight; ++li) {
-      const FLight L = cp(p.lights)[li];
+    const F3 so = f3(__builtin_fmaf(N.x, p->bias, hw.x), __builtin_fmaf(N.y, p->bias, hw.y),
+                     __builtin_fmaf(N.z, p->bias, hw.z));
+    for (int li = 0; li < p->nlight; ++li) {
+      p = params();
+      const FLight L = cp(p->lights)[li];
       F3 sd, I;
       float dist;
       if (L.type == LIGHT_POINT) {  // light.nim:52-62
@@ -440,7 +456,7 @@ __device__ __forceinline__ F3 shade_path(const FastParams& p, F3 o, F3 d, bool a
                    __builtin_fmaf(alb.z * I.z, ndl, local.z));
       }
     }
-    const bool reflect = lit && refl > 0.0f && depth <= p.max_depth;
+    const bool reflect = lit && refl > 0.0f && depth <= p->max_depth;
     const float wl = reflect ? w * (1.0f - refl) : w;
     if (lit) acc = f3(__builtin_fmaf(wl, local.x, acc.x), __builtin_fmaf(wl, local.y, acc.y),
                       __builtin_fmaf(wl, local.z, acc.z));
@@ -449,7 +465,7 @@ __device__ __forceinline__ F3 shade_path(const FastParams& p, F3 o, F3 d, bool a
       w = w * refl;
       const float ndi = 2.0f * dot3(N, d);
       const F3 rd = f3(d.x - N.x * ndi, d.y - N.y * ndi, d.z - N.z * ndi);
-      o = f3(__builtin_fmaf(rd.x, p.bias, hw.x), __builtin_fmaf(rd.y, p.bias, hw.y), __builtin_fmaf(rd.z, p.bias, hw.z));
+      o = f3(__builtin_fmaf(rd.x, p->bias, hw.x), __builtin_fmaf(rd.y, p->bias, hw.y), __builtin_fmaf(rd.z, p->bias, hw.z));
       d = rd;
       ++depth;
     }
@@ -466,17 +482,27 @@ __device__ __forceinline__ void flush(Stats32& ws, unsigned long long& tot, int 
   }
 }
 
+// Occupancy target: the kernel is latency-bound (serial node-fetch chains),
+// so resident waves matter more than a few spills. 6 waves/SIMD (<= 80
+// VGPRs) measured best: C3 12.0 -> 10.3 ms vs the unconstrained 5 waves
+// (98 VGPRs); 7 and 8 spill inside the traversal and lose.
+#ifndef RTMI_WAVES_PER_EU
+#define RTMI_WAVES_PER_EU 6
+#endif
+#define RTMI_OCC __attribute__((amdgpu_waves_per_eu(RTMI_WAVES_PER_EU)))
 template <bool COUNT>
-__global__ __launch_bounds__(256) void k_render_fast(const FastParams p) {
+__global__ __launch_bounds__(256) RTMI_OCC void k_render_fast(const FastParams params_by_value) {
+  (void)params_by_value;  // read through params() (kernarg segment)
+  KP p = params();
   const int lane = (int)__lane_id();
   const int wave = (int)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
-  const int L = p.lanes_per_px;
+  const int L = p->lanes_per_px;
   const int sub = lane & (L - 1);
-  const int pix = lane >> p.log2_lanes;
-  const int tpx = pix % p.tile_x, tpy = pix / p.tile_x;
-  const int iters = (p.spp + L - 1) / L;
-  const bool grid_aa = p.aa_kind != 0;
-  const int m = p.grid_m;
+  const int pix = lane >> p->log2_lanes;
+  const int tpx = pix % p->tile_x, tpy = pix / p->tile_x;
+  const int iters = (p->spp + L - 1) / L;
+  const bool grid_aa = p->aa_kind != 0;
+  const int m = p->grid_m;
   const int si0 = sub % m, sj0 = sub / m;  // grid coordinates of this lane's first sample
   const int dli = L % m, dlj = L / m;      // advance of the grid coordinates per iteration
   Stats32 ws;
@@ -485,47 +511,49 @@ __global__ __launch_bounds__(256) void k_render_fast(const FastParams p) {
   unsigned long long tot = 0ull;
 
   // Work queue: the grid is exactly the resident waves (host: occupancy
-  // query) and each wave pulls chunks of p.chunk pixel groups. One head word
+  // query) and each wave pulls chunks of p->chunk pixel groups. One head word
   // saturates near 90 dequeues/us, so the heads are sharded 8 ways, one per
   // blockIdx % 8 label (blocks sharing an XCD; fewer shards when the grid
   // has fewer than 8 blocks, so every shard has pullers), each on its own 128-B line;
   // shard k hands out chunks k, k+8, k+16, ... so every shard's work is
   // spread over the whole image. The next chunk's index is fetched one chunk
   // ahead, hiding the atomic's latency behind the samples.
-  const int shard = (int)(blockIdx.x % (unsigned int)p.shards);
-  unsigned int* head = p.queue + shard * kQueueStride;
-  const int C = p.chunk;
+  const int shard = (int)(blockIdx.x % (unsigned int)p->shards);
+  unsigned int* head = p->queue + shard * kQueueStride;
+  const int C = p->chunk;
   int qj = 0;
   if (lane == 0) qj = (int)atomicAdd(head, 1u);
   qj = __builtin_amdgcn_readfirstlane(qj);
   int qj_next = 0;
   if (lane == 0) qj_next = (int)atomicAdd(head, 1u);
-  int g = (qj * p.shards + shard) * C;
+  int g = (qj * p->shards + shard) * C;
   int in_chunk = 0;
-  while (g < p.ngroups) {
-    const int gx = g % p.tiles_x, gy = g / p.tiles_x;
-    const int j = gx * p.tile_x + tpx;
-    const int k = gy * p.tile_y + tpy;
-    const int x = j * p.step;
+  while (g < p->ngroups) {
+    p = params();
+    const int gx = g % p->tiles_x, gy = g / p->tiles_x;
+    const int j = gx * p->tile_x + tpx;
+    const int k = gy * p->tile_y + tpy;
+    const int x = j * p->step;
     int y, out_row;
-    bool valid = j < p.ncols && k < p.nrows;
-    if (p.mode == 0) {
-      y = p.y0 + k * p.step;
+    bool valid = j < p->ncols && k < p->nrows;
+    if (p->mode == 0) {
+      y = p->y0 + k * p->step;
       out_row = y;
     } else {
-      const int lb = k / p.band_h, rr = k % p.band_h;
-      y = (lb * p.world + p.rank) * p.band_h + rr;
+      const int lb = k / p->band_h, rr = k % p->band_h;
+      y = (lb * p->world + p->rank) * p->band_h + rr;
       out_row = k;
-      valid = valid && y < p.height;
+      valid = valid && y < p->height;
     }
-    if (p.step < p.max_step) {  // progressive refinement skip (renderer.nim:175-178)
-      const int mask = p.step * 2 - 1;
+    if (p->step < p->max_step) {  // progressive refinement skip (renderer.nim:175-178)
+      const int mask = p->step * 2 - 1;
       if ((x & mask) == 0 && (y & mask) == 0) valid = false;
     }
     F3 acc = f3(0.0f, 0.0f, 0.0f);
     int bi = 0, bj = 0;  // grid coordinates of sample it*L (wave-uniform)
     for (int it = 0; it < iters; ++it) {
-      const bool sv = valid && it * L + sub < p.spp;
+      p = params();
+      const bool sv = valid && it * L + sub < p->spp;
       float px = (float)x, py = (float)y;
       if (grid_aa) {  // grid() sampling.nim:5-18
         int si = bi + si0, sj = bj + sj0;
@@ -533,18 +561,18 @@ __global__ __launch_bounds__(256) void k_render_fast(const FastParams p) {
           si -= m;
           sj += 1;
         }
-        px += __builtin_fmaf((float)si, p.sample_step, p.sample_off);
-        py += __builtin_fmaf((float)sj, p.sample_step, p.sample_off);
+        px += __builtin_fmaf((float)si, p->sample_step, p->sample_off);
+        py += __builtin_fmaf((float)sj, p->sample_step, p->sample_off);
       }
       // castPrimaryRay (renderer.nim:31-44), constants folded on the host
       // ((2 x r)/w - r) f == (x - w/2) (2 r f / w): exact 0 on the centre
       // column / row, as the reference's own formula gives there
-      const float cx = (px - p.cam_b) * p.cam_a;
-      const float cy = (p.cam_d - py) * p.cam_c;
+      const float cx = (px - p->cam_b) * p->cam_a;
+      const float cy = (p->cam_d - py) * p->cam_c;
       const float rl = rsq(__builtin_fmaf(cx, cx, __builtin_fmaf(cy, cy, 1.0f)));
-      const F3 d = f3((cx * p.cam[3] + cy * p.cam[6] - p.cam[9]) * rl, (cx * p.cam[4] + cy * p.cam[7] - p.cam[10]) * rl,
-                      (cx * p.cam[5] + cy * p.cam[8] - p.cam[11]) * rl);
-      const F3 o = f3(p.cam[0], p.cam[1], p.cam[2]);
+      const F3 d = f3((cx * p->cam[3] + cy * p->cam[6] - p->cam[9]) * rl, (cx * p->cam[4] + cy * p->cam[7] - p->cam[10]) * rl,
+                      (cx * p->cam[5] + cy * p->cam[8] - p->cam[11]) * rl);
+      const F3 o = f3(p->cam[0], p->cam[1], p->cam[2]);
       ws.v[STAT_PRIMARY] += pc(bal(sv));
       RT_STAMP(t_s0);
       const F3 c = shade_path<COUNT>(p, o, d, sv, ws);
@@ -566,29 +594,29 @@ __global__ __launch_bounds__(256) void k_render_fast(const FastParams p) {
       acc.z += __shfl_xor(acc.z, off);
     }
     if (valid && sub == 0) {
-      if (grid_aa) acc = f3(acc.x * p.inv_len, acc.y * p.inv_len, acc.z * p.inv_len);
-      if (p.mode == 0 && p.step > 1) {
-        const int xe = min(x + p.step, p.width), ye = min(y + p.step, p.height);
+      if (grid_aa) acc = f3(acc.x * p->inv_len, acc.y * p->inv_len, acc.z * p->inv_len);
+      if (p->mode == 0 && p->step > 1) {
+        const int xe = min(x + p->step, p->width), ye = min(y + p->step, p->height);
         for (int yy = y; yy < ye; ++yy)
           for (int xx = x; xx < xe; ++xx) {
-            float* q = p.fb + ((size_t)yy * p.width + xx) * 3;
+            float* q = p->fb + ((size_t)yy * p->width + xx) * 3;
             q[0] = acc.x; q[1] = acc.y; q[2] = acc.z;
           }
       } else {
-        float* q = p.fb + ((size_t)out_row * p.width + x) * 3;
+        float* q = p->fb + ((size_t)out_row * p->width + x) * 3;
         q[0] = acc.x; q[1] = acc.y; q[2] = acc.z;
       }
     }
-    if (++in_chunk < C && g + 1 < p.ngroups) {
+    if (++in_chunk < C && g + 1 < p->ngroups) {
       ++g;
     } else {
       in_chunk = 0;
       qj = __builtin_amdgcn_readfirstlane(qj_next);
       if (lane == 0) qj_next = (int)atomicAdd(head, 1u);
-      g = (qj * p.shards + shard) * C;
+      g = (qj * p->shards + shard) * C;
     }
   }
-  if (lane < kStatSlots) p.partials[(size_t)wave * kStatSlots + lane] = tot;
+  if (lane < kStatSlots) p->partials[(size_t)wave * kStatSlots + lane] = tot;
 }
 
 }  // namespace fast
