@@ -379,19 +379,60 @@ __device__ __forceinline__ F3 analytic_normal(const FObj& ob, F3 ho) {
   return f3(0.0f, 1.0f, 0.0f);  // plane
 }
 
+// Per-lane LDS scratch of the shading loop, laid out [slot][lane] so a
+// wave's access to one slot touches 64 consecutive dwords (no bank
+// conflicts). Parking the reflected ray and the hit point here instead of in
+// VGPRs takes them out of the register peak, which sits inside the
+// shadow-ray traversal (DESIGN.md "Occupancy").
+enum : int { LDS_RO = 0, LDS_RD = 3, LDS_HW = 6, kLdsSlots = 9 };
+// An LDS-typed pointer: 32-bit addresses with the slot offsets folded into
+// the ds_* immediates (a generic float* here became a 64-bit flat address
+// per slot, hoisted and pinned in VGPRs).
+#if defined(__HIP_DEVICE_COMPILE__)
+using LdsF = __attribute__((address_space(3))) float;
+#else
+using LdsF = float;
+#endif
+
+// Radiance accumulator of the lane's current pixel samples. Kept in VGPRs:
+// LDS float atomics (ds_add_f32) measured ~50 % slower on C3 and a plain
+// LDS read-modify-write no faster than the three registers.
+struct Acc {
+  F3 v;
+};
+__device__ __forceinline__ void acc_add3(Acc& a, float x, float y, float z) {
+  a.v = f3(a.v.x + x, a.v.y + y, a.v.z + z);
+}
+// volatile: the value must really leave the registers (no store-to-load
+// forwarding across the light loop)
+__device__ __forceinline__ void lds_put3(LdsF* ls, int slot, F3 v) {
+  volatile LdsF* q = ls;
+  q[(slot + 0) * 64] = v.x;
+  q[(slot + 1) * 64] = v.y;
+  q[(slot + 2) * 64] = v.z;
+}
+__device__ __forceinline__ F3 lds_get3(LdsF* ls, int slot) {
+  volatile LdsF* q = ls;
+  return f3(q[(slot + 0) * 64], q[(slot + 1) * 64], q[(slot + 2) * 64]);
+}
+
 // One camera sample: trace + shade (renderer.nim:71-127), reflections as a
-// loop of levels with forward weights.
+// loop of levels with forward weights; radiance is added into `acc`.
+//  * renderer.nim:94-101: one shadow ray per light from hitW + N*bias; the
+//    light's shadeDiffuse term (shader.nim:12-17) is added when it misses.
+//  * renderer.nim:104-124: reflection > 0 and depth <= maxRayDepth traces
+//    r = i - 2 (n.i) n from hitW + r*bias; the level's local light is
+//    weighted (1 - reflection), the reflected colour reflection.
 template <bool COUNT>
-__device__ __forceinline__ F3 shade_path(KP p, F3 o, F3 d, bool active, Stats32& ws) {
+__device__ __forceinline__ void shade_path(KP p, F3 o, F3 d, bool active, LdsF* ls, Acc& acc, Stats32& ws) {
   bool act = active;
   int depth = 1;
-  F3 acc = f3(0.0f, 0.0f, 0.0f);
   float w = 1.0f;
   for (int lev = 0; lev < kMaxShadeLevels; ++lev) {
     p = params();
     if (bal(act) == 0ull) break;
     const Hit hit = trace<COUNT>(p, o, d, finf(), act, false, ws);
-    if (act && hit.obj < 0) acc = f3(acc.x + w * p->bg[0], acc.y + w * p->bg[1], acc.z + w * p->bg[2]);
+    if (act && hit.obj < 0) acc_add3(acc, w * p->bg[0], w * p->bg[1], w * p->bg[2]);
     const bool lit = act && hit.obj >= 0;
     const F3 hw = f3(__builtin_fmaf(d.x, hit.t, o.x), __builtin_fmaf(d.y, hit.t, o.y), __builtin_fmaf(d.z, hit.t, o.z));
     F3 N = f3(0.0f, 0.0f, 0.0f);
@@ -427,51 +468,56 @@ __device__ __forceinline__ F3 shade_path(KP p, F3 o, F3 d, bool active, Stats32&
         refl = ox.refl;
       }
     }
-    F3 local = f3(0.0f, 0.0f, 0.0f);
+    const bool reflect = lit && refl > 0.0f && depth <= p->max_depth;
+    const float wl = reflect ? w * (1.0f - refl) : w;
+    const F3 albw = f3(alb.x * wl, alb.y * wl, alb.z * wl);
+    ws.v[STAT_REFL] += pc(bal(reflect));
+    if (bal(reflect)) {  // park the reflected ray (renderer.nim:109-118)
+      if (reflect) {
+        const float ndi = 2.0f * dot3(N, d);
+        const F3 rd = f3(d.x - N.x * ndi, d.y - N.y * ndi, d.z - N.z * ndi);
+        lds_put3(ls, LDS_RO, f3(__builtin_fmaf(rd.x, p->bias, hw.x), __builtin_fmaf(rd.y, p->bias, hw.y),
+                                __builtin_fmaf(rd.z, p->bias, hw.z)));
+        lds_put3(ls, LDS_RD, rd);
+      }
+    }
     const F3 so = f3(__builtin_fmaf(N.x, p->bias, hw.x), __builtin_fmaf(N.y, p->bias, hw.y),
                      __builtin_fmaf(N.z, p->bias, hw.z));
+    if (p->has_point_light) lds_put3(ls, LDS_HW, hw);
     for (int li = 0; li < p->nlight; ++li) {
       p = params();
       const FLight L = cp(p->lights)[li];
-      F3 sd, I;
-      float dist;
+      F3 sd;
+      float dist, k = 1.0f;
       if (L.type == LIGHT_POINT) {  // light.nim:52-62
-        const F3 lv = f3(hw.x - L.v[0], hw.y - L.v[1], hw.z - L.v[2]);
+        const F3 h = lds_get3(ls, LDS_HW);
+        const F3 lv = f3(h.x - L.v[0], h.y - L.v[1], h.z - L.v[2]);
         const float r2 = dot3(lv, lv);
         const float rr = rsq(r2);
         sd = f3(-lv.x * rr, -lv.y * rr, -lv.z * rr);
-        const float k = rcp(12.566370614359172f * r2);
-        I = f3(L.ci[0] * k, L.ci[1] * k, L.ci[2] * k);
+        k = rcp(12.566370614359172f * r2);
         dist = r2 * rr;
       } else {  // light.nim:46-50
         sd = f3(-L.v[0], -L.v[1], -L.v[2]);
-        I = f3(L.ci[0], L.ci[1], L.ci[2]);
         dist = finf();
       }
       ws.v[STAT_SHADOW] += pc(bal(lit));
       const Hit sh = trace<COUNT>(p, so, sd, dist, lit, true, ws);
       if (lit && sh.obj < 0) {  // shadeDiffuse (shader.nim:12-17)
-        const float ndl = fmaxf(dot3(N, sd), 0.0f);
-        local = f3(__builtin_fmaf(alb.x * I.x, ndl, local.x), __builtin_fmaf(alb.y * I.y, ndl, local.y),
-                   __builtin_fmaf(alb.z * I.z, ndl, local.z));
+        const float ndl = fmaxf(dot3(N, sd), 0.0f) * k;
+        acc_add3(acc, albw.x * L.ci[0] * ndl, albw.y * L.ci[1] * ndl, albw.z * L.ci[2] * ndl);
       }
     }
-    const bool reflect = lit && refl > 0.0f && depth <= p->max_depth;
-    const float wl = reflect ? w * (1.0f - refl) : w;
-    if (lit) acc = f3(__builtin_fmaf(wl, local.x, acc.x), __builtin_fmaf(wl, local.y, acc.y),
-                      __builtin_fmaf(wl, local.z, acc.z));
-    ws.v[STAT_REFL] += pc(bal(reflect));
-    if (reflect) {  // renderer.nim:109-118
-      w = w * refl;
-      const float ndi = 2.0f * dot3(N, d);
-      const F3 rd = f3(d.x - N.x * ndi, d.y - N.y * ndi, d.z - N.z * ndi);
-      o = f3(__builtin_fmaf(rd.x, p->bias, hw.x), __builtin_fmaf(rd.y, p->bias, hw.y), __builtin_fmaf(rd.z, p->bias, hw.z));
-      d = rd;
-      ++depth;
+    // every lane reloads (lanes that do not reflect go inactive): o and d
+    // are then dead across the light loop instead of carried for them
+    if (bal(reflect)) {
+      o = lds_get3(ls, LDS_RO);
+      d = lds_get3(ls, LDS_RD);
     }
+    w = w * refl;
+    ++depth;
     act = reflect;
   }
-  return acc;
 }
 
 __device__ __forceinline__ void flush(Stats32& ws, unsigned long long& tot, int lane) {
@@ -483,17 +529,19 @@ __device__ __forceinline__ void flush(Stats32& ws, unsigned long long& tot, int 
 }
 
 // Occupancy target: the kernel is latency-bound (serial node-fetch chains),
-// so resident waves matter more than a few spills. 6 waves/SIMD (<= 80
-// VGPRs) measured best: C3 12.0 -> 10.3 ms vs the unconstrained 5 waves
-// (98 VGPRs); 7 and 8 spill inside the traversal and lose.
+// so resident waves matter more than a few spills in the outer loops.
+// 7 waves/SIMD (<= 72 VGPRs) measured best on C3/C2 (DESIGN.md
+// "Occupancy"); 8 spills inside the traversal and loses.
 #ifndef RTMI_WAVES_PER_EU
-#define RTMI_WAVES_PER_EU 6
+#define RTMI_WAVES_PER_EU 7
 #endif
 #define RTMI_OCC __attribute__((amdgpu_waves_per_eu(RTMI_WAVES_PER_EU)))
 template <bool COUNT>
 __global__ __launch_bounds__(256) RTMI_OCC void k_render_fast(const FastParams params_by_value) {
   (void)params_by_value;  // read through params() (kernarg segment)
   KP p = params();
+  __shared__ float lds[4][kLdsSlots][64];  // 4 waves per 256-thread block
+  LdsF* ls = (LdsF*)&lds[threadIdx.x >> 6][0][__lane_id()];
   const int lane = (int)__lane_id();
   const int wave = (int)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
   const int L = p->lanes_per_px;
@@ -549,7 +597,8 @@ __global__ __launch_bounds__(256) RTMI_OCC void k_render_fast(const FastParams p
       const int mask = p->step * 2 - 1;
       if ((x & mask) == 0 && (y & mask) == 0) valid = false;
     }
-    F3 acc = f3(0.0f, 0.0f, 0.0f);
+    Acc pacc;
+    pacc.v = f3(0.0f, 0.0f, 0.0f);
     int bi = 0, bj = 0;  // grid coordinates of sample it*L (wave-uniform)
     for (int it = 0; it < iters; ++it) {
       p = params();
@@ -575,11 +624,10 @@ __global__ __launch_bounds__(256) RTMI_OCC void k_render_fast(const FastParams p
       const F3 o = f3(p->cam[0], p->cam[1], p->cam[2]);
       ws.v[STAT_PRIMARY] += pc(bal(sv));
       RT_STAMP(t_s0);
-      const F3 c = shade_path<COUNT>(p, o, d, sv, ws);
+      shade_path<COUNT>(p, o, d, sv, ls, pacc, ws);
 #ifdef RTMI_STAMPS
       { RT_STAMP(t_s1); RT_ACC(7, t_s0, t_s1); }
 #endif
-      if (sv) acc = grid_aa ? f3(acc.x + c.x, acc.y + c.y, acc.z + c.z) : c;
       bi += dli;
       bj += dlj;
       if (bi >= m) {
@@ -588,6 +636,7 @@ __global__ __launch_bounds__(256) RTMI_OCC void k_render_fast(const FastParams p
       }
     }
     flush(ws, tot, lane);
+    F3 acc = pacc.v;
     for (int off = 1; off < L; off <<= 1) {
       acc.x += __shfl_xor(acc.x, off);
       acc.y += __shfl_xor(acc.y, off);

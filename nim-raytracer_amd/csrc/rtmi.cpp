@@ -131,6 +131,7 @@ struct rt_scene {
   hipEvent_t done = nullptr;
   int32_t nobj = 0, nlight = 0, nmesh = 0;
   int32_t shadow_mesh = -1;  // the only mesh object, or -1 (FastParams.shadow_mesh)
+  int32_t has_point_light = 0;
   bool any_reflective = false;
   double fov = 50.0;
   double c2w[16];
@@ -557,6 +558,8 @@ extern "C" int rt_scene_create(const rt_scene_desc* d, rt_scene** out_scene) {
     if (n_mesh_obj != 1) s->shadow_mesh = -1;
   }
   s->nlight = d->num_lights;
+  for (int i = 0; i < d->num_lights; ++i)
+    if (d->lights[i].type == RT_POINT_LIGHT) s->has_point_light = 1;
   s->nmesh = d->num_meshes;
   s->any_reflective = any_reflective;
   s->fov = d->fov;
@@ -739,6 +742,7 @@ void fill_fast(rt_scene* s, const rt_options* o, const Mapping& mp, float* fb, F
   p.sample_off = (float)(1.0 / (double)m * 0.5);
   p.nobj = s->nobj;
   p.nlight = s->nlight;
+  p.has_point_light = s->has_point_light;
   p.width = o->width;
   p.height = o->height;
   p.aa_kind = o->aa_kind;
