@@ -520,14 +520,6 @@ __device__ __forceinline__ void shade_path(KP p, F3 o, F3 d, bool active, LdsF* 
   }
 }
 
-__device__ __forceinline__ void flush(Stats32& ws, unsigned long long& tot, int lane) {
-#pragma unroll
-  for (int k = 0; k < kStatSlots; ++k) {
-    tot += (lane == k) ? (unsigned long long)ws.v[k] : 0ull;
-    ws.v[k] = 0u;
-  }
-}
-
 // Occupancy target: the kernel is latency-bound (serial node-fetch chains),
 // so resident waves matter more than a few spills in the outer loops.
 // 7 waves/SIMD (<= 72 VGPRs) measured best on C3/C2 (DESIGN.md
@@ -536,80 +528,102 @@ __device__ __forceinline__ void flush(Stats32& ws, unsigned long long& tot, int 
 #define RTMI_WAVES_PER_EU 7
 #endif
 #define RTMI_OCC __attribute__((amdgpu_waves_per_eu(RTMI_WAVES_PER_EU)))
+// The lane id from an opaque instruction: values derived from it are
+// recomputed inside the loops instead of hoisted to kernel scope, where
+// they would stay live (and spill) across the whole sample loop.
+__device__ __forceinline__ int lane_id_fresh() {
+  int l;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+  return l;
+}
+
+// q = n / dv, r = n - q*dv for 0 <= n < 2^21 and dv >= 1 via the float
+// reciprocal (exact: the quotient's fractional part keeps >= 0.5/dv from an
+// integer, far above the fp32 product's error); no integer-division sequence.
+__device__ __forceinline__ int div_small(int n, int dv, float inv_dv, int& r) {
+  const int q = (int)(((float)n + 0.5f) * inv_dv);
+  r = n - q * dv;
+  return q;
+}
+
+// A pixel group's placement: tile (tx x ty pixels, L lanes each, powers of
+// two) -> this lane's pixel (x, y), output row and validity.
+struct GroupPix {
+  int x, y, out_row, sub;
+  bool valid;
+};
+__device__ __forceinline__ GroupPix group_pixel(KP p, int g, int lane) {
+  GroupPix r;
+  r.sub = lane & (p->lanes_per_px - 1);
+  const int pix = lane >> p->log2_lanes;
+  const int tpx = pix & (p->tile_x - 1), tpy = pix >> p->log2_tile_x;
+  const int gy = g / p->tiles_x, gx = g - gy * p->tiles_x;  // wave-uniform (scalar)
+  const int j = gx * p->tile_x + tpx;
+  const int k = gy * p->tile_y + tpy;
+  r.x = j * p->step;
+  r.valid = j < p->ncols && k < p->nrows;
+  if (p->mode == 0) {
+    r.y = p->y0 + k * p->step;
+    r.out_row = r.y;
+  } else {  // round-robin bands (rt_render_bands_device)
+    int rr;
+    const int lb = div_small(k, p->band_h, p->inv_band_h, rr);
+    r.y = (lb * p->world + p->rank) * p->band_h + rr;
+    r.out_row = k;
+    r.valid = r.valid && r.y < p->height;
+  }
+  if (p->step < p->max_step) {  // progressive refinement skip (renderer.nim:175-178)
+    const int mask = p->step * 2 - 1;
+    if ((r.x & mask) == 0 && (r.y & mask) == 0) r.valid = false;
+  }
+  return r;
+}
+
 template <bool COUNT>
 __global__ __launch_bounds__(256) RTMI_OCC void k_render_fast(const FastParams params_by_value) {
   (void)params_by_value;  // read through params() (kernarg segment)
   KP p = params();
-  __shared__ float lds[4][kLdsSlots][64];  // 4 waves per 256-thread block
-  LdsF* ls = (LdsF*)&lds[threadIdx.x >> 6][0][__lane_id()];
-  const int lane = (int)__lane_id();
-  const int wave = (int)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
-  const int L = p->lanes_per_px;
-  const int sub = lane & (L - 1);
-  const int pix = lane >> p->log2_lanes;
-  const int tpx = pix % p->tile_x, tpy = pix / p->tile_x;
-  const int iters = (p->spp + L - 1) / L;
-  const bool grid_aa = p->aa_kind != 0;
-  const int m = p->grid_m;
-  const int si0 = sub % m, sj0 = sub / m;  // grid coordinates of this lane's first sample
-  const int dli = L % m, dlj = L / m;      // advance of the grid coordinates per iteration
+  __shared__ float lds[4][kLdsSlots][64];            // 4 waves per 256-thread block
+  __shared__ unsigned long long lds_tot[4][kStatSlots];  // per-wave 64-bit Stats totals
+  const int wib = (int)(threadIdx.x >> 6);
+  LdsF* ls = (LdsF*)&lds[wib][0][__lane_id()];
+  if (__lane_id() < (unsigned)kStatSlots) lds_tot[wib][__lane_id()] = 0ull;
   Stats32 ws;
 #pragma unroll
   for (int k = 0; k < kStatSlots; ++k) ws.v[k] = 0u;
-  unsigned long long tot = 0ull;
 
   // Work queue: the grid is exactly the resident waves (host: occupancy
   // query) and each wave pulls chunks of p->chunk pixel groups. One head word
   // saturates near 90 dequeues/us, so the heads are sharded 8 ways, one per
   // blockIdx % 8 label (blocks sharing an XCD; fewer shards when the grid
-  // has fewer than 8 blocks, so every shard has pullers), each on its own 128-B line;
-  // shard k hands out chunks k, k+8, k+16, ... so every shard's work is
-  // spread over the whole image. The next chunk's index is fetched one chunk
-  // ahead, hiding the atomic's latency behind the samples.
+  // has fewer than 8 blocks, so every shard has pullers), each on its own
+  // 128-B line; shard k hands out chunks k, k+8, k+16, ... so every shard's
+  // work is spread over the whole image. The next chunk's index is fetched
+  // one chunk ahead, hiding the atomic's latency behind the samples.
   const int shard = (int)(blockIdx.x % (unsigned int)p->shards);
   unsigned int* head = p->queue + shard * kQueueStride;
-  const int C = p->chunk;
   int qj = 0;
-  if (lane == 0) qj = (int)atomicAdd(head, 1u);
+  if (__lane_id() == 0) qj = (int)atomicAdd(head, 1u);
   qj = __builtin_amdgcn_readfirstlane(qj);
   int qj_next = 0;
-  if (lane == 0) qj_next = (int)atomicAdd(head, 1u);
-  int g = (qj * p->shards + shard) * C;
+  if (__lane_id() == 0) qj_next = (int)atomicAdd(head, 1u);
+  int g = (qj * p->shards + shard) * p->chunk;
   int in_chunk = 0;
   while (g < p->ngroups) {
     p = params();
-    const int gx = g % p->tiles_x, gy = g / p->tiles_x;
-    const int j = gx * p->tile_x + tpx;
-    const int k = gy * p->tile_y + tpy;
-    const int x = j * p->step;
-    int y, out_row;
-    bool valid = j < p->ncols && k < p->nrows;
-    if (p->mode == 0) {
-      y = p->y0 + k * p->step;
-      out_row = y;
-    } else {
-      const int lb = k / p->band_h, rr = k % p->band_h;
-      y = (lb * p->world + p->rank) * p->band_h + rr;
-      out_row = k;
-      valid = valid && y < p->height;
-    }
-    if (p->step < p->max_step) {  // progressive refinement skip (renderer.nim:175-178)
-      const int mask = p->step * 2 - 1;
-      if ((x & mask) == 0 && (y & mask) == 0) valid = false;
-    }
+    const int L = p->lanes_per_px;
+    const int iters = (p->spp + L - 1) / L;
+    const GroupPix gp = group_pixel(p, g, lane_id_fresh());
     Acc pacc;
     pacc.v = f3(0.0f, 0.0f, 0.0f);
-    int bi = 0, bj = 0;  // grid coordinates of sample it*L (wave-uniform)
     for (int it = 0; it < iters; ++it) {
       p = params();
-      const bool sv = valid && it * L + sub < p->spp;
-      float px = (float)x, py = (float)y;
-      if (grid_aa) {  // grid() sampling.nim:5-18
-        int si = bi + si0, sj = bj + sj0;
-        if (si >= m) {
-          si -= m;
-          sj += 1;
-        }
+      const int s = it * L + gp.sub;  // this lane's sample index
+      const bool sv = gp.valid && s < p->spp;
+      float px = (float)gp.x, py = (float)gp.y;
+      if (p->aa_kind != 0) {  // grid() sampling.nim:5-18: sample s = (si, sj)
+        int si;
+        const int sj = div_small(s, p->grid_m, p->sample_step, si);
         px += __builtin_fmaf((float)si, p->sample_step, p->sample_off);
         py += __builtin_fmaf((float)sj, p->sample_step, p->sample_off);
       }
@@ -628,44 +642,51 @@ __global__ __launch_bounds__(256) RTMI_OCC void k_render_fast(const FastParams p
 #ifdef RTMI_STAMPS
       { RT_STAMP(t_s1); RT_ACC(7, t_s0, t_s1); }
 #endif
-      bi += dli;
-      bj += dlj;
-      if (bi >= m) {
-        bi -= m;
-        bj += 1;
-      }
     }
-    flush(ws, tot, lane);
+    p = params();
+    const int lane = lane_id_fresh();
     F3 acc = pacc.v;
     for (int off = 1; off < L; off <<= 1) {
       acc.x += __shfl_xor(acc.x, off);
       acc.y += __shfl_xor(acc.y, off);
       acc.z += __shfl_xor(acc.z, off);
     }
-    if (valid && sub == 0) {
-      if (grid_aa) acc = f3(acc.x * p->inv_len, acc.y * p->inv_len, acc.z * p->inv_len);
+    if (gp.valid && gp.sub == 0) {
+      if (p->aa_kind != 0) acc = f3(acc.x * p->inv_len, acc.y * p->inv_len, acc.z * p->inv_len);
       if (p->mode == 0 && p->step > 1) {
-        const int xe = min(x + p->step, p->width), ye = min(y + p->step, p->height);
-        for (int yy = y; yy < ye; ++yy)
-          for (int xx = x; xx < xe; ++xx) {
+        const int xe = min(gp.x + p->step, p->width), ye = min(gp.y + p->step, p->height);
+        for (int yy = gp.y; yy < ye; ++yy)
+          for (int xx = gp.x; xx < xe; ++xx) {
             float* q = p->fb + ((size_t)yy * p->width + xx) * 3;
             q[0] = acc.x; q[1] = acc.y; q[2] = acc.z;
           }
       } else {
-        float* q = p->fb + ((size_t)out_row * p->width + x) * 3;
+        float* q = p->fb + ((size_t)gp.out_row * p->width + gp.x) * 3;
         q[0] = acc.x; q[1] = acc.y; q[2] = acc.z;
       }
     }
-    if (++in_chunk < C && g + 1 < p->ngroups) {
+    if (++in_chunk < p->chunk && g + 1 < p->ngroups) {
       ++g;
     } else {
+      // per chunk: 32-bit wave counters -> the wave's 64-bit LDS totals
+      if (lane < kStatSlots) {
+        unsigned int v = 0u;
+#pragma unroll
+        for (int k = 0; k < kStatSlots; ++k) v = lane == k ? ws.v[k] : v;
+        lds_tot[wib][lane] += v;
+      }
+#pragma unroll
+      for (int k = 0; k < kStatSlots; ++k) ws.v[k] = 0u;
       in_chunk = 0;
       qj = __builtin_amdgcn_readfirstlane(qj_next);
       if (lane == 0) qj_next = (int)atomicAdd(head, 1u);
-      g = (qj * p->shards + shard) * C;
+      g = (qj * p->shards + shard) * p->chunk;
     }
   }
-  if (lane < kStatSlots) p->partials[(size_t)wave * kStatSlots + lane] = tot;
+  p = params();
+  const int lane = (int)__lane_id();
+  const int wave = (int)(blockIdx.x * (blockDim.x >> 6) + threadIdx.x / 64u);
+  if (lane < kStatSlots) p->partials[(size_t)wave * kStatSlots + lane] = lds_tot[wib][lane];
 }
 
 }  // namespace fast

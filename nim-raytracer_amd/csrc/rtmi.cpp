@@ -765,6 +765,9 @@ void fill_fast(rt_scene* s, const rt_options* o, const Mapping& mp, float* fb, F
   p.log2_lanes = pl.log2L;
   p.tile_x = pl.tx;
   p.tile_y = pl.ty;
+  p.log2_tile_x = 0;
+  while ((1 << p.log2_tile_x) < pl.tx) ++p.log2_tile_x;
+  p.inv_band_h = mp.band_h > 0 ? (float)(1.0 / (double)mp.band_h) : 0.0f;
   p.tiles_x = pl.tiles_x;
   p.ngroups = pl.ngroups;
   // 4 groups per dequeue once every wave gets many chunks (tail <= 4 groups);
