@@ -226,7 +226,7 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
-                "kernel": "k_render<float>",
+                "kernel": "k_render_fast<false>",
                 "kernel_ms": round(kern_ms, 4),
                 "bytes_per_launch": int(bytes_launch),
                 "lane_node_visits": counters["lane_node_visits"],
