@@ -14,7 +14,7 @@ one RCCL all-gather + an on-GPU un-interleave assembles the frame on rank 0
 
 Printed (rank 0, one JSON line): value = (primary + shadow rays of all ranks)
 x K / max-over-ranks wall time, plus
-  roofline     — the dominant kernel (k_render<float>): bytes its BVH
+  roofline     — the dominant kernel (k_render_fast<false>): bytes its BVH
                  traversal fetches (wave-level node + triangle records, counted
                  on the GPU) / its average duration, timed live with HIP events
                  on the stream it runs on, vs the 8 TB/s HBM peak; `traffic` is
