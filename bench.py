@@ -53,9 +53,10 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(scene, width, height, target_s):
-    """The oracle (reference algorithm, fp64, brute-force mesh) on a uniform
-    row subsample of the same frame at 1 spp, on this host's cores."""
+def cpu_baseline(scene, width, height, target_s, bvh=False):
+    """The oracle (reference algorithm, fp64; bvh=False: the reference's
+    brute-force mesh loop, bvh=True: the same answers from a per-ray BVH) on
+    a uniform row subsample of the same frame at 1 spp, on this host's cores."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle
     from rtmi import Antialias, Options, Precision, akGrid
@@ -67,15 +68,26 @@ def cpu_baseline(scene, width, height, target_s):
     threads = max(1, min(16, ncpu))  # the GPU box's CPU share is 16 threads
     opts = Options(width=width, height=height, antialias=Antialias(akGrid, 1), bias=1e-4,
                    precision=Precision.fp64)
-    osc = oracle.OracleScene(scene)
-    # calibrate on a sparse probe, then size the sample to ~target_s
+    osc = oracle.OracleScene(scene, bvh=bvh)
+    # calibrate on a sparse probe, then size the sample to ~target_s: a row
+    # subsample at 1 spp, or (a fast CPU path) the whole frame at m x m spp
     probe = list(range(7, height, max(1, height // 24)))
     _, st, secs = osc.render(opts, rows=probe, nthreads=threads)
     per_row = secs / len(probe)
     n = int(max(len(probe), min(height, target_s / max(per_row, 1e-6))))
+    grid = 1
+    if n >= height:
+        grid = max(1, min(16, int((target_s / max(per_row * height, 1e-6)) ** 0.5)))
+        opts = Options(width=width, height=height, antialias=Antialias(akGrid, grid), bias=1e-4,
+                       precision=Precision.fp64)
     stride = max(1, height // n)
     rows = list(range(stride // 2, height, stride))
     _, st, secs = osc.render(opts, rows=rows, nthreads=threads)
+    if n >= height and grid < 16 and secs < target_s / 3:  # one refinement of the sample size
+        grid = max(grid, min(16, int(grid * (target_s / max(secs, 1e-6)) ** 0.5)))
+        opts = Options(width=width, height=height, antialias=Antialias(akGrid, grid), bias=1e-4,
+                       precision=Precision.fp64)
+        _, st, secs = osc.render(opts, rows=rows, nthreads=threads)
     rays = st.numPrimaryRays + st.numShadowRays
     return {
         "value": rays / secs / 1e6,
@@ -83,9 +95,11 @@ def cpu_baseline(scene, width, height, target_s):
         "cores": threads,
         "kind": "port",
         "sample": (f"oracle/rt_oracle.c (fp64 restatement of the reference path: linear object loop, "
-                   f"brute-force TriangleMesh.intersect, scanline pool of {threads} threads), same "
-                   f"scene/camera at 1 spp (akGrid 1), {len(rows)} of {height} rows (every "
-                   f"{stride}th), {rays} rays in {secs:.2f} s"),
+                   + ("per-ray fp64 binned-SAH BVH with the brute-force loop's exact answers"
+                      if bvh else "brute-force TriangleMesh.intersect")
+                   + f", scanline pool of {threads} threads), same scene/camera at {grid * grid} spp "
+                   f"(akGrid {grid}), "
+                   f"{len(rows)} of {height} rows (every {stride}th), {rays} rays in {secs:.2f} s"),
     }
 
 
@@ -238,6 +252,9 @@ def main():
         }
         if world == 1 and not args.no_cpu:
             out["cpu_baseline"] = cpu_baseline(scene, W, H, args.cpu_seconds)
+            # the same algorithm class on the CPU (BVH), so the
+            # GPU/CPU ratio is also judged against a fair CPU implementation
+            out["cpu_baseline_same_bvh"] = cpu_baseline(scene, W, H, args.cpu_seconds, bvh=True)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

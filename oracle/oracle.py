@@ -36,6 +36,8 @@ def _load():
     lib.oracle_scene_create.argtypes = [C.POINTER(abi.rt_scene_desc)]
     lib.oracle_scene_destroy.restype = None
     lib.oracle_scene_destroy.argtypes = [P]
+    lib.oracle_scene_build_bvh.restype = C.c_int
+    lib.oracle_scene_build_bvh.argtypes = [P]
     lib.oracle_render_line.restype = C.c_int
     lib.oracle_render_line.argtypes = [P, C.POINTER(abi.rt_options), C.POINTER(C.c_float),
                                        C.c_int32, C.c_int32, C.c_int32, C.POINTER(abi.rt_stats)]
@@ -81,13 +83,17 @@ def _dp(a):
 
 
 class OracleScene:
-    """The reference algorithm over one flattened scene (fp64, brute force)."""
+    """The reference algorithm over one flattened scene (fp64). bvh=False:
+    the reference's brute-force face loop; bvh=True: the same answers from a
+    per-ray fp64 BVH (the "CPU same-BVH" baseline)."""
 
-    def __init__(self, scene):
+    def __init__(self, scene, bvh=False):
         self.flat = flatten(scene)
         self.h = lib().oracle_scene_create(C.byref(self.flat.desc))
         if not self.h:
             raise ValueError("oracle rejected the scene description")
+        if bvh:
+            lib().oracle_scene_build_bvh(self.h)
 
     def close(self):
         if self.h:

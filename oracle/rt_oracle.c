@@ -175,12 +175,23 @@ static double ray_triangle(v4 o, v4 d, const double *v0, const double *v1,
 
 /* ---- scene --------------------------------------------------------------- */
 
+/* Same-BVH CPU baseline (SURVEY.md 8(d) "CPU same-BVH"): a per-ray fp64
+ * BVH over the mesh, built by oracle_scene_build_bvh. count > 0: leaf over
+ * order[first, first + count); else children left / right. */
+typedef struct {
+  double lo[3], hi[3];
+  int32_t left, right, first, count;
+} obvh_node;
+
 typedef struct {
   int64_t nv, nf;
   double *vertices; /* nv*3 */
   int32_t *faces;   /* nf*3 */
   double *normals;  /* nf*3 face normals */
   v4 aabb[2];       /* calcAABB (geom.nim:175-188) */
+  obvh_node *bvh;   /* NULL: brute force (the reference's loop) */
+  int32_t *order;
+  int32_t nbvh;
 } oracle_mesh;
 
 struct oracle_scene {
@@ -269,6 +280,8 @@ void oracle_scene_destroy(oracle_scene *s) {
     free(s->meshes[m].vertices);
     free(s->meshes[m].faces);
     free(s->meshes[m].normals);
+    free(s->meshes[m].bvh);
+    free(s->meshes[m].order);
   }
   free(s->meshes);
   free(s->objects);
@@ -294,6 +307,206 @@ static double mesh_intersect(const oracle_mesh *m, ray_t *r) {
   return tmin;
 }
 
+/* ---- same-BVH baseline ------------------------------------------------- */
+/* Binned SAH (16 bins, <= 4 faces per leaf, median fallback) over fp64 face
+ * bounds inflated by 2^-30 of the mesh scale, so a face the exact
+ * Moller-Trumbore test hits is never culled by a box. The traversal keeps
+ * the brute-force loop's answer exactly: a face replaces the best when
+ * t >= 0 and (t < best or t == best with a lower face index), and a box is
+ * skipped only when its entry distance exceeds the best (ties visited).
+ * tests/test_oracle_bvh.py checks image + Stats equality with brute force. */
+typedef struct {
+  const oracle_mesh *m;
+  double *blo, *bhi, *cen; /* per-face bounds / centroids */
+  int32_t *idx;
+  obvh_node *nodes;
+  int32_t nnodes, cap;
+  double eps;
+} obvh_builder;
+
+static int32_t obvh_new(obvh_builder *B) {
+  if (B->nnodes == B->cap) {
+    B->cap = B->cap ? 2 * B->cap : 1024;
+    B->nodes = (obvh_node *)realloc(B->nodes, sizeof(obvh_node) * (size_t)B->cap);
+  }
+  return B->nnodes++;
+}
+
+static int32_t obvh_build(obvh_builder *B, int32_t b, int32_t e) {
+  const int32_t me = obvh_new(B);
+  double lo[3] = {POS_INF, POS_INF, POS_INF}, hi[3] = {NEG_INF, NEG_INF, NEG_INF};
+  double clo[3] = {POS_INF, POS_INF, POS_INF}, chi[3] = {NEG_INF, NEG_INF, NEG_INF};
+  for (int32_t i = b; i < e; ++i) {
+    const int32_t f = B->idx[i];
+    for (int a = 0; a < 3; ++a) {
+      lo[a] = fmin(lo[a], B->blo[3 * f + a]);
+      hi[a] = fmax(hi[a], B->bhi[3 * f + a]);
+      clo[a] = fmin(clo[a], B->cen[3 * f + a]);
+      chi[a] = fmax(chi[a], B->cen[3 * f + a]);
+    }
+  }
+  for (int a = 0; a < 3; ++a) {
+    B->nodes[me].lo[a] = lo[a] - B->eps;
+    B->nodes[me].hi[a] = hi[a] + B->eps;
+  }
+  const int32_t n = e - b;
+  if (n <= 4) {
+    B->nodes[me].first = b;
+    B->nodes[me].count = n;
+    B->nodes[me].left = B->nodes[me].right = -1;
+    return me;
+  }
+  int axis = 0;
+  for (int a = 1; a < 3; ++a)
+    if (chi[a] - clo[a] > chi[axis] - clo[axis]) axis = a;
+  int32_t mid = -1;
+  if (chi[axis] > clo[axis]) { /* binned SAH on the widest centroid axis */
+    enum { NB = 16 };
+    int32_t cnt[NB] = {0};
+    double blo[NB][3], bhi[NB][3];
+    for (int k = 0; k < NB; ++k)
+      for (int a = 0; a < 3; ++a) { blo[k][a] = POS_INF; bhi[k][a] = NEG_INF; }
+    const double scale = NB / (chi[axis] - clo[axis]);
+    for (int32_t i = b; i < e; ++i) {
+      const int32_t f = B->idx[i];
+      int k = (int)((B->cen[3 * f + axis] - clo[axis]) * scale);
+      k = k < 0 ? 0 : (k >= NB ? NB - 1 : k);
+      cnt[k]++;
+      for (int a = 0; a < 3; ++a) {
+        blo[k][a] = fmin(blo[k][a], B->blo[3 * f + a]);
+        bhi[k][a] = fmax(bhi[k][a], B->bhi[3 * f + a]);
+      }
+    }
+    double best = POS_INF;
+    int best_k = -1;
+    for (int k = 0; k < NB - 1; ++k) { /* split after bin k */
+      double l_lo[3] = {POS_INF, POS_INF, POS_INF}, l_hi[3] = {NEG_INF, NEG_INF, NEG_INF};
+      double r_lo[3] = {POS_INF, POS_INF, POS_INF}, r_hi[3] = {NEG_INF, NEG_INF, NEG_INF};
+      int32_t nl = 0, nr = 0;
+      for (int j = 0; j < NB; ++j) {
+        double *L = j <= k ? l_lo : r_lo, *H = j <= k ? l_hi : r_hi;
+        if (j <= k) nl += cnt[j]; else nr += cnt[j];
+        for (int a = 0; a < 3; ++a) { L[a] = fmin(L[a], blo[j][a]); H[a] = fmax(H[a], bhi[j][a]); }
+      }
+      if (!nl || !nr) continue;
+      const double al = (l_hi[0] - l_lo[0]) * (l_hi[1] - l_lo[1]) + (l_hi[1] - l_lo[1]) * (l_hi[2] - l_lo[2]) +
+                        (l_hi[2] - l_lo[2]) * (l_hi[0] - l_lo[0]);
+      const double ar = (r_hi[0] - r_lo[0]) * (r_hi[1] - r_lo[1]) + (r_hi[1] - r_lo[1]) * (r_hi[2] - r_lo[2]) +
+                        (r_hi[2] - r_lo[2]) * (r_hi[0] - r_lo[0]);
+      const double cost = al * nl + ar * nr;
+      if (cost < best) { best = cost; best_k = k; }
+    }
+    if (best_k >= 0) {
+      int32_t i = b, j = e - 1;
+      while (i <= j) {
+        const int32_t f = B->idx[i];
+        int k = (int)((B->cen[3 * f + axis] - clo[axis]) * scale);
+        k = k < 0 ? 0 : (k >= NB ? NB - 1 : k);
+        if (k <= best_k) { ++i; } else { const int32_t t = B->idx[i]; B->idx[i] = B->idx[j]; B->idx[j] = t; --j; }
+      }
+      mid = i;
+    }
+  }
+  if (mid <= b || mid >= e) mid = b + n / 2; /* degenerate: split the list */
+  const int32_t l = obvh_build(B, b, mid);
+  const int32_t r = obvh_build(B, mid, e);
+  B->nodes[me].left = l;
+  B->nodes[me].right = r;
+  B->nodes[me].first = 0;
+  B->nodes[me].count = 0;
+  return me;
+}
+
+int oracle_scene_build_bvh(oracle_scene *s) {
+  for (int32_t mi = 0; mi < s->nmesh; ++mi) {
+    oracle_mesh *m = &s->meshes[mi];
+    if (m->bvh || m->nf <= 0) continue;
+    obvh_builder B;
+    memset(&B, 0, sizeof B);
+    B.m = m;
+    B.blo = (double *)malloc(sizeof(double) * 3 * (size_t)m->nf);
+    B.bhi = (double *)malloc(sizeof(double) * 3 * (size_t)m->nf);
+    B.cen = (double *)malloc(sizeof(double) * 3 * (size_t)m->nf);
+    B.idx = (int32_t *)malloc(sizeof(int32_t) * (size_t)m->nf);
+    double mag = 0.0;
+    for (int64_t f = 0; f < m->nf; ++f) {
+      B.idx[f] = (int32_t)f;
+      for (int a = 0; a < 3; ++a) {
+        double lo = POS_INF, hi = NEG_INF;
+        for (int k = 0; k < 3; ++k) {
+          const double x = m->vertices[3 * m->faces[3 * f + k] + a];
+          lo = fmin(lo, x);
+          hi = fmax(hi, x);
+        }
+        B.blo[3 * f + a] = lo;
+        B.bhi[3 * f + a] = hi;
+        B.cen[3 * f + a] = 0.5 * (lo + hi);
+        mag = fmax(mag, fmax(fabs(lo), fabs(hi)));
+      }
+    }
+    B.eps = ldexp(mag, -30) + 1e-300;
+    obvh_build(&B, 0, (int32_t)m->nf);
+    m->bvh = B.nodes;
+    m->nbvh = B.nnodes;
+    m->order = B.idx;
+    free(B.blo);
+    free(B.bhi);
+    free(B.cen);
+  }
+  return 0;
+}
+
+/* Entry distance of a conservative slab test (NaN products from 0 * inf are
+ * ignored by fmin/fmax, i.e. never cull); +inf on a miss. */
+static double obvh_enter(const obvh_node *nd, const ray_t *r) {
+  double tn = NEG_INF, tf = POS_INF;
+  const double o[3] = {r->orig.x, r->orig.y, r->orig.z};
+  for (int a = 0; a < 3; ++a) {
+    const double t0 = (nd->lo[a] - o[a]) * r->inv[a], t1 = (nd->hi[a] - o[a]) * r->inv[a];
+    tn = fmax(tn, fmin(t0, t1));
+    tf = fmin(tf, fmax(t0, t1));
+  }
+  tf = tf * (1.0 + 1e-12) + 1e-300;
+  return (tn <= tf && tf >= 0.0) ? tn : POS_INF;
+}
+
+static double mesh_intersect_bvh(const oracle_mesh *m, ray_t *r) {
+  if (aabb_intersect(m->aabb, r) < 0) return NEG_INF; /* the reference's gate */
+  double tmin = POS_INF;
+  int64_t best = -1;
+  int32_t stack[128];
+  int sp = 0;
+  stack[sp++] = 0;
+  if (obvh_enter(&m->bvh[0], r) == POS_INF) return tmin;
+  while (sp) {
+    /* entry distances are re-tested at pop: the best may have shrunk */
+    const obvh_node *nd = &m->bvh[stack[--sp]];
+    if (obvh_enter(nd, r) > tmin) continue;
+    if (nd->count > 0) {
+      for (int32_t i = nd->first; i < nd->first + nd->count; ++i) {
+        const int32_t f = m->order[i];
+        const int32_t *fi = &m->faces[3 * (int64_t)f];
+        const double t = ray_triangle(r->orig, r->dir, &m->vertices[3 * fi[0]],
+                                      &m->vertices[3 * fi[1]], &m->vertices[3 * fi[2]]);
+        if (t >= 0 && (t < tmin || (t == tmin && f < best))) {
+          tmin = t;
+          best = f;
+        }
+      }
+    } else {
+      /* +inf = the box is missed: never pushed (tmin may still be +inf) */
+      const double tl = obvh_enter(&m->bvh[nd->left], r), tr = obvh_enter(&m->bvh[nd->right], r);
+      const int near_left = tl <= tr;
+      const int32_t nn = near_left ? nd->left : nd->right, fn = near_left ? nd->right : nd->left;
+      const double tnn = near_left ? tl : tr, tfn = near_left ? tr : tl;
+      if (tfn != POS_INF && tfn <= tmin) stack[sp++] = fn; /* far first, near popped next */
+      if (tnn != POS_INF && tnn <= tmin) stack[sp++] = nn;
+    }
+  }
+  if (best >= 0) r->tri_hit = best;
+  return tmin;
+}
+
 static double object_intersect(const oracle_scene *s, const rt_object_desc *ob, ray_t *r) {
   switch (ob->type) {
     case RT_SPHERE: return sphere_intersect(ob->radius, r);
@@ -303,7 +516,10 @@ static double object_intersect(const oracle_scene *s, const rt_object_desc *ob, 
                        {ob->box_max[0], ob->box_max[1], ob->box_max[2], 0.0}};
       return aabb_intersect(b, r);
     }
-    case RT_MESH: return mesh_intersect(&s->meshes[ob->mesh], r);
+    case RT_MESH: {
+      const oracle_mesh *m = &s->meshes[ob->mesh];
+      return m->bvh ? mesh_intersect_bvh(m, r) : mesh_intersect(m, r);
+    }
     default: return NEG_INF; /* Geometry.intersect base (geom.nim:213) */
   }
 }

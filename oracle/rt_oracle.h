@@ -19,6 +19,9 @@ typedef struct oracle_scene oracle_scene;
 
 oracle_scene *oracle_scene_create(const rt_scene_desc *desc);
 void oracle_scene_destroy(oracle_scene *s);
+/* Switch mesh intersection from the reference's brute-force face loop to a
+ * per-ray fp64 BVH with the same answers (the "CPU same-BVH" baseline). */
+int oracle_scene_build_bvh(oracle_scene *s);
 
 /* renderLine (renderer.nim:162-211) for one row. fb is w*h*3 float32. */
 int oracle_render_line(const oracle_scene *s, const rt_options *o, float *fb,
