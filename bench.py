@@ -14,12 +14,15 @@ one RCCL all-gather + an on-GPU un-interleave assembles the frame on rank 0
 
 Printed (rank 0, one JSON line): value = (primary + shadow rays of all ranks)
 x K / max-over-ranks wall time, plus
-  roofline     — the dominant kernel (k_render_fast<false>): bytes its BVH
-                 traversal fetches (wave-level node + triangle records, counted
-                 on the GPU) / its average duration, timed live with HIP events
-                 on the stream it runs on, vs the 8 TB/s HBM peak; `traffic` is
-                 the PMC-measured HBM bytes per launch from the committed
-                 rocprofv3 summary (profiles/), or null;
+  roofline     — the dominant kernel (k_render_fast<false>): SURVEY 8(d)'s
+                 algorithmic bytes (per ray 32 B per BVH box tested + 36 B per
+                 triangle tested + 12 B per pixel, counts from one instrumented
+                 launch) / its average duration, timed live with HIP events on
+                 the stream it runs on, vs the 8 TB/s HBM peak; also the bytes
+                 the wave-coherent kernel actually requests (one record fetch
+                 serves 64 lanes); `traffic` is the PMC-measured HBM bytes per
+                 launch from the committed rocprofv3 summary (profiles/), or
+                 null;
   cpu_baseline — the fp64 oracle (the reference algorithm: linear objects,
                  brute-force mesh, scanline thread pool) on this host, 1 spp on
                  a bounded row subsample of the same frame (rank 0, N = 1 only).
@@ -34,9 +37,30 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "nim-raytracer_amd"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md "Chip-level parameters")
-NODE_BYTES = 64        # one BvhNode record (two child boxes + refs)
+# SURVEY.md 8(d) algorithmic bytes per ray: 32 B per BVH box tested (a node
+# record visited = its two child boxes = 64 B), 36 B per triangle tested (three
+# fp32 vertices, the .geom record), 12 B per pixel written (12/spp per ray)
+SURVEY_BOX_BYTES = 32
+SURVEY_TRI_BYTES = 36
+PIXEL_BYTES = 12
+NODE_BYTES = 64        # what the kernel fetches: one BvhNode record (two child boxes + refs)
 TRI_BYTES = 64         # one TriFast record (v0, e2, -e1, -n, face id)
 BAND_H = 16
+
+
+def _scene(name):
+    from rtmi import scenes
+    return {"bunny": scenes.mesh_bunny, "boxes2": scenes.boxes2, "torus": scenes.torus_scene}[name]()
+
+
+# BASELINE.json configs on one GPU (C4/C5 are quoted on 8 GPUs; at N=1 this is
+# one GPU's whole frame, at N>1 the band-sharded frame)
+CONFIGS = {
+    "C2": ("boxes2", 1920, 1080, 8, "C2: boxes2.nim (16 analytic primitives, 1 distant light)"),
+    "C3": ("bunny", 1920, 1080, 16, "C3: bunny.geom baked x30 + ground plane, mesh-bunny.nim lights/camera"),
+    "C4": ("bunny", 3840, 2160, 32, "C4: bunny.geom baked x30 + ground plane, mesh-bunny.nim lights/camera"),
+    "C5": ("torus", 3840, 2160, 64, "C5: 1,000,000-triangle procedural torus + ground, mesh-bunny.nim lights/camera"),
+}
 
 
 def parse():
@@ -44,9 +68,11 @@ def parse():
     ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--width", type=int, default=1920)
-    ap.add_argument("--height", type=int, default=1080)
-    ap.add_argument("--grid", type=int, default=16, help="akGrid m (spp = m*m)")
+    ap.add_argument("--config", default="C3", choices=sorted(CONFIGS),
+                    help="BASELINE.json config (C3 = the headline metric)")
+    ap.add_argument("--width", type=int, default=None)
+    ap.add_argument("--height", type=int, default=None)
+    ap.add_argument("--grid", type=int, default=None, help="akGrid m (spp = m*m)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--flags", type=int, default=0, help="rt_options.flags (1 = any-hit shadows)")
@@ -134,8 +160,11 @@ def main():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
-    W, H, m = args.width, args.height, args.grid
-    scene = scenes.mesh_bunny()
+    scene_name, W, H, m, desc = CONFIGS[args.config]
+    W = args.width or W
+    H = args.height or H
+    m = args.grid or m
+    scene = _scene(scene_name)
     t0 = time.time()
     ds = DeviceScene(scene, device=local)
     info = ds.info()
@@ -203,16 +232,23 @@ def main():
     kern_ms = sum(a.elapsed_time(b) for a, b in evs) / max(1, args.steps)
 
     value = rays_frame * args.steps / elapsed / 1e6
-    # algorithmic traffic of one k_render launch on this rank (wave-level record fetches)
-    bytes_launch = (counters["wave_node_fetches"] * NODE_BYTES + counters["wave_tri_fetches"] * TRI_BYTES
-                    + rows * W * 12)
+    # algorithmic bytes of one launch on this rank, SURVEY.md 8(d): per ray
+    # 32 B x boxes tested + 36 B x triangles tested + 12/spp B, summed over
+    # the launch's rays (per-ray visit counts from the instrumented launch)
+    bytes_launch = (counters["lane_node_visits"] * 2 * SURVEY_BOX_BYTES
+                    + counters["lane_tri_tests"] * SURVEY_TRI_BYTES + rows * W * PIXEL_BYTES)
     achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
-    workload_key = f"c3_{W}x{H}_m{m}_world{world}"
+    # what the wave-coherent kernel actually requests: one record fetch serves
+    # all 64 lanes of a wave
+    fetch_bytes = (counters["wave_node_fetches"] * NODE_BYTES + counters["wave_tri_fetches"] * TRI_BYTES
+                   + rows * W * PIXEL_BYTES)
+    workload_key = f"{args.config.lower()}_{W}x{H}_m{m}_world{world}"
     traffic = load_traffic(workload_key)
 
     if rank == 0:
         out = {
-            "metric": "Mray/s (primary+shadow) on bunny.geom 1080p/256spp; 1/2/4/8-GPU scaling",
+            "metric": ("Mray/s (primary+shadow) on bunny.geom 1080p/256spp; 1/2/4/8-GPU scaling"
+                       if args.config == "C3" else f"Mray/s (primary+shadow) on {args.config}"),
             "value": round(value, 2),
             "unit": "Mray/s",
             "n_gpus": world,
@@ -223,10 +259,11 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic rays over the reference's bunny.geom fixture (69,451 triangles)",
+            "data": {"bunny": "synthetic rays over the reference's bunny.geom fixture (69,451 triangles)",
+                     "boxes2": "synthetic rays over the reference's boxes2.nim scene",
+                     "torus": "synthetic rays over a deterministic procedural 1M-triangle torus"}[scene_name],
             "config": {
-                "workload": ("C3: bunny.geom baked x30 + ground plane, mesh-bunny.nim lights/camera, "
-                             f"{W}x{H}, akGrid {m}x{m} = {m * m} spp, fp32, {BAND_H}-row bands "
+                "workload": (f"{desc}, {W}x{H}, akGrid {m}x{m} = {m * m} spp, fp32, {BAND_H}-row bands "
                              f"round-robin over {world} GPU(s) + RCCL all-gather"),
                 "width": W, "height": H, "spp": m * m, "triangles": info["num_triangles"],
                 "bvh_nodes": info["num_bvh_nodes"], "primary_rays_per_frame": prim_frame,
@@ -243,6 +280,9 @@ def main():
                 "kernel": "k_render_fast<false>",
                 "kernel_ms": round(kern_ms, 4),
                 "bytes_per_launch": int(bytes_launch),
+                "definition": "SURVEY 8(d): 32 B/box + 36 B/triangle tested per ray + 12 B/pixel",
+                "record_fetch_bytes_per_launch": int(fetch_bytes),
+                "record_fetch_gbs": round(fetch_bytes / (kern_ms * 1e-3) / 1e9, 1),
                 "lane_node_visits": counters["lane_node_visits"],
                 "lane_tri_tests": counters["lane_tri_tests"],
                 "wave_node_fetches": counters["wave_node_fetches"],
@@ -251,7 +291,10 @@ def main():
             "cpu_baseline": None,
         }
         if world == 1 and not args.no_cpu:
-            out["cpu_baseline"] = cpu_baseline(scene, W, H, args.cpu_seconds)
+            # the reference's brute-force mesh loop is infeasible past ~200k
+            # triangles (~1e11 triangle tests per 4K row): same-BVH only there
+            if info["num_triangles"] <= 200_000:
+                out["cpu_baseline"] = cpu_baseline(scene, W, H, args.cpu_seconds)
             # the same algorithm class on the CPU (BVH), so the
             # GPU/CPU ratio is also judged against a fair CPU implementation
             out["cpu_baseline_same_bvh"] = cpu_baseline(scene, W, H, args.cpu_seconds, bvh=True)

@@ -154,7 +154,8 @@ typedef struct rt_stats {
 typedef struct rt_traversal_counters {
   uint64_t wave_node_fetches;  /* BVH node records fetched (per wave)     */
   uint64_t wave_tri_fetches;   /* triangle records fetched (per wave)     */
-  uint64_t lane_node_visits;   /* sum over rays of node records visited   */
+  uint64_t lane_node_visits;   /* sum over rays of node records visited
+                                  (a ray visits a node whose box it hit)  */
   uint64_t lane_tri_tests;     /* sum over rays of triangle tests         */
 } rt_traversal_counters;
 

@@ -221,11 +221,17 @@ __device__ __forceinline__ void traverse(KP p, int root, F3 o, F3 d, bool active
   int stack = 0;
   int sp = 0;
   int node = root;
+  // COUNT only: the lanes whose own ray hit the current node's box at its
+  // parent (per-ray visits); far children's masks are
+  // stacked alongside (two more VGPR stacks, diagnostic kernel only)
+  unsigned long long vm = 0ull;
+  int mlo = 0, mhi = 0;
+  if constexpr (COUNT) vm = bal(tc >= 0.0f);
   for (;;) {
     const BvhNode nd = cp(p->nodes)[node];
     if constexpr (COUNT) {
       ws.v[STAT_NODE_FETCH] += 1u;
-      ws.v[STAT_LANE_NODES] += pc(bal(tc >= 0.0f));
+      ws.v[STAT_LANE_NODES] += pc(vm);
     }
     const float ax0 = __builtin_fmaf(nd.lo0[0], ni.x, -oi.x), bx0 = __builtin_fmaf(nd.hi0[0], ni.x, -oi.x);
     const float ay0 = __builtin_fmaf(nd.lo0[1], ni.y, -oi.y), by0 = __builtin_fmaf(nd.hi0[1], ni.y, -oi.y);
@@ -267,17 +273,28 @@ __device__ __forceinline__ void traverse(KP p, int root, F3 o, F3 d, bool active
       const int near = first0 ? nd.c0 : nd.c1;
       const int far = first0 ? nd.c1 : nd.c0;
       stack = (lane == sp) ? far : stack;
+      if constexpr (COUNT) {
+        const unsigned long long fm = first0 ? m1 : m0;
+        mlo = (lane == sp) ? (int)(unsigned int)fm : mlo;
+        mhi = (lane == sp) ? (int)(unsigned int)(fm >> 32) : mhi;
+        vm = first0 ? m0 : m1;
+      }
       ++sp;
       node = near;
     } else if (m0) {
       node = nd.c0;
+      if constexpr (COUNT) vm = m0;
     } else if (m1) {
       node = nd.c1;
+      if constexpr (COUNT) vm = m1;
     } else {
       if (sp == 0) break;
       if (early && bal(tc >= 0.0f) == 0ull) break;
       --sp;
       node = __builtin_amdgcn_readlane(stack, sp);
+      if constexpr (COUNT)
+        vm = (unsigned long long)(unsigned int)__builtin_amdgcn_readlane(mlo, sp) |
+             ((unsigned long long)(unsigned int)__builtin_amdgcn_readlane(mhi, sp) << 32);
     }
   }
   if (key != key0) {
