@@ -8,8 +8,8 @@ One step = one full frame of BASELINE config C3 (mesh-bunny layout: baked
 bunny.geom 69,451 triangles + ground plane, 2 distant lights, akGrid 16x16 =
 256 samples per pixel, fp32 performance mode) rendered from a scene resident
 in HBM into a device framebuffer. With N GPUs the SAME frame is cut into
-16-row bands dealt round-robin to the ranks, each rank renders its bands and
-one RCCL all-gather + an on-GPU un-interleave assembles the frame on rank 0
+4-row bands dealt round-robin to the ranks, each rank renders its bands and
+one RCCL gather + an on-GPU un-interleave assembles the frame on rank 0
 (strong scaling; the gather is inside the timed region).
 
 Printed (rank 0, one JSON line): value = (primary + shadow rays of all ranks)
@@ -45,7 +45,7 @@ SURVEY_TRI_BYTES = 36
 PIXEL_BYTES = 12
 NODE_BYTES = 64        # what the kernel fetches: one BvhNode record (two child boxes + refs)
 TRI_BYTES = 64         # one TriFast record (v0, e2, -e1, -n, face id)
-BAND_H = 16
+BAND_H = 4             # rows per band (round-robin over ranks)
 
 
 def _scene(name):
@@ -147,7 +147,7 @@ def main():
     import torch.distributed as dist
 
     from rtmi import Antialias, Options, Precision, akGrid, scenes
-    from rtmi.dist import band_rows, render_frame_distributed
+    from rtmi.dist import band_rows, gather_bands
     from rtmi.renderer import DeviceScene
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -190,7 +190,7 @@ def main():
         if time_kernel is not None:
             time_kernel[1].record(stream)
         if world > 1:
-            dist.all_gather_into_tensor(gathered, local_buf)
+            gather_bands(local_buf, gathered if rank == 0 else None, rows * W * 3)
             if rank == 0:
                 unshard_bands_device(gathered, fb, W, H, BAND_H, world, stream=stream)
 
@@ -264,7 +264,7 @@ def main():
                      "torus": "synthetic rays over a deterministic procedural 1M-triangle torus"}[scene_name],
             "config": {
                 "workload": (f"{desc}, {W}x{H}, akGrid {m}x{m} = {m * m} spp, fp32, {BAND_H}-row bands "
-                             f"round-robin over {world} GPU(s) + RCCL all-gather"),
+                             f"round-robin over {world} GPU(s) + RCCL gather to rank 0"),
                 "width": W, "height": H, "spp": m * m, "triangles": info["num_triangles"],
                 "bvh_nodes": info["num_bvh_nodes"], "primary_rays_per_frame": prim_frame,
                 "shadow_rays_per_frame": shadow_frame, "parallelism": f"bands{world}",

@@ -200,7 +200,7 @@ struct FastParams {
   float inv_len;
   float sample_step, sample_off;
   int32_t nobj, nlight, width, height;
-  int32_t aa_kind, grid_m, spp, max_depth, flags, shadow_mesh, chunk, shards, has_point_light, log2_tile_x;
+  int32_t aa_kind, grid_m, spp, max_depth, flags, shadow_mesh, shards, has_point_light, log2_tile_x;
   float inv_band_h;
   int32_t mode, y0, nrows, ncols, step, max_step, band_h, rank, world;
   int32_t lanes_per_px, log2_lanes, tile_x, tile_y, tiles_x, ngroups;

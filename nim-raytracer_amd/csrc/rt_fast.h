@@ -610,13 +610,14 @@ __global__ __launch_bounds__(256) RTMI_OCC void k_render_fast(const FastParams p
   for (int k = 0; k < kStatSlots; ++k) ws.v[k] = 0u;
 
   // Work queue: the grid is exactly the resident waves (host: occupancy
-  // query) and each wave pulls chunks of p->chunk pixel groups. One head word
-  // saturates near 90 dequeues/us, so the heads are sharded 8 ways, one per
-  // blockIdx % 8 label (blocks sharing an XCD; fewer shards when the grid
-  // has fewer than 8 blocks, so every shard has pullers), each on its own
-  // 128-B line; shard k hands out chunks k, k+8, k+16, ... so every shard's
-  // work is spread over the whole image. The next chunk's index is fetched
-  // one chunk ahead, hiding the atomic's latency behind the samples.
+  // query) and each wave pulls one work item at a time (coarser chunks left
+  // an expensive tail in every launch). One head word saturates near 90
+  // dequeues/us, so the heads are sharded 8 ways, one per blockIdx % 8 label
+  // (blocks sharing an XCD; fewer shards when the grid has fewer than 8
+  // blocks, so every shard has pullers), each on its own 128-B line; shard k
+  // hands out items k, k+8, k+16, ... so every shard's work spans the whole
+  // image. The next index is fetched one item ahead, hiding the atomic's
+  // latency behind the samples.
   const int shard = (int)(blockIdx.x % (unsigned int)p->shards);
   unsigned int* head = p->queue + shard * kQueueStride;
   int qj = 0;
@@ -624,8 +625,7 @@ __global__ __launch_bounds__(256) RTMI_OCC void k_render_fast(const FastParams p
   qj = __builtin_amdgcn_readfirstlane(qj);
   int qj_next = 0;
   if (__lane_id() == 0) qj_next = (int)atomicAdd(head, 1u);
-  int g = (qj * p->shards + shard) * p->chunk;
-  int in_chunk = 0;
+  int g = qj * p->shards + shard;
   while (g < p->ngroups) {
     p = params();
     const int L = p->lanes_per_px;
@@ -682,23 +682,18 @@ __global__ __launch_bounds__(256) RTMI_OCC void k_render_fast(const FastParams p
         q[0] = acc.x; q[1] = acc.y; q[2] = acc.z;
       }
     }
-    if (++in_chunk < p->chunk && g + 1 < p->ngroups) {
-      ++g;
-    } else {
-      // per chunk: 32-bit wave counters -> the wave's 64-bit LDS totals
-      if (lane < kStatSlots) {
-        unsigned int v = 0u;
+    // 32-bit wave counters -> the wave's 64-bit LDS totals
+    if (lane < kStatSlots) {
+      unsigned int v = 0u;
 #pragma unroll
-        for (int k = 0; k < kStatSlots; ++k) v = lane == k ? ws.v[k] : v;
-        lds_tot[wib][lane] += v;
-      }
-#pragma unroll
-      for (int k = 0; k < kStatSlots; ++k) ws.v[k] = 0u;
-      in_chunk = 0;
-      qj = __builtin_amdgcn_readfirstlane(qj_next);
-      if (lane == 0) qj_next = (int)atomicAdd(head, 1u);
-      g = (qj * p->shards + shard) * p->chunk;
+      for (int k = 0; k < kStatSlots; ++k) v = lane == k ? ws.v[k] : v;
+      lds_tot[wib][lane] += v;
     }
+#pragma unroll
+    for (int k = 0; k < kStatSlots; ++k) ws.v[k] = 0u;
+    qj = __builtin_amdgcn_readfirstlane(qj_next);
+    if (lane == 0) qj_next = (int)atomicAdd(head, 1u);
+    g = qj * p->shards + shard;
   }
   p = params();
   const int lane = (int)__lane_id();

@@ -5,11 +5,14 @@ src/concurrency/workerpool.nim) with one process per GPU:
   * the scene (objects, BVH, triangles) is replicated on every GPU;
   * image rows are cut into bands of `band_h` rows and band b is rendered by
     rank b % world (round-robin keeps the load balanced: the bunny covers
-    a small part of the frame);
-  * each rank writes its bands into a compact buffer; ONE all-gather over
-    RCCL/xGMI (torch.distributed "nccl" backend) brings them to every rank,
-    rank 0 un-interleaves them on the GPU (rt_unshard_bands_device) and the
-    Stats are summed with one all-reduce.
+    a small part of the frame; 4-row bands put the slowest of 8 ranks within
+    ~3 % of the mean on C3);
+  * each rank writes its bands into a compact buffer; ONE gather over
+    RCCL/xGMI (torch.distributed "nccl" backend) brings them to rank 0 — only
+    rank 0 needs the frame, so the other ranks send 1/world of what an
+    all-gather moves and rank 0 receives over all its links at once —, rank 0
+    un-interleaves them on the GPU (rt_unshard_bands_device) and the Stats
+    are summed with one all-reduce.
 The pure-Python mapping helpers below are the host-side statement of the
 layout (and what the gloo CPU tests check against).
 """
@@ -45,7 +48,19 @@ def unshard_host(gathered, height, band_h):
     return fb
 
 
-def render_frame_distributed(dscene, opts, band_h=16, group=None, stream=None, gather=True):
+def gather_bands(local, gathered, n, group=None):
+    """Rank 0 receives every rank's compact band buffer (n floats each) into
+    `gathered` (world * n floats, rank order); other ranks pass None."""
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+    if dist.get_rank(group) == 0:
+        dist.gather(local, [gathered[r * n:(r + 1) * n] for r in range(world)], dst=0, group=group)
+    else:
+        dist.gather(local, None, dst=0, group=group)
+
+
+def render_frame_distributed(dscene, opts, band_h=4, group=None, stream=None, gather=True):
     """Render one frame across all ranks of the (initialised) process group.
 
     Returns (fb, stats): fb is a (height*width*3) float32 CUDA tensor on rank 0
@@ -68,8 +83,8 @@ def render_frame_distributed(dscene, opts, band_h=16, group=None, stream=None, g
                                     stream=stream or torch.cuda.current_stream(), stats=True)
     if not gather:
         return local, st
-    gathered = torch.empty(world * rows * w * 3, dtype=torch.float32, device=dev)
-    dist.all_gather_into_tensor(gathered, local, group=group)
+    gathered = torch.empty(world * rows * w * 3, dtype=torch.float32, device=dev) if rank == 0 else None
+    gather_bands(local, gathered, rows * w * 3, group=group)
     counts = torch.tensor([st.numPrimaryRays, st.numIntersectionTests, st.numIntersectionHits,
                            st.numShadowRays, st.numReflectionRays], dtype=torch.int64, device=dev)
     dist.all_reduce(counts, group=group)

@@ -1,15 +1,16 @@
-"""The N > 1 path on CPU: world_size-2 torch.distributed (gloo). Each rank
-renders its round-robin image bands (with the oracle, standing in for the
-GPU's rt_render_bands_device), one all-gather assembles them, rank 0
-un-interleaves (the host statement of rt_unshard_bands_device), and Stats are
-all-reduced — checked against a whole-frame render."""
+"""The N > 1 path on CPU: torch.distributed (gloo), world sizes 2 and 3. Each
+rank renders its round-robin image bands (with the oracle, standing in for the
+GPU's rt_render_bands_device), rtmi.dist.gather_bands (the bench's collective)
+brings them to rank 0, which un-interleaves (the host statement of
+rt_unshard_bands_device), and Stats are all-reduced — checked against a
+whole-frame render."""
 import os
 import socket
 
 import numpy as np
 import pytest
 
-BAND_H = 16
+BAND_H = 4
 
 
 def _free_port():
@@ -28,7 +29,7 @@ def _worker(rank, world, port, out_path):
 
     import oracle
     from rtmi import Antialias, Options, Precision, akGrid, scenes
-    from rtmi.dist import band_rows, rank_rows, unshard_host
+    from rtmi.dist import band_rows, gather_bands, rank_rows, unshard_host
 
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -42,8 +43,9 @@ def _worker(rank, world, port, out_path):
     _, st, _ = o.render(opts, rows=[int(y) for y in ys if y >= 0], fb=full, nthreads=2)
     local = np.zeros((rows, opts.width, 3), np.float32)
     local[ys >= 0] = full[ys[ys >= 0]]
-    gathered = torch.zeros((world * rows, opts.width, 3), dtype=torch.float32)
-    dist.all_gather_into_tensor(gathered, torch.from_numpy(local))
+    n = rows * opts.width * 3
+    gathered = torch.zeros(world * n, dtype=torch.float32) if rank == 0 else None
+    gather_bands(torch.from_numpy(local).reshape(-1), gathered, n)
     counts = torch.tensor([st.numPrimaryRays, st.numIntersectionTests, st.numIntersectionHits,
                            st.numShadowRays], dtype=torch.int64)
     dist.all_reduce(counts)
@@ -54,7 +56,7 @@ def _worker(rank, world, port, out_path):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2])
+@pytest.mark.parametrize("world", [2, 3])
 def test_band_shard_gather_matches_whole_frame(tmp_path, oracle_mod, world):
     import torch.multiprocessing as mp
 
