@@ -210,16 +210,21 @@ enum : int32_t {
   STAT_PRIMARY = 0, STAT_TESTS = 1, STAT_HITS = 2, STAT_SHADOW = 3, STAT_REFL = 4,
   STAT_NODE_FETCH = 5, STAT_TRI_FETCH = 6, STAT_LANE_NODES = 7, STAT_LANE_TRIS = 8
 };
-// float32 kernel work queue: 8 head words, 128 B apart, zeroed per launch
-constexpr int kQueueShards = 8, kQueueStride = 32;
+// float32 kernel scene-feature subset index (rt_kernels_f32_part.hip): bit 0
+// sphere, 1 box, 2 mesh, 3 general transform, 4 point light, 5 reflection
+enum : unsigned {
+  SUB_SPHERE = 1u, SUB_BOX = 2u, SUB_MESH = 4u, SUB_XF_GENERAL = 8u, SUB_POINT = 16u, SUB_REFLECT = 32u
+};
+// float32 kernel work queue: 64 head words, 128 B apart, zeroed per launch
+constexpr int kQueueShards = 64, kQueueStride = 32;
 
 }  // namespace rtmi
 
 // Launchers implemented by the precision-specific translation units.
 extern "C" {
-int rtmi_launch_render_f32(const rtmi::FastParams* p, int blocks, void* stream);
+int rtmi_launch_render_f32(const rtmi::FastParams* p, unsigned subset, int blocks, void* stream);
 int rtmi_launch_render_f64(const rtmi::RenderParams<double>* p, int blocks, void* stream);
-int rtmi_render_f32_blocks_per_cu(int count);
+int rtmi_render_f32_blocks_per_cu(int count, unsigned subset);
 int rtmi_launch_reduce_stats(const unsigned long long* partials, int num_waves,
                              unsigned long long* acc, void* stream);
 int rtmi_launch_unshard(const float* gathered, float* fb, int width, int height, int band_h,

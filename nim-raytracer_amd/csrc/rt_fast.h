@@ -29,8 +29,23 @@
 #endif
 
 
+#ifndef RTMI_TRANSITION_ARITH
+#define RTMI_TRANSITION_ARITH 0
+#endif
+
 namespace rtmi {
 namespace fast {
+
+// Scene-feature mask of a kernel instantiation: code for a feature whose bit
+// is clear is removed at compile time (the host picks the smallest
+// instantiation covering the scene, rtmi.cpp feature_mask()).
+enum : unsigned {
+  F_SPHERE = 1u, F_BOX = 2u, F_PLANE = 4u, F_MESH = 8u,
+  F_XF_GENERAL = 16u,  // rotations / scales (identity and translation always)
+  F_POINT = 32u,       // point lights
+  F_REFLECT = 64u,     // reflective materials
+  F_ALL = 127u
+};
 
 template <class T>
 __device__ __forceinline__ const RT_CONST T* cp(const T* p) {
@@ -92,12 +107,13 @@ struct Hit {
 };
 
 // World -> object space (FObj.xf classification).
+template <unsigned F>
 __device__ __forceinline__ void to_object(KP p, const FObj& ob, int i, F3 o, F3 d, F3& ro,
                                           F3& rd) {
   if (ob.xf == XF_IDENTITY) {
     ro = o;
     rd = d;
-  } else if (ob.xf == XF_TRANSLATE) {
+  } else if (!(F & F_XF_GENERAL) || ob.xf == XF_TRANSLATE) {
     ro = f3(o.x + ob.t[0], o.y + ob.t[1], o.z + ob.t[2]);
     rd = d;
   } else {
@@ -267,6 +283,39 @@ __device__ __forceinline__ void traverse(KP p, int root, F3 o, F3 d, bool active
       }
       m1 = 0ull;
     }
+#if RTMI_TRANSITION_ARITH
+    // Transition as straight-line scalar arithmetic (one branch): the
+    // if / else-if / else form lowered to flag-passing flow blocks costing
+    // 20-37 SALU per node step.
+    if ((m0 | m1) != 0ull) {
+      const unsigned long long both = m0 & m1;
+      const unsigned int has_both = both != 0ull;
+      // near child: majority vote of the lanes that hit both boxes
+      const unsigned int take1 =
+          (unsigned int)(m0 == 0ull) | (has_both & (unsigned int)(pc(bal(tn0 <= tn1) & both) * 2u < pc(both)));
+      const int next = take1 ? nd.c1 : nd.c0;
+      const int far = take1 ? nd.c0 : nd.c1;
+      const int push_lane = has_both ? sp : 64;  // 64: no lane takes the push
+      stack = (lane == push_lane) ? far : stack;
+      if constexpr (COUNT) {
+        const unsigned long long fm = take1 ? m0 : m1;
+        mlo = (lane == push_lane) ? (int)(unsigned int)fm : mlo;
+        mhi = (lane == push_lane) ? (int)(unsigned int)(fm >> 32) : mhi;
+        vm = take1 ? m1 : m0;
+      }
+      sp += (int)has_both;
+      node = next;
+    } else {
+      if (sp == 0) break;
+      if (early && bal(tc >= 0.0f) == 0ull) break;
+      --sp;
+      node = __builtin_amdgcn_readlane(stack, sp);
+      if constexpr (COUNT)
+        vm = (unsigned long long)(unsigned int)__builtin_amdgcn_readlane(mlo, sp) |
+             ((unsigned long long)(unsigned int)__builtin_amdgcn_readlane(mhi, sp) << 32);
+    }
+  }
+#else
     if (m0 && m1) {
       const unsigned long long both = m0 & m1;
       const bool first0 = pc(bal(tn0 <= tn1) & both) * 2u >= pc(both);
@@ -297,6 +346,7 @@ __device__ __forceinline__ void traverse(KP p, int root, F3 o, F3 d, bool active
              ((unsigned long long)(unsigned int)__builtin_amdgcn_readlane(mhi, sp) << 32);
     }
   }
+#endif
   if (key != key0) {
     tbest = __uint_as_float((unsigned int)(key >> 32));
     best_id = (int)(unsigned int)key;
@@ -308,12 +358,14 @@ __device__ __forceinline__ void traverse(KP p, int root, F3 o, F3 d, bool active
 
 // t of analytic object i in world space, -inf on a miss (Sphere / Plane /
 // Box .intersect, geom.nim:215-248, 76-96).
+template <unsigned F>
 __device__ __forceinline__ float analytic_t(KP p, const FObj& ob, int i, F3 o, F3 d) {
   F3 ro, rd;
-  to_object(p, ob, i, o, d, ro, rd);
-  if (ob.type == GEOM_PLANE) return plane(ro, rd);
-  if (ob.type == GEOM_SPHERE) return sphere(ob.r, ro, rd);
-  return aabb(ob.lo, ob.hi, ro, f3(rcp(rd.x), rcp(rd.y), rcp(rd.z)));
+  to_object<F>(p, ob, i, o, d, ro, rd);
+  if ((F & F_PLANE) && ob.type == GEOM_PLANE) return plane(ro, rd);
+  if ((F & F_SPHERE) && ob.type == GEOM_SPHERE) return sphere(ob.r, ro, rd);
+  if (F & F_BOX) return aabb(ob.lo, ob.hi, ro, f3(rcp(rd.x), rcp(rd.y), rcp(rd.z)));
+  return -finf();
 }
 
 // trace (renderer.nim:47-67): linear closest hit over the objects in order;
@@ -325,16 +377,16 @@ __device__ __forceinline__ float analytic_t(KP p, const FObj& ob, int i, F3 o, F
 // t <= stop = min t of the analytic objects after the mesh, every later
 // comparison is decided and the lane retires: exact, not an approximation.
 // Applied when the scene has exactly one mesh object (p->shadow_mesh).
-template <bool COUNT>
+template <bool COUNT, unsigned F>
 __device__ __forceinline__ Hit trace(KP p, F3 o, F3 d, float tmax, bool active, bool shadow,
                                      Stats32& ws) {
   Hit h{-1, -1, tmax};
-  const bool early = shadow && p->shadow_mesh >= 0;
+  const bool early = (F & F_MESH) && shadow && p->shadow_mesh >= 0;
   float stop = -1.0f;
   if (early) {
     stop = finf();
     for (int i = p->shadow_mesh + 1; i < p->nobj; ++i) {
-      const float t = analytic_t(p, cp(p->objs)[i], i, o, d);
+      const float t = analytic_t<F>(p, cp(p->objs)[i], i, o, d);
       stop = t >= 0.0f ? fminf(stop, t) : stop;
     }
   }
@@ -342,11 +394,11 @@ __device__ __forceinline__ Hit trace(KP p, F3 o, F3 d, float tmax, bool active, 
     const FObj ob = cp(p->objs)[i];
     float t;
     int tri = -1;
-    if (ob.type != GEOM_MESH) {
-      t = analytic_t(p, ob, i, o, d);
+    if (!(F & F_MESH) || ob.type != GEOM_MESH) {
+      t = analytic_t<F>(p, ob, i, o, d);
     } else {
       F3 ro, rd;
-      to_object(p, ob, i, o, d, ro, rd);
+      to_object<F>(p, ob, i, o, d, ro, rd);
       const FMesh m = cp(p->meshes)[ob.mesh];
       // TriangleMesh.intersect (geom.nim:339-358): a ray starting inside
       // the mesh AABB misses; otherwise the closest face.
@@ -370,12 +422,13 @@ __device__ __forceinline__ Hit trace(KP p, F3 o, F3 d, float tmax, bool active, 
 }
 
 // normal(*) (geom.nim:361-379) for analytic geometry, object space.
+template <unsigned F>
 __device__ __forceinline__ F3 analytic_normal(const FObj& ob, F3 ho) {
-  if (ob.type == GEOM_SPHERE) {
+  if ((F & F_SPHERE) && ob.type == GEOM_SPHERE) {
     const float r = rsq(dot3(ho, ho));
     return f3(ho.x * r, ho.y * r, ho.z * r);
   }
-  if (ob.type == GEOM_BOX) {
+  if ((F & F_BOX) && ob.type == GEOM_BOX) {
     const float cx = (ob.lo[0] + ob.hi[0]) * 0.5f, cy = (ob.lo[1] + ob.hi[1]) * 0.5f,
                 cz = (ob.lo[2] + ob.hi[2]) * 0.5f;
     const float qx = (ho.x - cx) * rcp(fabsf((ob.lo[0] - ob.hi[0]) * 0.5f));
@@ -440,15 +493,15 @@ __device__ __forceinline__ F3 lds_get3(LdsF* ls, int slot) {
 //  * renderer.nim:104-124: reflection > 0 and depth <= maxRayDepth traces
 //    r = i - 2 (n.i) n from hitW + r*bias; the level's local light is
 //    weighted (1 - reflection), the reflected colour reflection.
-template <bool COUNT>
+template <bool COUNT, unsigned F>
 __device__ __forceinline__ void shade_path(KP p, F3 o, F3 d, bool active, LdsF* ls, Acc& acc, Stats32& ws) {
   bool act = active;
   int depth = 1;
   float w = 1.0f;
-  for (int lev = 0; lev < kMaxShadeLevels; ++lev) {
+  for (int lev = 0; lev < ((F & F_REFLECT) ? kMaxShadeLevels : 1); ++lev) {
     p = params();
     if (bal(act) == 0ull) break;
-    const Hit hit = trace<COUNT>(p, o, d, finf(), act, false, ws);
+    const Hit hit = trace<COUNT, F>(p, o, d, finf(), act, false, ws);
     if (act && hit.obj < 0) acc_add3(acc, w * p->bg[0], w * p->bg[1], w * p->bg[2]);
     const bool lit = act && hit.obj >= 0;
     const F3 hw = f3(__builtin_fmaf(d.x, hit.t, o.x), __builtin_fmaf(d.y, hit.t, o.y), __builtin_fmaf(d.z, hit.t, o.z));
@@ -465,15 +518,15 @@ __device__ __forceinline__ void shade_path(KP p, F3 o, F3 d, bool active, LdsF* 
       const RT_CONST FObjX& ox = cp(p->objx)[oi];
       if (mine) {
         F3 n;
-        if (ob.type == GEOM_MESH) {
+        if ((F & F_MESH) && ob.type == GEOM_MESH) {
           const float* fn = p->normals + 3 * (size_t)(ox.normal_base + hit.tri);
           n = f3(fn[0], fn[1], fn[2]);
         } else {
           F3 ho, unused;
-          to_object(p, ob, oi, hw, f3(0.0f, 0.0f, 0.0f), ho, unused);
-          n = analytic_normal(ob, ho);
+          to_object<F>(p, ob, oi, hw, f3(0.0f, 0.0f, 0.0f), ho, unused);
+          n = analytic_normal<F>(ob, ho);
         }
-        if (ob.xf == XF_GENERAL) {  // object_to_world * n, not re-normalised
+        if ((F & F_XF_GENERAL) && ob.xf == XF_GENERAL) {  // object_to_world * n, not re-normalised
           const float* m = ox.o2w;
           N = f3(__builtin_fmaf(m[0], n.x, __builtin_fmaf(m[3], n.y, m[6] * n.z)),
                  __builtin_fmaf(m[1], n.x, __builtin_fmaf(m[4], n.y, m[7] * n.z)),
@@ -485,11 +538,11 @@ __device__ __forceinline__ void shade_path(KP p, F3 o, F3 d, bool active, LdsF* 
         refl = ox.refl;
       }
     }
-    const bool reflect = lit && refl > 0.0f && depth <= p->max_depth;
+    const bool reflect = (F & F_REFLECT) && lit && refl > 0.0f && depth <= p->max_depth;
     const float wl = reflect ? w * (1.0f - refl) : w;
     const F3 albw = f3(alb.x * wl, alb.y * wl, alb.z * wl);
-    ws.v[STAT_REFL] += pc(bal(reflect));
-    if (bal(reflect)) {  // park the reflected ray (renderer.nim:109-118)
+    if (F & F_REFLECT) ws.v[STAT_REFL] += pc(bal(reflect));
+    if ((F & F_REFLECT) && bal(reflect)) {  // park the reflected ray (renderer.nim:109-118)
       if (reflect) {
         const float ndi = 2.0f * dot3(N, d);
         const F3 rd = f3(d.x - N.x * ndi, d.y - N.y * ndi, d.z - N.z * ndi);
@@ -500,13 +553,13 @@ __device__ __forceinline__ void shade_path(KP p, F3 o, F3 d, bool active, LdsF* 
     }
     const F3 so = f3(__builtin_fmaf(N.x, p->bias, hw.x), __builtin_fmaf(N.y, p->bias, hw.y),
                      __builtin_fmaf(N.z, p->bias, hw.z));
-    if (p->has_point_light) lds_put3(ls, LDS_HW, hw);
+    if ((F & F_POINT) && p->has_point_light) lds_put3(ls, LDS_HW, hw);
     for (int li = 0; li < p->nlight; ++li) {
       p = params();
       const FLight L = cp(p->lights)[li];
       F3 sd;
       float dist, k = 1.0f;
-      if (L.type == LIGHT_POINT) {  // light.nim:52-62
+      if ((F & F_POINT) && L.type == LIGHT_POINT) {  // light.nim:52-62
         const F3 h = lds_get3(ls, LDS_HW);
         const F3 lv = f3(h.x - L.v[0], h.y - L.v[1], h.z - L.v[2]);
         const float r2 = dot3(lv, lv);
@@ -519,7 +572,7 @@ __device__ __forceinline__ void shade_path(KP p, F3 o, F3 d, bool active, LdsF* 
         dist = finf();
       }
       ws.v[STAT_SHADOW] += pc(bal(lit));
-      const Hit sh = trace<COUNT>(p, so, sd, dist, lit, true, ws);
+      const Hit sh = trace<COUNT, F>(p, so, sd, dist, lit, true, ws);
       if (lit && sh.obj < 0) {  // shadeDiffuse (shader.nim:12-17)
         const float ndl = fmaxf(dot3(N, sd), 0.0f) * k;
         acc_add3(acc, albw.x * L.ci[0] * ndl, albw.y * L.ci[1] * ndl, albw.z * L.ci[2] * ndl);
@@ -527,7 +580,7 @@ __device__ __forceinline__ void shade_path(KP p, F3 o, F3 d, bool active, LdsF* 
     }
     // every lane reloads (lanes that do not reflect go inactive): o and d
     // are then dead across the light loop instead of carried for them
-    if (bal(reflect)) {
+    if ((F & F_REFLECT) && bal(reflect)) {
       o = lds_get3(ls, LDS_RO);
       d = lds_get3(ls, LDS_RD);
     }
@@ -596,7 +649,7 @@ __device__ __forceinline__ GroupPix group_pixel(KP p, int g, int lane) {
   return r;
 }
 
-template <bool COUNT>
+template <bool COUNT, unsigned F>
 __global__ __launch_bounds__(256) RTMI_OCC void k_render_fast(const FastParams params_by_value) {
   (void)params_by_value;  // read through params() (kernarg segment)
   KP p = params();
@@ -655,7 +708,7 @@ __global__ __launch_bounds__(256) RTMI_OCC void k_render_fast(const FastParams p
       const F3 o = f3(p->cam[0], p->cam[1], p->cam[2]);
       ws.v[STAT_PRIMARY] += pc(bal(sv));
       RT_STAMP(t_s0);
-      shade_path<COUNT>(p, o, d, sv, ls, pacc, ws);
+      shade_path<COUNT, F>(p, o, d, sv, ls, pacc, ws);
 #ifdef RTMI_STAMPS
       { RT_STAMP(t_s1); RT_ACC(7, t_s0, t_s1); }
 #endif

@@ -51,26 +51,48 @@ __global__ __launch_bounds__(256) void k_unshard_scalar(const float* __restrict_
   for (int i = threadIdx.x; i < row_f; i += blockDim.x) fb[(size_t)y * row_f + i] = gathered[src_row * row_f + i];
 }
 
-template __global__ void fast::k_render_fast<false>(const FastParams);
-template __global__ void fast::k_render_fast<true>(const FastParams);
+// the instrumented (RT_FLAG_COUNT_TRAVERSAL) kernel: all features
+template __global__ void fast::k_render_fast<true, fast::F_ALL>(const FastParams);
 
 }  // namespace rtmi
 
-extern "C" int rtmi_launch_render_f32(const rtmi::FastParams* p, int blocks, void* stream) {
-  if (p->flags & rtmi::RT_DEV_FLAG_COUNT)
-    hipLaunchKernelGGL((rtmi::fast::k_render_fast<true>), dim3(blocks), dim3(256), 0, (hipStream_t)stream, *p);
-  else
-    hipLaunchKernelGGL((rtmi::fast::k_render_fast<false>), dim3(blocks), dim3(256), 0, (hipStream_t)stream, *p);
-  return (int)hipGetLastError();
+// feature-subset specialisations: rt_kernels_f32_part.hip, 8 objects
+#define RTMI_PART_DECL(k)                                                                             \
+  extern "C" int rtmi_launch_render_f32_part##k(unsigned, const rtmi::FastParams*, int, void*);      \
+  extern "C" int rtmi_render_f32_part_blocks_per_cu##k(unsigned);
+RTMI_PART_DECL(0) RTMI_PART_DECL(1) RTMI_PART_DECL(2) RTMI_PART_DECL(3)
+RTMI_PART_DECL(4) RTMI_PART_DECL(5) RTMI_PART_DECL(6) RTMI_PART_DECL(7)
+
+namespace {
+int (*const kLaunch[8])(unsigned, const rtmi::FastParams*, int, void*) = {
+    rtmi_launch_render_f32_part0, rtmi_launch_render_f32_part1, rtmi_launch_render_f32_part2,
+    rtmi_launch_render_f32_part3, rtmi_launch_render_f32_part4, rtmi_launch_render_f32_part5,
+    rtmi_launch_render_f32_part6, rtmi_launch_render_f32_part7};
+int (*const kOccupancy[8])(unsigned) = {
+    rtmi_render_f32_part_blocks_per_cu0, rtmi_render_f32_part_blocks_per_cu1, rtmi_render_f32_part_blocks_per_cu2,
+    rtmi_render_f32_part_blocks_per_cu3, rtmi_render_f32_part_blocks_per_cu4, rtmi_render_f32_part_blocks_per_cu5,
+    rtmi_render_f32_part_blocks_per_cu6, rtmi_render_f32_part_blocks_per_cu7};
+}  // namespace
+
+extern "C" int rtmi_launch_render_f32(const rtmi::FastParams* p, unsigned subset, int blocks, void* stream) {
+  if (p->flags & rtmi::RT_DEV_FLAG_COUNT) {
+    hipLaunchKernelGGL((rtmi::fast::k_render_fast<true, rtmi::fast::F_ALL>), dim3(blocks), dim3(256), 0,
+                       (hipStream_t)stream, *p);
+    return (int)hipGetLastError();
+  }
+  return kLaunch[(subset >> 3) & 7u](subset & 63u, p, blocks, stream);
 }
 
 // Resident 256-thread blocks per CU of the render kernel (grid sizing for the
 // work-queue loop: launch exactly what fits, waves pull pixel groups).
-extern "C" int rtmi_render_f32_blocks_per_cu(int count) {
-  int nb = 0;
-  hipError_t e = count ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, rtmi::fast::k_render_fast<true>, 256, 0)
-                       : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, rtmi::fast::k_render_fast<false>, 256, 0);
-  return e == hipSuccess && nb > 0 ? nb : 1;
+extern "C" int rtmi_render_f32_blocks_per_cu(int count, unsigned subset) {
+  if (count) {
+    int nb = 0;
+    const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &nb, rtmi::fast::k_render_fast<true, rtmi::fast::F_ALL>, 256, 0);
+    return e == hipSuccess && nb > 0 ? nb : 1;
+  }
+  return kOccupancy[(subset >> 3) & 7u](subset & 63u);
 }
 
 extern "C" int rtmi_launch_reduce_stats(const unsigned long long* partials, int num_waves,

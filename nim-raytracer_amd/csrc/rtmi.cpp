@@ -133,6 +133,7 @@ struct rt_scene {
   int32_t nobj = 0, nlight = 0, nmesh = 0;
   int32_t shadow_mesh = -1;  // the only mesh object, or -1 (FastParams.shadow_mesh)
   int32_t has_point_light = 0;
+  unsigned f32_subset = 0;   // SUB_* feature bits of the scene (kernel specialisation)
   bool any_reflective = false;
   double fov = 50.0;
   double c2w[16];
@@ -563,6 +564,17 @@ extern "C" int rt_scene_create(const rt_scene_desc* d, rt_scene** out_scene) {
     if (d->lights[i].type == RT_POINT_LIGHT) s->has_point_light = 1;
   s->nmesh = d->num_meshes;
   s->any_reflective = any_reflective;
+  // scene features -> the float32 kernel specialisation (rt_kernels_f32_part.hip)
+  s->f32_subset = 0;
+  for (int i = 0; i < d->num_objects; ++i) {
+    const rt_object_desc& ob = d->objects[i];
+    if (ob.type == RT_SPHERE) s->f32_subset |= SUB_SPHERE;
+    if (ob.type == RT_BOX) s->f32_subset |= SUB_BOX;
+    if (ob.type == RT_MESH) s->f32_subset |= SUB_MESH;
+    if (classify_xf(ob.world_to_object, ob.object_to_world) == XF_GENERAL) s->f32_subset |= SUB_XF_GENERAL;
+  }
+  if (s->has_point_light) s->f32_subset |= SUB_POINT;
+  if (any_reflective) s->f32_subset |= SUB_REFLECT;
   s->fov = d->fov;
   std::memcpy(s->c2w, d->camera_to_world, sizeof s->c2w);
   std::memcpy(s->bg, d->bg_color, sizeof s->bg);
@@ -702,7 +714,7 @@ Plan plan_mapping(const rt_scene* s, const rt_options* o, const Mapping& mp, int
   const long long want = (ng + 3) / 4;
   long long cap = s->max_waves / 4;
   if (o->precision == RT_FP32) {  // work-queue kernel: launch what is resident
-    const int per_cu = rtmi_render_f32_blocks_per_cu((o->flags & RT_FLAG_COUNT_TRAVERSAL) ? 1 : 0);
+    const int per_cu = rtmi_render_f32_blocks_per_cu((o->flags & RT_FLAG_COUNT_TRAVERSAL) ? 1 : 0, s->f32_subset);
     cap = std::min<long long>(cap, (long long)per_cu * s->num_cus);
   }
   pl.blocks = (int)std::max(1LL, std::min<long long>(want, cap));
@@ -863,7 +875,7 @@ int launch(rt_scene* s, const rt_options* o, const Mapping& mp, float* d_out, hi
     FastParams p;
     fill_fast(s, o, mp, d_out, p, &blocks);
     if (p.ngroups == 0) return RT_OK;
-    const int e = rtmi_launch_render_f32(&p, blocks, st);
+    const int e = rtmi_launch_render_f32(&p, s->f32_subset, blocks, st);
     if (e) return fail(RT_E_DEVICE, "render kernel launch failed: %s", hipGetErrorString((hipError_t)e));
   }
   const int e = rtmi_launch_reduce_stats(s->partials.p, blocks * 4, s->acc.p, st);
