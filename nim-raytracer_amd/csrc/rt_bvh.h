@@ -15,7 +15,8 @@
 namespace rtmi {
 
 struct BvhBuildParams {
-  int max_leaf = kLeafMax;  // triangles per leaf, SAH may stop earlier
+  int max_leaf = kLeafMax;  // triangles per leaf, SAH may stop earlier (4 measured best:
+                            // C3 8.45 ms vs 8.54 at 6 and 8.73 at 8)
   int bins = 32;            // SAH bins per axis
   float cost_node = 1.0f;   // relative cost of one node fetch (two boxes)
   float cost_tri = 1.0f;    // relative cost of one triangle test
