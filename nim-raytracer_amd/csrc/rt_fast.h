@@ -592,12 +592,19 @@ __device__ __forceinline__ void shade_path(KP p, F3 o, F3 d, bool active, LdsF* 
 
 // Occupancy target: the kernel is latency-bound (serial node-fetch chains),
 // so resident waves matter more than a few spills in the outer loops.
-// 7 waves/SIMD (<= 72 VGPRs) measured best on C3/C2 (DESIGN.md
-// "Occupancy"); 8 spills inside the traversal and loses.
-#ifndef RTMI_WAVES_PER_EU
-#define RTMI_WAVES_PER_EU 7
+// 8 waves/SIMD (<= 64 VGPRs) for every feature subset except meshes combined
+// with point lights or reflection, which spill inside the traversal at 8 and
+// run at 7 (<= 72 VGPRs). C3 (mesh + plane): 8 waves 8.06 ms vs 7 waves
+// 8.38 ms (DESIGN.md "Occupancy").
+template <unsigned F>
+constexpr unsigned waves_per_eu() {
+#ifdef RTMI_WAVES_PER_EU
+  return RTMI_WAVES_PER_EU;
+#else
+  return ((F & 8u) && (F & (32u | 64u))) ? 7u : 8u;  // F_MESH && (F_POINT || F_REFLECT)
 #endif
-#define RTMI_OCC __attribute__((amdgpu_waves_per_eu(RTMI_WAVES_PER_EU)))
+}
+#define RTMI_OCC __attribute__((amdgpu_waves_per_eu(waves_per_eu<F>())))
 // The lane id from an opaque instruction: values derived from it are
 // recomputed inside the loops instead of hoisted to kernel scope, where
 // they would stay live (and spill) across the whole sample loop.
