@@ -242,6 +242,25 @@ int rt_unshard_bands_device(const float *d_gathered, float *d_fb,
 int rt_band_rows(int32_t height, int32_t band_h, int32_t world,
                  int32_t *out_rows);
 
+/* ---- output (framebuf.nim:55-93 writePpm) ------------------------------ */
+
+/* The P6 payload of writePpm for a device framebuffer (width*height*3
+ * float32, the Framebuf.data layout): per component clamp to [0, 1], optional
+ * linearToSRGB (color.nim:17-22), round(c * (2^bits - 1)); bits in 1..16;
+ * bits <= 8: one byte per component, else two bytes big-endian. d_out
+ * receives rt_ppm_payload_bytes() bytes (device memory). Replaces
+ * framebuf.nim:82-88's per-component loop; the caller writes
+ * rt_ppm_header() and then the payload. */
+int rt_ppm_encode_device(const float *d_fb, int32_t width, int32_t height,
+                         int32_t bits, int32_t srgb, void *d_out,
+                         void *hip_stream);
+/* Payload size in bytes (width*height*3*(bits <= 8 ? 1 : 2)), or < 0. */
+int64_t rt_ppm_payload_bytes(int32_t width, int32_t height, int32_t bits);
+/* writeHeader (framebuf.nim:60-61): "P6 <w> <h> <maxval> " into buf; returns
+ * its length (excluding the NUL), or < 0 if buf_len is too small. */
+int rt_ppm_header(int32_t width, int32_t height, int32_t bits, char *buf,
+                  int32_t buf_len);
+
 /* Traversal counters of the last render call on this scene (waits for it).
  * Zero unless that call set RT_FLAG_COUNT_TRAVERSAL. */
 int rt_scene_last_counters(rt_scene *scene, rt_traversal_counters *out);

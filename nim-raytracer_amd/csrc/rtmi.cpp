@@ -1023,6 +1023,28 @@ extern "C" int rt_unshard_bands_device(const float* d_gathered, float* d_fb, int
   return RT_OK;
 }
 
+extern "C" int64_t rt_ppm_payload_bytes(int32_t width, int32_t height, int32_t bits) {
+  if (width <= 0 || height <= 0 || bits < 1 || bits > 16) return fail(RT_E_INVALID, "bad ppm size / bits");
+  return (int64_t)width * height * 3 * (bits <= 8 ? 1 : 2);
+}
+
+extern "C" int rt_ppm_header(int32_t width, int32_t height, int32_t bits, char* buf, int32_t buf_len) {
+  if (width <= 0 || height <= 0 || bits < 1 || bits > 16 || !buf) return fail(RT_E_INVALID, "bad arguments");
+  const int n = std::snprintf(buf, (size_t)std::max(0, buf_len), "P6 %d %d %d ", width, height, (1 << bits) - 1);
+  if (n < 0 || n >= buf_len) return fail(RT_E_INVALID, "header buffer too small (%d bytes)", buf_len);
+  return n;
+}
+
+extern "C" int rt_ppm_encode_device(const float* d_fb, int32_t width, int32_t height, int32_t bits, int32_t srgb,
+                                    void* d_out, void* stream) {
+  if (!d_fb || !d_out) return fail(RT_E_INVALID, "null buffer");
+  if (rt_ppm_payload_bytes(width, height, bits) < 0) return RT_E_INVALID;
+  if (((uintptr_t)d_fb & 15) || ((uintptr_t)d_out & 7)) return fail(RT_E_INVALID, "buffers must be 16-B (fb) / 8-B (out) aligned");
+  const int e = rtmi_launch_ppm_encode(d_fb, (long long)width * height * 3, bits, srgb ? 1 : 0, d_out, stream);
+  if (e) return fail(RT_E_DEVICE, "ppm encode launch failed: %s", hipGetErrorString((hipError_t)e));
+  return RT_OK;
+}
+
 extern "C" int rt_scene_last_counters(rt_scene* s, rt_traversal_counters* out) {
   if (!s || !out) return fail(RT_E_INVALID, "null argument");
   std::lock_guard<std::mutex> lk(s->mu);

@@ -154,6 +154,9 @@ SIGNATURES = {
     "rt_scene_last_counters": (C.c_int, [_P, C.POINTER(rt_traversal_counters)]),
     "rt_mat4_inverse": (C.c_int, [C.POINTER(C.c_double), C.POINTER(C.c_double)]),
     "rt_load_geom": (C.c_int, [C.c_char_p, C.POINTER(C.c_int64), C.POINTER(C.c_double)]),
+    "rt_ppm_encode_device": (C.c_int, [_P, C.c_int32, C.c_int32, C.c_int32, C.c_int32, _P, _P]),
+    "rt_ppm_payload_bytes": (C.c_int64, [C.c_int32, C.c_int32, C.c_int32]),
+    "rt_ppm_header": (C.c_int, [C.c_int32, C.c_int32, C.c_int32, C.c_char_p, C.c_int32]),
 }
 
 

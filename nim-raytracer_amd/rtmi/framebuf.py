@@ -42,14 +42,17 @@ def linearToSRGB(v):
 
 
 def to_uint(data, bits=8, sRGB=True):
-    """writePpm's outvalue (framebuf.nim:74-78): clamp, sRGB, round(c*maxval)."""
-    maxval = float(2 ** bits - 1)
-    c = np.clip(np.asarray(data, dtype=np.float32), 0.0, 1.0).astype(np.float64)
+    """writePpm's outvalue (framebuf.nim:74-78): clamp (float32), sRGB
+    (float64 inside, float32 result), round(c * maxval) as a float32 product
+    rounded half away from zero (Nim round on float32). NaN -> 0."""
+    maxval = np.float32(2 ** bits - 1)
+    c = np.clip(np.nan_to_num(np.asarray(data, dtype=np.float32), nan=0.0), 0.0, 1.0).astype(np.float32)
     if sRGB:
-        c = linearToSRGB(c)
-    c = c.astype(np.float32).astype(np.float64) * maxval
-    # Nim round() = round half away from zero
-    return np.floor(c + 0.5).astype(np.uint16 if bits > 8 else np.uint8)
+        c = linearToSRGB(c.astype(np.float64)).astype(np.float32)
+    x = c * maxval                      # float32 product
+    r = np.floor(x)
+    r = r + (x - r >= np.float32(0.5))  # half away from zero, exact in float32 (x >= 0)
+    return r.astype(np.uint16 if bits > 8 else np.uint8)
 
 
 def writePpm(data, filename, bits=8, sRGB=True):

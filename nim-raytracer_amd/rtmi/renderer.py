@@ -124,6 +124,37 @@ def render_frame(scene: DeviceScene, opts: Options, fb=None):
     return fb, st
 
 
+def ppm_encode_device(d_fb, width, height, bits=8, sRGB=True, stream=None):
+    """writePpm's payload (framebuf.nim:55-93) of a device framebuffer,
+    quantised on the GPU; returns (header bytes, uint8 CUDA tensor)."""
+    import torch
+    n = lib().rt_ppm_payload_bytes(int(width), int(height), int(bits))
+    if n < 0:
+        raise RtmiError(n, lib().rt_last_error().decode())
+    out = torch.empty(n, dtype=torch.uint8, device=d_fb.device)
+    check(lib().rt_ppm_encode_device(C.c_void_p(_ptr(d_fb, width * height * 3)), int(width), int(height),
+                                     int(bits), 1 if sRGB else 0, C.c_void_p(int(out.data_ptr())),
+                                     _stream(stream)))
+    buf = C.create_string_buffer(64)
+    hl = lib().rt_ppm_header(int(width), int(height), int(bits), buf, 64)
+    if hl < 0:
+        raise RtmiError(hl, lib().rt_last_error().decode())
+    return buf.raw[:hl], out
+
+
+def write_ppm_device(d_fb, width, height, filename, bits=8, sRGB=True, stream=None):
+    """Framebuf.writePpm for a device framebuffer: the quantisation runs on
+    the GPU and only the 8/16-bit payload crosses PCIe."""
+    header, payload = ppm_encode_device(d_fb, width, height, bits, sRGB, stream)
+    try:
+        with open(filename, "wb") as f:
+            f.write(header)
+            f.write(payload.cpu().numpy().tobytes())
+        return True
+    except OSError:
+        return False
+
+
 def _ptr(buf, min_floats):
     if isinstance(buf, int):
         return buf
@@ -152,5 +183,5 @@ def _stream(stream):
     return C.c_void_p(int(stream.cuda_stream) or None)
 
 
-__all__ = ["DeviceScene", "RtmiError", "band_rows", "device_count", "initRenderer", "renderLine",
-           "render_frame", "unshard_bands_device"]
+__all__ = ["DeviceScene", "RtmiError", "band_rows", "device_count", "initRenderer", "ppm_encode_device",
+           "renderLine", "render_frame", "unshard_bands_device", "write_ppm_device"]

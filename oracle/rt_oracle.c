@@ -858,11 +858,16 @@ int32_t oracle_trace(const oracle_scene *s, const double orig[4], const double d
 
 /* linearToSRGB (color.nim:17-22) + writePpm.outvalue (framebuf.nim:74-78). */
 int32_t oracle_ppm_outvalue(float v, int32_t bits, int32_t srgb) {
-  const double maxval = (double)((1 << bits) - 1);
-  double c = v < 0.0f ? 0.0 : (v > 1.0f ? 1.0 : (double)v);
+  /* maxval = float32(2^bits - 1) (framebuf.nim:58); c = clamp(v, 0, 1) is
+   * float32; linearToSRGB (color.nim:17-22) evaluates in float64 (its `a` is
+   * a float64 let) and returns float32; `round(c * maxval)` is a float32
+   * product rounded half away from zero (Nim round on float32). */
+  const float maxval = (float)((1 << bits) - 1);
+  float c = v < 0.0f ? 0.0f : (v > 1.0f ? 1.0f : v);
+  if (c != c) c = 0.0f; /* NaN: the reference's Natural() conversion raises; 0 here */
   if (srgb) {
-    const double a = 0.055;
-    c = c <= 0.0031308 ? 12.92 * c : (1 + a) * pow(c, 1 / 2.4) - a;
+    const double a = 0.055, cd = (double)c;
+    c = (float)(cd <= 0.0031308 ? 12.92 * cd : (1 + a) * pow(cd, 1 / 2.4) - a);
   }
-  return (int32_t)round((double)(float)c * maxval);
+  return (int32_t)roundf(c * maxval);
 }

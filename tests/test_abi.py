@@ -137,3 +137,38 @@ def test_scene_create_validates_before_touching_a_device():
     flat._objs[1].object_to_world[3] = 0.5  # projective row: unsupported
     assert L.rt_scene_create(C.byref(flat.desc), C.byref(h)) == abi.RT_E_UNSUPPORTED
     assert not h.value
+
+
+def test_ppm_header_and_sizes():
+    """rt_ppm_header / rt_ppm_payload_bytes (host-side, no GPU): writeHeader of
+    framebuf.nim:60-61 and the payload size of the 8- / 16-bit formats."""
+    import ctypes as C
+
+    from rtmi._lib import lib
+    L = lib()
+    buf = C.create_string_buffer(64)
+    n = L.rt_ppm_header(1920, 1080, 8, buf, 64)
+    assert buf.raw[:n] == b"P6 1920 1080 255 "
+    n = L.rt_ppm_header(4, 2, 16, buf, 64)
+    assert buf.raw[:n] == b"P6 4 2 65535 "
+    assert L.rt_ppm_header(4, 2, 8, buf, 5) < 0          # too small
+    assert L.rt_ppm_payload_bytes(1920, 1080, 8) == 1920 * 1080 * 3
+    assert L.rt_ppm_payload_bytes(3, 5, 16) == 3 * 5 * 6
+    assert L.rt_ppm_payload_bytes(3, 5, 0) < 0 and L.rt_ppm_payload_bytes(3, 5, 17) < 0
+
+
+def test_ppm_quantisation_matches_oracle(oracle_mod):
+    """rtmi.framebuf.to_uint (the host writer and the GPU pass's reference)
+    equals the oracle's outvalue on edge and random values."""
+    import numpy as np
+
+    from rtmi.framebuf import to_uint
+    rng = np.random.default_rng(7)
+    v = np.concatenate([rng.random(20000).astype(np.float32) * 1.4 - 0.2,
+                        np.array([0.0031308, np.nextafter(np.float32(0.0031308), 1), 0.5 / 255, 1.5 / 255,
+                                  254.5 / 255, 0.5, 1.0, -0.0, 2.0, -1.0, np.nan], np.float32)])
+    for bits in (8, 16, 3):
+        for srgb in (True, False):
+            q = to_uint(v, bits, srgb).astype(np.int64)
+            o = np.array([oracle_mod.ppm_outvalue(float(x), bits, srgb) for x in v])
+            assert np.array_equal(q, o), (bits, srgb)
