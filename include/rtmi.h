@@ -56,6 +56,12 @@ enum rt_geom_type { RT_SPHERE = 0, RT_PLANE = 1, RT_BOX = 2, RT_MESH = 3 };
 enum rt_light_type { RT_DISTANT_LIGHT = 0, RT_POINT_LIGHT = 1 };
 
 /* AntialiasKind (src/renderer/renderer.nim:11-12). */
+/* Antialias kinds (renderer.nim:14-21 AntialiasKind). The stochastic kinds
+ * (sampling.nim:21-113) draw from a counter-based RNG keyed by
+ * (rt_options.seed, absolute pixel, draw index) instead of the reference's
+ * clock-seeded Nim `random` — reproducible, and independent of how rows are
+ * split across calls, bands or GPUs. float32: (correlated) multi-jittered up
+ * to grid_size 32; float64: up to 256. */
 enum rt_aa_kind {
   RT_AA_NONE = 0,
   RT_AA_GRID = 1,
@@ -128,7 +134,7 @@ typedef struct rt_options {
   double bias;                 /* Options.bias                           */
   int32_t max_ray_depth;       /* Options.maxRayDepth                    */
   int32_t precision;           /* rt_precision                           */
-  uint64_t seed;               /* stochastic samplers (not yet supported) */
+  uint64_t seed;               /* stochastic samplers: counter-RNG seed  */
   uint32_t flags;              /* RT_FLAG_*                              */
   uint32_t reserved;
 } rt_options;

@@ -133,6 +133,8 @@ struct RenderParams {
   int32_t flags;
   int32_t max_iters;               // traversal bound: each node entered at most once
   int32_t shadow_mesh;             // the scene's only mesh object, or -1 (trace early exit)
+  uint64_t seed;                   // stochastic samplers (rt_sampling.h)
+  R* sample_scratch;               // per-lane sample tables [lanes][2][spp] (aa_kind >= 2)
   // work mapping: rows k in [0, nrows), columns j in [0, ncols), x = j*step.
   int32_t mode;                    // 0: y = y0 + k*step into full image; 1: bands
   int32_t y0, nrows, ncols, step, max_step;
@@ -201,6 +203,7 @@ struct FastParams {
   float sample_step, sample_off;
   int32_t nobj, nlight, width, height;
   int32_t aa_kind, grid_m, spp, max_depth, flags, shadow_mesh, shards, has_point_light, log2_tile_x;
+  uint64_t seed;                   // stochastic samplers (rt_sampling.h)
   float inv_band_h;
   int32_t mode, y0, nrows, ncols, step, max_step, band_h, rank, world;
   int32_t lanes_per_px, log2_lanes, tile_x, tile_y, tiles_x, ngroups;
@@ -211,9 +214,11 @@ enum : int32_t {
   STAT_NODE_FETCH = 5, STAT_TRI_FETCH = 6, STAT_LANE_NODES = 7, STAT_LANE_TRIS = 8
 };
 // float32 kernel scene-feature subset index (rt_kernels_f32_part.hip): bit 0
-// sphere, 1 box, 2 mesh, 3 general transform, 4 point light, 5 reflection
+// sphere, 1 box, 2 mesh, 3 general transform, 4 point light, 5 reflection,
+// 6 stochastic sampling (a per-launch option, not a scene property)
 enum : unsigned {
-  SUB_SPHERE = 1u, SUB_BOX = 2u, SUB_MESH = 4u, SUB_XF_GENERAL = 8u, SUB_POINT = 16u, SUB_REFLECT = 32u
+  SUB_SPHERE = 1u, SUB_BOX = 2u, SUB_MESH = 4u, SUB_XF_GENERAL = 8u, SUB_POINT = 16u, SUB_REFLECT = 32u,
+  SUB_STOCHASTIC = 64u
 };
 // float32 kernel work queue: 64 head words, 128 B apart, zeroed per launch
 constexpr int kQueueShards = 64, kQueueStride = 32;
@@ -222,9 +227,9 @@ constexpr int kQueueShards = 64, kQueueStride = 32;
 
 // Launchers implemented by the precision-specific translation units.
 extern "C" {
-int rtmi_launch_render_f32(const rtmi::FastParams* p, unsigned subset, int blocks, void* stream);
+int rtmi_launch_render_f32(const rtmi::FastParams* p, unsigned subset, int blocks, size_t shmem, void* stream);
 int rtmi_launch_render_f64(const rtmi::RenderParams<double>* p, int blocks, void* stream);
-int rtmi_render_f32_blocks_per_cu(int count, unsigned subset);
+int rtmi_render_f32_blocks_per_cu(int count, unsigned subset, size_t shmem);
 int rtmi_launch_ppm_encode(const float* fb, long long n, int bits, int srgb, void* out, void* stream);
 int rtmi_launch_reduce_stats(const unsigned long long* partials, int num_waves,
                              unsigned long long* acc, void* stream);

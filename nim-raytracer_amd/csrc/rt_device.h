@@ -22,6 +22,7 @@
 #include <hip/hip_runtime.h>
 
 #include "rt_common.h"
+#include "rt_sampling.h"
 
 #ifndef RT_CONST
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -674,11 +675,23 @@ __global__ __launch_bounds__(256, RTMI_MIN_WAVES) void k_render(const RenderPara
       if ((x & mask) == 0 && (y & mask) == 0) valid = false;
     }
     V3<R> acc{R(0), R(0), R(0)};
+    // stochastic kinds (sampling.nim:21-113): this lane's pixel table, built
+    // sequentially like calcPixel's `samples` in its slice of the scratch
+    R* tsx = nullptr;
+    R* tsy = nullptr;
+    if (p.aa_kind >= 2 && valid) {
+      tsx = p.sample_scratch + (size_t)(wave * 64 + lane) * 2 * (size_t)p.spp;
+      tsy = tsx + p.spp;
+      sample_table_seq<R>(p.aa_kind, p.grid_m, rng_pixel_key(p.seed, x, y), tsx, tsy);
+    }
     for (int it = 0; it < iters; ++it) {
       const int s = it * L + sub;
       const bool sv = valid && s < p.spp;
       R px = R(x), py = R(y);
-      if (grid_aa) {  // grid() sampling.nim:5-18, p[j*m + i]
+      if (tsx) {
+        px = R(x) + tsx[s];
+        py = R(y) + tsy[s];
+      } else if (grid_aa) {  // grid() sampling.nim:5-18, p[j*m + i]
         const int si = s % p.grid_m, sj = s / p.grid_m;
         px = R(x) + (R(si) * p.sample_step + p.sample_off);
         py = R(y) + (R(sj) * p.sample_step + p.sample_off);

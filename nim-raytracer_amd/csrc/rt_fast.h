@@ -19,6 +19,7 @@
 #include <hip/hip_runtime.h>
 
 #include "rt_common.h"
+#include "rt_sampling.h"
 
 #ifndef RT_CONST
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -44,7 +45,8 @@ enum : unsigned {
   F_XF_GENERAL = 16u,  // rotations / scales (identity and translation always)
   F_POINT = 32u,       // point lights
   F_REFLECT = 64u,     // reflective materials
-  F_ALL = 127u
+  F_STOCHASTIC = 128u, // jittered / (correlated) multi-jittered sampling
+  F_ALL = 255u
 };
 
 template <class T>
@@ -661,6 +663,7 @@ __global__ __launch_bounds__(256) RTMI_OCC void k_render_fast(const FastParams p
   (void)params_by_value;  // read through params() (kernarg segment)
   KP p = params();
   __shared__ float lds[4][kLdsSlots][64];            // 4 waves per 256-thread block
+  extern __shared__ float sample_lds[];              // (multi-)jittered tables, sized by the host
   __shared__ unsigned long long lds_tot[4][kStatSlots];  // per-wave 64-bit Stats totals
   const int wib = (int)(threadIdx.x >> 6);
   LdsF* ls = (LdsF*)&lds[wib][0][__lane_id()];
@@ -691,6 +694,43 @@ __global__ __launch_bounds__(256) RTMI_OCC void k_render_fast(const FastParams p
     const int L = p->lanes_per_px;
     const int iters = (p->spp + L - 1) / L;
     const GroupPix gp = group_pixel(p, g, lane_id_fresh());
+    // multiJittered / correlatedMultiJittered (sampling.nim:39-113): the
+    // wave builds each of its pixels' (m, m) tables in LDS — canonical
+    // entries spread over the pixel's lanes, then the x shuffle with one
+    // lane per column and the y shuffle with one lane per row (each lane
+    // only touches its own column / row, so the sequential reference order
+    // holds per lane; rt_sampling.h draw indices)
+    LdsF* tb = nullptr;
+    if ((F & F_STOCHASTIC) && p->aa_kind >= 3) {
+      const int m = p->grid_m, spp = p->spp;
+      const uint64_t key = rng_pixel_key(p->seed, gp.x, gp.y);
+      tb = (LdsF*)sample_lds + ((size_t)(wib * (64 / L) + (lane_id_fresh() >> p->log2_lanes)) * 2 * spp);
+      volatile LdsF* t = tb;
+      for (int e = gp.sub; e < spp; e += L) {
+        double a, b;
+        canonical_entry(key, m, e, a, b);
+        t[e] = (float)a;
+        t[spp + e] = (float)b;
+      }
+      const uint64_t bx = 2 * (uint64_t)spp;
+      const uint64_t by = bx + (p->aa_kind == 3 ? (uint64_t)spp : (uint64_t)m);
+      if (gp.sub < m) {
+        const int i = gp.sub;  // column i: the x shuffle
+        for (int j = 0; j < m; ++j) {
+          const int k = rng_pick(rng_draw(key, p->aa_kind == 3 ? bx + (uint64_t)j * m + i : bx + (uint64_t)j), j, m);
+          const float a = t[j * m + i], b = t[k * m + i];
+          t[j * m + i] = b;
+          t[k * m + i] = a;
+        }
+        const int j = gp.sub;  // row j: the y shuffle
+        for (int ii = 0; ii < m; ++ii) {
+          const int k = rng_pick(rng_draw(key, p->aa_kind == 3 ? by + (uint64_t)ii * m + j : by + (uint64_t)ii), ii, m);
+          const float a = t[spp + j * m + ii], b = t[spp + j * m + k];
+          t[spp + j * m + ii] = b;
+          t[spp + j * m + k] = a;
+        }
+      }
+    }
     Acc pacc;
     pacc.v = f3(0.0f, 0.0f, 0.0f);
     for (int it = 0; it < iters; ++it) {
@@ -698,11 +738,21 @@ __global__ __launch_bounds__(256) RTMI_OCC void k_render_fast(const FastParams p
       const int s = it * L + gp.sub;  // this lane's sample index
       const bool sv = gp.valid && s < p->spp;
       float px = (float)gp.x, py = (float)gp.y;
-      if (p->aa_kind != 0) {  // grid() sampling.nim:5-18: sample s = (si, sj)
+      if (p->aa_kind == 1) {  // grid() sampling.nim:5-18: sample s = (si, sj)
         int si;
         const int sj = div_small(s, p->grid_m, p->sample_step, si);
         px += __builtin_fmaf((float)si, p->sample_step, p->sample_off);
         py += __builtin_fmaf((float)sj, p->sample_step, p->sample_off);
+      } else if ((F & F_STOCHASTIC) && p->aa_kind == 2) {  // jitteredGrid (sampling.nim:21-33): no table needed
+        double a, b;
+        jittered_entry(rng_pixel_key(p->seed, gp.x, gp.y), p->grid_m, s < p->spp ? s : 0, a, b);
+        px += (float)a;
+        py += (float)b;
+      } else if (tb) {
+        const volatile LdsF* t = tb;
+        const int ss = s < p->spp ? s : 0;
+        px += t[ss];
+        py += t[p->spp + ss];
       }
       // castPrimaryRay (renderer.nim:31-44), constants folded on the host
       // ((2 x r)/w - r) f == (x - w/2) (2 r f / w): exact 0 on the centre

@@ -56,43 +56,46 @@ template __global__ void fast::k_render_fast<true, fast::F_ALL>(const FastParams
 
 }  // namespace rtmi
 
-// feature-subset specialisations: rt_kernels_f32_part.hip, 8 objects
+// feature-subset specialisations: rt_kernels_f32_part.hip, 16 objects
 #define RTMI_PART_DECL(k)                                                                             \
-  extern "C" int rtmi_launch_render_f32_part##k(unsigned, const rtmi::FastParams*, int, void*);      \
-  extern "C" int rtmi_render_f32_part_blocks_per_cu##k(unsigned);
+  extern "C" int rtmi_launch_render_f32_part##k(unsigned, const rtmi::FastParams*, int, size_t, void*); \
+  extern "C" int rtmi_render_f32_part_blocks_per_cu##k(unsigned, size_t);
 RTMI_PART_DECL(0) RTMI_PART_DECL(1) RTMI_PART_DECL(2) RTMI_PART_DECL(3)
 RTMI_PART_DECL(4) RTMI_PART_DECL(5) RTMI_PART_DECL(6) RTMI_PART_DECL(7)
+RTMI_PART_DECL(8) RTMI_PART_DECL(9) RTMI_PART_DECL(10) RTMI_PART_DECL(11)
+RTMI_PART_DECL(12) RTMI_PART_DECL(13) RTMI_PART_DECL(14) RTMI_PART_DECL(15)
 
 namespace {
-int (*const kLaunch[8])(unsigned, const rtmi::FastParams*, int, void*) = {
-    rtmi_launch_render_f32_part0, rtmi_launch_render_f32_part1, rtmi_launch_render_f32_part2,
-    rtmi_launch_render_f32_part3, rtmi_launch_render_f32_part4, rtmi_launch_render_f32_part5,
-    rtmi_launch_render_f32_part6, rtmi_launch_render_f32_part7};
-int (*const kOccupancy[8])(unsigned) = {
-    rtmi_render_f32_part_blocks_per_cu0, rtmi_render_f32_part_blocks_per_cu1, rtmi_render_f32_part_blocks_per_cu2,
-    rtmi_render_f32_part_blocks_per_cu3, rtmi_render_f32_part_blocks_per_cu4, rtmi_render_f32_part_blocks_per_cu5,
-    rtmi_render_f32_part_blocks_per_cu6, rtmi_render_f32_part_blocks_per_cu7};
+#define RTMI_L(k) rtmi_launch_render_f32_part##k
+#define RTMI_O(k) rtmi_render_f32_part_blocks_per_cu##k
+int (*const kLaunch[16])(unsigned, const rtmi::FastParams*, int, size_t, void*) = {
+    RTMI_L(0), RTMI_L(1), RTMI_L(2),  RTMI_L(3),  RTMI_L(4),  RTMI_L(5),  RTMI_L(6),  RTMI_L(7),
+    RTMI_L(8), RTMI_L(9), RTMI_L(10), RTMI_L(11), RTMI_L(12), RTMI_L(13), RTMI_L(14), RTMI_L(15)};
+int (*const kOccupancy[16])(unsigned, size_t) = {
+    RTMI_O(0), RTMI_O(1), RTMI_O(2),  RTMI_O(3),  RTMI_O(4),  RTMI_O(5),  RTMI_O(6),  RTMI_O(7),
+    RTMI_O(8), RTMI_O(9), RTMI_O(10), RTMI_O(11), RTMI_O(12), RTMI_O(13), RTMI_O(14), RTMI_O(15)};
 }  // namespace
 
-extern "C" int rtmi_launch_render_f32(const rtmi::FastParams* p, unsigned subset, int blocks, void* stream) {
+extern "C" int rtmi_launch_render_f32(const rtmi::FastParams* p, unsigned subset, int blocks, size_t shmem,
+                                      void* stream) {
   if (p->flags & rtmi::RT_DEV_FLAG_COUNT) {
-    hipLaunchKernelGGL((rtmi::fast::k_render_fast<true, rtmi::fast::F_ALL>), dim3(blocks), dim3(256), 0,
+    hipLaunchKernelGGL((rtmi::fast::k_render_fast<true, rtmi::fast::F_ALL>), dim3(blocks), dim3(256), shmem,
                        (hipStream_t)stream, *p);
     return (int)hipGetLastError();
   }
-  return kLaunch[(subset >> 3) & 7u](subset & 63u, p, blocks, stream);
+  return kLaunch[(subset >> 3) & 15u](subset & 127u, p, blocks, shmem, stream);
 }
 
 // Resident 256-thread blocks per CU of the render kernel (grid sizing for the
 // work-queue loop: launch exactly what fits, waves pull pixel groups).
-extern "C" int rtmi_render_f32_blocks_per_cu(int count, unsigned subset) {
+extern "C" int rtmi_render_f32_blocks_per_cu(int count, unsigned subset, size_t shmem) {
   if (count) {
     int nb = 0;
     const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &nb, rtmi::fast::k_render_fast<true, rtmi::fast::F_ALL>, 256, 0);
+        &nb, rtmi::fast::k_render_fast<true, rtmi::fast::F_ALL>, 256, shmem);
     return e == hipSuccess && nb > 0 ? nb : 1;
   }
-  return kOccupancy[(subset >> 3) & 7u](subset & 63u);
+  return kOccupancy[(subset >> 3) & 15u](subset & 127u, shmem);
 }
 
 extern "C" int rtmi_launch_reduce_stats(const unsigned long long* partials, int num_waves,

@@ -1,15 +1,15 @@
 // rt_kernels_f32_part.hip — the float32 render kernel specialised for scene
-// feature subsets (rt_fast.h F_* bits). Compiled 8 times (Makefile,
-// -DRTMI_PART=0..7), each object instantiating 8 of the 64 subsets of
-// {sphere, box, mesh, general transform, point light, reflection}; the plane
-// is always included. The host launches the exact subset a scene uses
+// feature subsets (rt_fast.h F_* bits). Compiled 16 times (Makefile,
+// -DRTMI_PART=0..15), each object instantiating 8 of the 128 subsets of
+// {sphere, box, mesh, general transform, point light, reflection,
+// stochastic sampling}; the plane is always included. The host launches the exact subset a scene uses
 // (rtmi.cpp scene_features), so e.g. the mesh + plane scenes of C3-C5 run
 // without the sphere / box / rotation / point-light / reflection code paths
 // (fewer branches, fewer SALU, 66 instead of 72+ VGPRs).
 #include "rt_fast.h"
 
 #ifndef RTMI_PART
-#error "compile with -DRTMI_PART=<0..7>"
+#error "compile with -DRTMI_PART=<0..15>"
 #endif
 
 namespace {
@@ -19,19 +19,22 @@ namespace f = rtmi::fast;
 
 constexpr unsigned subset_mask(unsigned i) {
   return f::F_PLANE | ((i & 1u) ? f::F_SPHERE : 0u) | ((i & 2u) ? f::F_BOX : 0u) | ((i & 4u) ? f::F_MESH : 0u) |
-         ((i & 8u) ? f::F_XF_GENERAL : 0u) | ((i & 16u) ? f::F_POINT : 0u) | ((i & 32u) ? f::F_REFLECT : 0u);
+         ((i & 8u) ? f::F_XF_GENERAL : 0u) | ((i & 16u) ? f::F_POINT : 0u) | ((i & 32u) ? f::F_REFLECT : 0u) |
+         ((i & 64u) ? f::F_STOCHASTIC : 0u);
 }
 
 template <unsigned I>
-int launch_one(const FastParams* p, int blocks, void* stream) {
-  hipLaunchKernelGGL((f::k_render_fast<false, subset_mask(I)>), dim3(blocks), dim3(256), 0, (hipStream_t)stream, *p);
+int launch_one(const FastParams* p, int blocks, size_t shmem, void* stream) {
+  hipLaunchKernelGGL((f::k_render_fast<false, subset_mask(I)>), dim3(blocks), dim3(256), shmem, (hipStream_t)stream,
+                     *p);
   return (int)hipGetLastError();
 }
 
 template <unsigned I>
-int occupancy_one() {
+int occupancy_one(size_t shmem) {
   int nb = 0;
-  const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, f::k_render_fast<false, subset_mask(I)>, 256, 0);
+  const hipError_t e =
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, f::k_render_fast<false, subset_mask(I)>, 256, shmem);
   return e == hipSuccess && nb > 0 ? nb : 1;
 }
 
@@ -42,30 +45,30 @@ constexpr unsigned B = RTMI_PART * 8u;
 #define RTMI_CAT2(a, b) a##b
 #define RTMI_CAT(a, b) RTMI_CAT2(a, b)
 
-// subset index i (0..63) -> launch; i >> 3 selects the part
+// subset index i (0..127) -> launch; i >> 3 selects the part
 extern "C" int RTMI_CAT(rtmi_launch_render_f32_part, RTMI_PART)(unsigned i, const FastParams* p, int blocks,
-                                                                 void* stream) {
+                                                                 size_t shmem, void* stream) {
   switch (i & 7u) {
-    case 0: return launch_one<B + 0>(p, blocks, stream);
-    case 1: return launch_one<B + 1>(p, blocks, stream);
-    case 2: return launch_one<B + 2>(p, blocks, stream);
-    case 3: return launch_one<B + 3>(p, blocks, stream);
-    case 4: return launch_one<B + 4>(p, blocks, stream);
-    case 5: return launch_one<B + 5>(p, blocks, stream);
-    case 6: return launch_one<B + 6>(p, blocks, stream);
-    default: return launch_one<B + 7>(p, blocks, stream);
+    case 0: return launch_one<B + 0>(p, blocks, shmem, stream);
+    case 1: return launch_one<B + 1>(p, blocks, shmem, stream);
+    case 2: return launch_one<B + 2>(p, blocks, shmem, stream);
+    case 3: return launch_one<B + 3>(p, blocks, shmem, stream);
+    case 4: return launch_one<B + 4>(p, blocks, shmem, stream);
+    case 5: return launch_one<B + 5>(p, blocks, shmem, stream);
+    case 6: return launch_one<B + 6>(p, blocks, shmem, stream);
+    default: return launch_one<B + 7>(p, blocks, shmem, stream);
   }
 }
 
-extern "C" int RTMI_CAT(rtmi_render_f32_part_blocks_per_cu, RTMI_PART)(unsigned i) {
+extern "C" int RTMI_CAT(rtmi_render_f32_part_blocks_per_cu, RTMI_PART)(unsigned i, size_t shmem) {
   switch (i & 7u) {
-    case 0: return occupancy_one<B + 0>();
-    case 1: return occupancy_one<B + 1>();
-    case 2: return occupancy_one<B + 2>();
-    case 3: return occupancy_one<B + 3>();
-    case 4: return occupancy_one<B + 4>();
-    case 5: return occupancy_one<B + 5>();
-    case 6: return occupancy_one<B + 6>();
-    default: return occupancy_one<B + 7>();
+    case 0: return occupancy_one<B + 0>(shmem);
+    case 1: return occupancy_one<B + 1>(shmem);
+    case 2: return occupancy_one<B + 2>(shmem);
+    case 3: return occupancy_one<B + 3>(shmem);
+    case 4: return occupancy_one<B + 4>(shmem);
+    case 5: return occupancy_one<B + 5>(shmem);
+    case 6: return occupancy_one<B + 6>(shmem);
+    default: return occupancy_one<B + 7>(shmem);
   }
 }

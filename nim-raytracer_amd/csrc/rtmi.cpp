@@ -144,6 +144,7 @@ struct rt_scene {
   DevBuf<unsigned long long> partials;
   DevBuf<unsigned long long> acc;
   DevBuf<unsigned int> queue;      // float32 work-queue heads (kQueueShards * kQueueStride)
+  DevBuf<double> f64_tables;       // float64 kernel per-lane stochastic sample tables
   DevBuf<float> fb_scratch;
   int max_waves = 0;
   int64_t num_triangles = 0, num_nodes = 0;
@@ -156,6 +157,7 @@ struct rt_scene {
     nodes.release();
     partials.release();
     queue.release();
+    f64_tables.release();
     acc.release();
     fb_scratch.release();
     if (done) (void)hipEventDestroy(done);
@@ -663,17 +665,36 @@ int check_options(const rt_scene* s, const rt_options* o) {
   if (!o) return fail(RT_E_INVALID, "null options");
   if (o->width <= 0 || o->height <= 0 || o->width > 65536 || o->height > 65536)
     return fail(RT_E_INVALID, "bad image size %dx%d", o->width, o->height);
-  if (o->aa_kind == RT_AA_JITTERED || o->aa_kind == RT_AA_MULTI_JITTERED ||
-      o->aa_kind == RT_AA_CORRELATED_MULTI_JITTERED)
-    return fail(RT_E_UNSUPPORTED, "stochastic antialias kind %d is not implemented yet", o->aa_kind);
-  if (o->aa_kind != RT_AA_NONE && o->aa_kind != RT_AA_GRID) return fail(RT_E_INVALID, "bad aa_kind %d", o->aa_kind);
-  if (o->aa_kind == RT_AA_GRID && (o->grid_size < 1 || o->grid_size > 256))
+  if (o->aa_kind < RT_AA_NONE || o->aa_kind > RT_AA_CORRELATED_MULTI_JITTERED)
+    return fail(RT_E_INVALID, "bad aa_kind %d", o->aa_kind);
+  if (o->aa_kind != RT_AA_NONE && (o->grid_size < 1 || o->grid_size > 256))
     return fail(RT_E_INVALID, "grid_size %d out of range [1, 256]", o->grid_size);
   if (o->precision != RT_FP32 && o->precision != RT_FP64) return fail(RT_E_INVALID, "bad precision");
+  // the float32 kernel builds a (multi-)jittered table in LDS per pixel:
+  // 8 KB per wave at m = 32
+  if (o->precision == RT_FP32 && o->aa_kind >= RT_AA_MULTI_JITTERED && o->grid_size > 32)
+    return fail(RT_E_UNSUPPORTED, "float32 (multi-)jittered sampling supports grid_size <= 32 (got %d)",
+                o->grid_size);
   if (s->any_reflective && o->max_ray_depth > kMaxShadeLevels - 1)
     return fail(RT_E_UNSUPPORTED, "max_ray_depth %d > %d with reflective materials", o->max_ray_depth,
                 kMaxShadeLevels - 1);
   return RT_OK;
+}
+
+// The float32 kernel specialisation of a launch: the scene's features plus
+// stochastic sampling when the options ask for it.
+unsigned f32_subset(const rt_scene* s, const rt_options* o) {
+  return s->f32_subset | (o->aa_kind >= RT_AA_JITTERED ? SUB_STOCHASTIC : 0u);
+}
+
+// Dynamic LDS of a float32 launch: the (multi-)jittered tables, 64/L
+// pixels per wave x 2 x spp floats x 4 waves per block.
+size_t f32_table_lds(const rt_options* o) {
+  if (o->precision != RT_FP32 || o->aa_kind < RT_AA_MULTI_JITTERED) return 0;
+  const int spp = o->grid_size * o->grid_size;
+  int L = 1;
+  while (L * 2 <= std::min(spp, 64)) L *= 2;
+  return (size_t)4 * (64 / L) * 2 * (size_t)spp * sizeof(float);
 }
 
 // Lanes per pixel (L), pixels per wave tile, number of wave groups, grid.
@@ -714,7 +735,8 @@ Plan plan_mapping(const rt_scene* s, const rt_options* o, const Mapping& mp, int
   const long long want = (ng + 3) / 4;
   long long cap = s->max_waves / 4;
   if (o->precision == RT_FP32) {  // work-queue kernel: launch what is resident
-    const int per_cu = rtmi_render_f32_blocks_per_cu((o->flags & RT_FLAG_COUNT_TRAVERSAL) ? 1 : 0, s->f32_subset);
+    const int per_cu = rtmi_render_f32_blocks_per_cu((o->flags & RT_FLAG_COUNT_TRAVERSAL) ? 1 : 0,
+                                                     f32_subset(s, o), f32_table_lds(o));
     cap = std::min<long long>(cap, (long long)per_cu * s->num_cus);
   }
   pl.blocks = (int)std::max(1LL, std::min<long long>(want, cap));
@@ -748,7 +770,7 @@ void fill_fast(rt_scene* s, const rt_options* o, const Mapping& mp, float* fb, F
   p.cam_d = (float)(0.5 * (double)o->height);
   for (int k = 0; k < 3; ++k) p.bg[k] = (float)s->bg[k];
   p.bias = (float)o->bias;
-  const int m = o->aa_kind == RT_AA_GRID ? o->grid_size : 1;
+  const int m = o->aa_kind != RT_AA_NONE ? o->grid_size : 1;
   const int spp = m * m;
   p.inv_len = (float)(1.0 / (double)spp);
   p.sample_step = (float)(1.0 / (double)m);
@@ -756,6 +778,7 @@ void fill_fast(rt_scene* s, const rt_options* o, const Mapping& mp, float* fb, F
   p.nobj = s->nobj;
   p.nlight = s->nlight;
   p.has_point_light = s->has_point_light;
+  p.seed = o->seed;
   p.width = o->width;
   p.height = o->height;
   p.aa_kind = o->aa_kind;
@@ -810,7 +833,7 @@ void fill_params(rt_scene* s, const PrecisionData<R>& pd, const rt_options* o, c
   p.f = (R)std::tan(s->fov * (3.14159265358979323846 / 180.0) / 2);
   p.aspect = (R)((double)o->width / (double)o->height);
   p.bias = (R)o->bias;
-  const int m = o->aa_kind == RT_AA_GRID ? o->grid_size : 1;
+  const int m = o->aa_kind != RT_AA_NONE ? o->grid_size : 1;
   const int spp = m * m;
   p.inv_len = (R)(1.0 / (double)spp);
   const double xs = 1.0 / (double)m;  // grid(): xs = 1/n, ys = 1/m (m = n)
@@ -826,6 +849,8 @@ void fill_params(rt_scene* s, const PrecisionData<R>& pd, const rt_options* o, c
   p.max_depth = o->max_ray_depth;
   p.flags = (int32_t)o->flags;
   p.shadow_mesh = s->shadow_mesh;
+  p.seed = o->seed;
+  p.sample_scratch = nullptr;
   p.max_iters = (int32_t)std::min<int64_t>(INT32_MAX, 2 * s->num_nodes + 16);
   p.mode = mp.mode;
   p.y0 = mp.y0;
@@ -860,7 +885,12 @@ void fill_params(rt_scene* s, const PrecisionData<R>& pd, const rt_options* o, c
   const long long tiles_y = (mp.nrows + ty - 1) / ty;
   p.ngroups = (long long)p.tiles_x * tiles_y;
   const long long want = (p.ngroups + 3) / 4;
-  *blocks = (int)std::max(1LL, std::min<long long>(want, s->max_waves / 4));
+  long long cap = s->max_waves / 4;
+  if (o->aa_kind >= RT_AA_JITTERED) {  // per-lane sample tables: keep the scratch <= 256 MB
+    const long long per_block = 256LL * 2 * spp * (long long)sizeof(R);
+    cap = std::min(cap, std::max(1LL, (256LL << 20) / per_block));
+  }
+  *blocks = (int)std::max(1LL, std::min<long long>(want, cap));
 }
 
 int launch(rt_scene* s, const rt_options* o, const Mapping& mp, float* d_out, hipStream_t st) {
@@ -869,13 +899,22 @@ int launch(rt_scene* s, const rt_options* o, const Mapping& mp, float* d_out, hi
     RenderParams<double> p;
     fill_params<double>(s, s->f64, o, mp, d_out, p, &blocks);
     if (p.ngroups == 0) return RT_OK;
+    if (p.aa_kind >= RT_AA_JITTERED) {
+      const size_t need = (size_t)blocks * 256 * 2 * (size_t)p.spp;
+      if (s->f64_tables.n < need) {
+        HIP_TRY(hipStreamSynchronize(st));  // an earlier launch may still use the old buffer
+        int rc = s->f64_tables.alloc(need);
+        if (rc) return rc;
+      }
+      p.sample_scratch = s->f64_tables.p;
+    }
     const int e = rtmi_launch_render_f64(&p, blocks, st);
     if (e) return fail(RT_E_DEVICE, "render kernel launch failed: %s", hipGetErrorString((hipError_t)e));
   } else {
     FastParams p;
     fill_fast(s, o, mp, d_out, p, &blocks);
     if (p.ngroups == 0) return RT_OK;
-    const int e = rtmi_launch_render_f32(&p, s->f32_subset, blocks, st);
+    const int e = rtmi_launch_render_f32(&p, f32_subset(s, o), blocks, f32_table_lds(o), st);
     if (e) return fail(RT_E_DEVICE, "render kernel launch failed: %s", hipGetErrorString((hipError_t)e));
   }
   const int e = rtmi_launch_reduce_stats(s->partials.p, blocks * 4, s->acc.p, st);

@@ -38,6 +38,8 @@ def _load():
     lib.oracle_scene_destroy.argtypes = [P]
     lib.oracle_scene_build_bvh.restype = C.c_int
     lib.oracle_scene_build_bvh.argtypes = [P]
+    lib.oracle_sample_table.restype = None
+    lib.oracle_sample_table.argtypes = [C.c_int32, C.c_int32, C.c_uint64, C.c_int32, C.c_int32, dp, dp]
     lib.oracle_render_line.restype = C.c_int
     lib.oracle_render_line.argtypes = [P, C.POINTER(abi.rt_options), C.POINTER(C.c_float),
                                        C.c_int32, C.c_int32, C.c_int32, C.POINTER(abi.rt_stats)]
@@ -80,6 +82,15 @@ def lib():
 def _dp(a):
     a = np.ascontiguousarray(np.asarray(a, dtype=np.float64))
     return a, a.ctypes.data_as(C.POINTER(C.c_double))
+
+
+def sample_table(kind, m, seed, x, y):
+    """(sx, sy) of a stochastic antialias kind's m*m table for pixel (x, y)."""
+    sx = np.zeros(m * m)
+    sy = np.zeros(m * m)
+    lib().oracle_sample_table(int(kind), int(m), int(seed), int(x), int(y),
+                              sx.ctypes.data_as(C.POINTER(C.c_double)), sy.ctypes.data_as(C.POINTER(C.c_double)))
+    return sx, sy
 
 
 class OracleScene:

@@ -672,8 +672,95 @@ static void sample(const oracle_scene *s, const rt_options *o, double px, double
   shade(s, o, &ray, obj, t, out, st);
 }
 
+/* ---- stochastic samplers (sampling.nim:21-113) -------------------------- */
+/* The reference draws from Nim's `random`, seeded from the clock
+ * (renderer.nim:215 `randomize()`), so its jittered images are not
+ * reproducible. Here every draw is a pure function of (options.seed, pixel,
+ * draw index) — a SplitMix64 counter RNG — so the device kernels (which
+ * build a pixel's table in parallel) reproduce it exactly; the ORDER of the
+ * draws is the reference's loop order:
+ *   jitteredGrid   sampling.nim:21-33  2 draws per (j, i), row-major;
+ *   multiJittered  sampling.nim:39-76  2 per (j, i) canonical, then one per
+ *                                      (j, i) for the x shuffle, then one per
+ *                                      (i, j) (i outer) for the y shuffle;
+ *   correlatedMJ   sampling.nim:79-113 same canonical, one per row j (x), one
+ *                                      per column i (y).
+ * random(x) = u * x with u uniform in [0, 1) (53 bits); `.int` truncates. */
+static uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+  return z ^ (z >> 31);
+}
+static uint64_t pixel_key(uint64_t seed, int32_t x, int32_t y) {
+  return mix64(seed ^ mix64(((uint64_t)(uint32_t)y << 32) | (uint32_t)x));
+}
+static double draw_u(uint64_t key, uint64_t k) {
+  return (double)(mix64(key + (k + 1) * 0x9E3779B97F4A7C15ULL) >> 11) * (1.0 / 9007199254740992.0);
+}
+
+/* p[j*m + i] of jitteredGrid / multiJittered / correlatedMultiJittered (m, m). */
+static void sample_table(int32_t kind, int32_t m, uint64_t key, double *sx, double *sy) {
+  const int32_t n = m;
+  const double xs = 1.0 / (double)n, ys = 1.0 / (double)m;
+  if (kind == RT_AA_JITTERED) {
+    for (int32_t j = 0; j < m; ++j)
+      for (int32_t i = 0; i < n; ++i) {
+        const int32_t e = j * m + i;
+        sx[e] = (double)i * xs + draw_u(key, 2 * (uint64_t)e) * xs;
+        sy[e] = (double)j * ys + draw_u(key, 2 * (uint64_t)e + 1) * ys;
+      }
+    return;
+  }
+  for (int32_t j = 0; j < n; ++j)
+    for (int32_t i = 0; i < m; ++i) {
+      const int32_t e = j * m + i;
+      sx[e] = ((double)i + ((double)j + draw_u(key, 2 * (uint64_t)e)) * xs) * ys;
+      sy[e] = ((double)j + ((double)i + draw_u(key, 2 * (uint64_t)e + 1)) * ys) * xs;
+    }
+  const uint64_t bx = 2 * (uint64_t)m * n;
+  if (kind == RT_AA_MULTI_JITTERED) {
+    const uint64_t by = bx + (uint64_t)m * n;
+    for (int32_t j = 0; j < n; ++j)
+      for (int32_t i = 0; i < m; ++i) {
+        const int32_t k = j + (int32_t)(draw_u(key, bx + (uint64_t)j * m + i) * (double)(n - j));
+        const double t = sx[j * m + i];
+        sx[j * m + i] = sx[k * m + i];
+        sx[k * m + i] = t;
+      }
+    for (int32_t i = 0; i < m; ++i)
+      for (int32_t j = 0; j < n; ++j) {
+        const int32_t k = i + (int32_t)(draw_u(key, by + (uint64_t)i * n + j) * (double)(m - i));
+        const double t = sy[j * m + i];
+        sy[j * m + i] = sy[j * m + k];
+        sy[j * m + k] = t;
+      }
+  } else { /* correlated: one k per row (x) and per column (y) */
+    const uint64_t by = bx + (uint64_t)n;
+    for (int32_t j = 0; j < n; ++j) {
+      const int32_t k = j + (int32_t)(draw_u(key, bx + (uint64_t)j) * (double)(n - j));
+      for (int32_t i = 0; i < m; ++i) {
+        const double t = sx[j * m + i];
+        sx[j * m + i] = sx[k * m + i];
+        sx[k * m + i] = t;
+      }
+    }
+    for (int32_t i = 0; i < m; ++i) {
+      const int32_t k = i + (int32_t)(draw_u(key, by + (uint64_t)i) * (double)(m - i));
+      for (int32_t j = 0; j < n; ++j) {
+        const double t = sy[j * m + i];
+        sy[j * m + i] = sy[j * m + k];
+        sy[j * m + k] = t;
+      }
+    }
+  }
+}
+
+void oracle_sample_table(int32_t kind, int32_t m, uint64_t seed, int32_t x, int32_t y, double *sx, double *sy) {
+  sample_table(kind, m, pixel_key(seed, x, y), sx, sy);
+}
+
 /* calcPixelNoSampling / calcPixel (renderer.nim:132-159) with grid()
- * (sampling.nim:5-18, incl. yoffs = xs*0.5). */
+ * (sampling.nim:5-18, incl. yoffs = xs*0.5) or the stochastic tables. */
 void oracle_calc_pixel(const oracle_scene *s, const rt_options *o, int32_t x, int32_t y,
                        double rgb[3], rt_stats *st) {
   if (o->aa_kind == RT_AA_NONE) {
@@ -685,13 +772,20 @@ void oracle_calc_pixel(const oracle_scene *s, const rt_options *o, int32_t x, in
   const double xoffs = xs * 0.5, yoffs = xs * 0.5;
   double acc[3] = {0.0, 0.0, 0.0};
   const int32_t len = m * n;
+  double *tx = NULL, *ty = NULL;
+  if (o->aa_kind != RT_AA_GRID) {
+    tx = (double *)malloc(sizeof(double) * 2 * (size_t)len);
+    ty = tx + len;
+    sample_table(o->aa_kind, m, pixel_key(o->seed, x, y), tx, ty);
+  }
   for (int32_t k = 0; k < len; ++k) {
     const int32_t j = k / m, i = k % m; /* p[j*m + i] */
-    const double sx = (double)i * xs + xoffs, sy = (double)j * ys + yoffs;
+    const double sx = tx ? tx[k] : (double)i * xs + xoffs, sy = ty ? ty[k] : (double)j * ys + yoffs;
     double c[3];
     sample(s, o, (double)x + sx, (double)y + sy, c, st);
     for (int q = 0; q < 3; ++q) acc[q] = acc[q] + c[q];
   }
+  free(tx);
   const double inv = 1.0 / (double)len;
   for (int q = 0; q < 3; ++q) rgb[q] = acc[q] * inv;
 }
@@ -703,8 +797,8 @@ int oracle_render_line(const oracle_scene *s, const rt_options *o, float *fb, in
   if (!s || !o || !fb) return RT_E_INVALID;
   if (!is_pow2(step) || !is_pow2(max_step) || max_step < step) return RT_E_INVALID;
   if (y < 0 || y >= o->height) return RT_E_INVALID;
-  if (o->aa_kind != RT_AA_NONE && o->aa_kind != RT_AA_GRID) return RT_E_UNSUPPORTED;
-  if (o->aa_kind == RT_AA_GRID && o->grid_size < 1) return RT_E_INVALID;
+  if (o->aa_kind < RT_AA_NONE || o->aa_kind > RT_AA_CORRELATED_MULTI_JITTERED) return RT_E_INVALID;
+  if (o->aa_kind != RT_AA_NONE && (o->grid_size < 1 || o->grid_size > 256)) return RT_E_INVALID;
   rt_stats st;
   memset(&st, 0, sizeof(st));
   const int32_t w = o->width, h = o->height;

@@ -60,6 +60,10 @@ double oracle_sphere_intersect(double r, const double orig[4],
 int32_t oracle_trace(const oracle_scene *s, const double orig[4],
                      const double dir[4], double t_near, double *t_hit,
                      int64_t *tri_hit, rt_stats *stats);
+/* The (m, m) sample table of a stochastic antialias kind for pixel (x, y):
+ * sx/sy hold m*m offsets in the reference's p[j*m + i] order. */
+void oracle_sample_table(int32_t kind, int32_t m, uint64_t seed, int32_t x,
+                         int32_t y, double *sx, double *sy);
 /* calcPixelNoSampling / calcPixel (renderer.nim:132-159), fp64 colour. */
 void oracle_calc_pixel(const oracle_scene *s, const rt_options *o, int32_t x,
                        int32_t y, double rgb[3], rt_stats *stats);

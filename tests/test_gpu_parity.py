@@ -221,3 +221,58 @@ def test_fp32_tiny_launches(gpu, oracle_mod, w, h, m):
     got, gst, _ = _gpu_frame(scene, _opts(w, h, Precision.fp32, aa, m))
     assert gst.numPrimaryRays == rst.numPrimaryRays == w * h * m * m
     assert np.abs(got - ref).max() <= 2e-3
+
+
+STOCHASTIC = ["akJittered", "akMultiJittered", "akCorrelatedMultiJittered"]
+
+
+def _kind(name):
+    from rtmi import scene as sc
+    return getattr(sc, name)
+
+
+@pytest.mark.parametrize("kind", STOCHASTIC)
+@pytest.mark.parametrize("name,m", [("spheres-warm-3", 3), ("mesh-bunny", 4)])
+def test_stochastic_fp64_bit_exact(gpu, oracle_mod, kind, name, m):
+    """jitteredGrid / multiJittered / correlatedMultiJittered (sampling.nim:21-113)
+    over the counter RNG (rt_sampling.h): the fp64 kernel's per-lane tables
+    reproduce the oracle's exactly."""
+    scene = scenes.SCENES[name]()
+    opts = _opts(40, 24, Precision.fp64, _kind(kind), m, seed=0xC0FFEE)
+    ref, rst = _oracle_frame(oracle_mod, scene, opts)
+    got, gst, _ = _gpu_frame(scene, opts)
+    assert np.array_equal(got, ref)
+    assert gst == rst
+
+
+@pytest.mark.parametrize("kind", STOCHASTIC)
+@pytest.mark.parametrize("m", [2, 9, 16])
+def test_stochastic_fp32_within_tolerance(gpu, oracle_mod, kind, m):
+    """The fp32 kernel's LDS-built tables (one lane per column / row for the
+    shuffles): 9x9 spreads 81 samples over 64 lanes, 2x2 packs 16 pixels in
+    a wave."""
+    scene = scenes.spheres_warm(3)
+    ref, rst = _oracle_frame(oracle_mod, scene, _opts(32, 20, Precision.fp64, _kind(kind), m, seed=99))
+    got, gst, _ = _gpu_frame(scene, _opts(32, 20, Precision.fp32, _kind(kind), m, seed=99))
+    _assert_fp32_close(got, ref)
+    assert gst.numPrimaryRays == rst.numPrimaryRays == 32 * 20 * m * m
+
+
+@pytest.mark.parametrize("prec", [Precision.fp64, Precision.fp32])
+def test_stochastic_bands_match_full_frame(gpu, prec):
+    """Samples depend only on (seed, absolute pixel): band-sharded renders are
+    bit-identical to the whole frame."""
+    import torch
+
+    ds = DeviceScene(scenes.spheres_warm(3))
+    opts = _opts(48, 40, prec, _kind("akMultiJittered"), 8, seed=5)
+    full = torch.zeros(48 * 40 * 3, dtype=torch.float32, device="cuda")
+    ds.render_device(opts, full)
+    world, band_h = 3, 4
+    rows = band_rows(40, band_h, world)
+    gathered = torch.zeros(world * rows * 48 * 3, dtype=torch.float32, device="cuda")
+    for r in range(world):
+        ds.render_bands_device(opts, gathered[r * rows * 48 * 3:(r + 1) * rows * 48 * 3], band_h, r, world)
+    fb = torch.zeros_like(full)
+    unshard_bands_device(gathered, fb, 48, 40, band_h, world)
+    assert torch.equal(fb, full)
