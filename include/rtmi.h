@@ -146,6 +146,12 @@ typedef struct rt_options {
 /* Run the instrumented kernel that also counts BVH node / triangle record
  * fetches (rt_scene_last_counters). Slower; the image and Stats are the same. */
 #define RT_FLAG_COUNT_TRAVERSAL 0x2u
+/* float32 kernel: always hand pixel groups out in screen order. By default a
+ * short launch (a band set of a multi-GPU frame) that repeats a mapping already
+ * rendered on this scene hands them out longest-first, from per-group
+ * durations measured on its first launch. Scheduling only: the image and
+ * Stats are the same either way. */
+#define RT_FLAG_NO_REORDER 0x4u
 
 /* Stats (src/renderer/stats.nim:4-13) plus ray counts for Mray/s. */
 typedef struct rt_stats {

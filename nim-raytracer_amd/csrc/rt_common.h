@@ -194,6 +194,8 @@ struct FastParams {
   float* fb;
   unsigned long long* partials;
   unsigned int* queue;             // kQueueShards heads (atomicAdd), zeroed at launch
+  const int32_t* order;            // launch order of the pixel groups, or nullptr (identity)
+  unsigned* cost;                  // per pixel group: its duration in cycles, or nullptr
   float cam[12];       // origin, C2W column 0, 1, 2 (xyz each)
   float cam_a, cam_b;  // cx = (px - cam_b) * cam_a, cam_b = w/2   (renderer.nim:39)
   float cam_c, cam_d;  // cy = (cam_d - py) * cam_c, cam_d = h/2   (renderer.nim:40)

@@ -680,7 +680,9 @@ __global__ __launch_bounds__(256) RTMI_OCC void k_render_fast(const FastParams p
   // blocks, so every shard has pullers), each on its own 128-B line; shard k
   // hands out items k, k+8, k+16, ... so every shard's work spans the whole
   // image. The next index is fetched one item ahead, hiding the atomic's
-  // latency behind the samples.
+  // latency behind the samples. Item g is pixel group order[g] when the
+  // host supplies an expensive-first order; a measuring launch records each
+  // group's duration in cost[] (rtmi.cpp group_order).
   const int shard = (int)(blockIdx.x % (unsigned int)p->shards);
   unsigned int* head = p->queue + shard * kQueueStride;
   int qj = 0;
@@ -693,7 +695,9 @@ __global__ __launch_bounds__(256) RTMI_OCC void k_render_fast(const FastParams p
     p = params();
     const int L = p->lanes_per_px;
     const int iters = (p->spp + L - 1) / L;
-    const GroupPix gp = group_pixel(p, g, lane_id_fresh());
+    const int gg = p->order ? cp(p->order)[g] : g;
+    const unsigned t_item = (unsigned)__builtin_amdgcn_s_memtime();
+    const GroupPix gp = group_pixel(p, gg, lane_id_fresh());
     // multiJittered / correlatedMultiJittered (sampling.nim:39-113): the
     // wave builds each of its pixels' (m, m) tables in LDS — canonical
     // entries spread over the pixel's lanes, then the x shuffle with one
@@ -792,6 +796,7 @@ __global__ __launch_bounds__(256) RTMI_OCC void k_render_fast(const FastParams p
         q[0] = acc.x; q[1] = acc.y; q[2] = acc.z;
       }
     }
+    if (p->cost && lane == 0) p->cost[gg] = (unsigned)__builtin_amdgcn_s_memtime() - t_item;
     // 32-bit wave counters -> the wave's 64-bit LDS totals
     if (lane < kStatSlots) {
       unsigned int v = 0u;

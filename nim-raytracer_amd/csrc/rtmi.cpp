@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <chrono>
 #include <cmath>
@@ -145,6 +146,18 @@ struct rt_scene {
   DevBuf<unsigned long long> acc;
   DevBuf<unsigned int> queue;      // float32 work-queue heads (kQueueShards * kQueueStride)
   DevBuf<double> f64_tables;       // float64 kernel per-lane stochastic sample tables
+  struct Order {                   // one launch mapping's measured costs -> launch order
+    std::array<int64_t, 17> key;
+    DevBuf<unsigned> cost;         // cycles per pixel group, written by the measuring launch
+    DevBuf<int32_t> perm;          // the expensive-first order, once built
+    hipEvent_t measured = nullptr; // recorded after the measuring launch
+    ~Order() {
+      cost.release();
+      perm.release();
+      if (measured) (void)hipEventDestroy(measured);
+    }
+  };
+  std::vector<std::unique_ptr<Order>> orders;  // most recently used first, at most 8
   DevBuf<float> fb_scratch;
   int max_waves = 0;
   int64_t num_triangles = 0, num_nodes = 0;
@@ -743,7 +756,121 @@ Plan plan_mapping(const rt_scene* s, const rt_options* o, const Mapping& mp, int
   return pl;
 }
 
-void fill_fast(rt_scene* s, const rt_options* o, const Mapping& mp, float* fb, FastParams& p, int* blocks) {
+// Launch order of the pixel groups: expensive first, from measured costs.
+// Per-pixel cost varies ~20x (sky vs bunny + its shadows) and the work queue
+// hands groups out in index order, so a launch ends when the wave that drew
+// the last expensive group finishes it: a fixed ~0.2 ms on every C3 launch
+// (a group at 256 spp is one pixel, up to ~0.2 ms of a wave's time), 2.5 %
+// of a frame on one GPU and ~17 % of each rank's share on 8. The first
+// launch of a mapping (image size, rows, bands, sampling) runs in screen
+// order and records each group's duration (s_memtime); later launches of the
+// same mapping hand groups out longest-first (LPT), so the tail is cheap
+// groups — for launches short enough that the tail matters (below). Scheduling only: every launch traces every ray, and the image and
+// Stats do not depend on the order. Off with RT_FLAG_NO_REORDER.
+constexpr long long kLptGroupsPerWave = 96;
+
+struct OrderUse {
+  const int32_t* order = nullptr;  // FastParams.order
+  unsigned* cost = nullptr;        // FastParams.cost (the measuring launch)
+  rt_scene::Order* entry = nullptr;
+};
+
+int order_policy() {
+  static const int v = [] {
+    // tuning knob: 0 off, 1 LPT, 2 LPT in half octaves, 3 heavy then light
+    // (split at the RTMI_ORDER_P cost quantile, screen order within each),
+    // 4 = 3 with the light part longest-first
+    const char* e = std::getenv("RTMI_ORDER");
+    return e ? std::atoi(e) : 1;
+  }();
+  return v;
+}
+
+double order_quantile() {
+  static const double v = [] {
+    const char* e = std::getenv("RTMI_ORDER_P");
+    return e ? std::atof(e) : 0.5;
+  }();
+  return v;
+}
+
+OrderUse group_order(rt_scene* s, const rt_options* o, const Mapping& mp, const FastParams& p, int blocks) {
+  OrderUse u;
+  const int policy = order_policy();
+  // LPT only where the tail outweighs locality: with >= ~128 groups per
+  // resident wave, screen order's spatial coherence (neighbouring pixels
+  // share BVH paths in the scalar caches) is worth more than the tail (C3:
+  // whole frame 8.15 ms screen vs 8.36 LPT; half frame equal; quarter 2.22
+  // vs 2.10; eighth 1.23 vs 1.07; 1/64 0.34 vs 0.26)
+  const long long waves = (long long)blocks * 4;
+  if (policy == 0 || (o->flags & RT_FLAG_NO_REORDER) || p.ngroups < waves || p.ngroups > kLptGroupsPerWave * waves)
+    return u;
+  const std::array<int64_t, 17> key = {o->width,   o->height,  mp.mode,     mp.y0,       mp.nrows,  mp.ncols,
+                                       mp.step,    mp.max_step, mp.band_h,  mp.rank,     mp.world,  p.tile_x,
+                                       p.tile_y,   p.ngroups,   o->aa_kind, o->grid_size, o->max_ray_depth};
+  size_t i = 0;
+  while (i < s->orders.size() && s->orders[i]->key != key) ++i;
+  if (i == s->orders.size()) {  // new mapping: measure it
+    std::unique_ptr<rt_scene::Order> e(new rt_scene::Order());
+    e->key = key;
+    if (e->cost.alloc((size_t)p.ngroups) != RT_OK ||
+        hipEventCreateWithFlags(&e->measured, hipEventDisableTiming) != hipSuccess)
+      return u;
+    s->orders.insert(s->orders.begin(), std::move(e));
+    if (s->orders.size() > 8) s->orders.pop_back();
+    u.cost = s->orders[0]->cost.p;
+    u.entry = s->orders[0].get();
+    return u;
+  }
+  std::rotate(s->orders.begin(), s->orders.begin() + (long)i, s->orders.begin() + (long)i + 1);
+  rt_scene::Order& e = *s->orders[0];
+  if (!e.perm.p) {
+    std::vector<unsigned> c((size_t)p.ngroups);
+    if (hipEventSynchronize(e.measured) != hipSuccess ||
+        hipMemcpy(c.data(), e.cost.p, c.size() * sizeof(unsigned), hipMemcpyDeviceToHost) != hipSuccess)
+      return u;
+    // stable counting sort, most expensive bucket first
+    constexpr int kBuckets = 4096;
+    unsigned cmax = 1;
+    for (unsigned v : c) cmax = std::max(cmax, v);
+    unsigned split = 0;  // policies 3/4: costs above this are "heavy"
+    if (policy >= 3) {
+      std::vector<unsigned> t(c);
+      const size_t q = std::min(t.size() - 1, (size_t)(order_quantile() * (double)t.size()));
+      std::nth_element(t.begin(), t.begin() + (long)q, t.end());
+      split = t[q];
+    }
+    std::vector<uint16_t> bucket(c.size());
+    std::vector<int32_t> start(kBuckets + 1, 0);
+    for (size_t g = 0; g < c.size(); ++g) {
+      int b;
+      if (policy == 3) {
+        b = c[g] > split ? kBuckets - 1 : 0;
+      } else if (policy == 4) {
+        b = c[g] > split ? kBuckets - 1 : (int)((uint64_t)c[g] * (kBuckets - 2) / std::max(split, 1u));
+      } else if (policy == 2) {  // half-octave classes: keeps screen order within a class
+        const unsigned v = std::max(c[g], 1u);
+        const int l = 31 - __builtin_clz(v);
+        b = 2 * l + (l > 0 ? (int)((v >> (l - 1)) & 1u) : 0);
+      } else {
+        b = (int)((uint64_t)c[g] * (kBuckets - 1) / cmax);
+      }
+      b = kBuckets - 1 - b;
+      bucket[g] = (uint16_t)b;
+      ++start[(size_t)b + 1];
+    }
+    for (int b = 0; b < kBuckets; ++b) start[(size_t)b + 1] += start[(size_t)b];
+    std::vector<int32_t> perm(c.size());
+    for (size_t g = 0; g < c.size(); ++g) perm[(size_t)start[bucket[g]]++] = (int32_t)g;
+    if (e.perm.upload(perm) != RT_OK) return u;
+    e.cost.release();
+  }
+  u.order = e.perm.p;
+  return u;
+}
+
+void fill_fast(rt_scene* s, const rt_options* o, const Mapping& mp, float* fb, FastParams& p, int* blocks,
+               rt_scene::Order** measuring) {
   std::memset(&p, 0, sizeof p);
   p.objs = s->f32.objs.p;
   p.objx = s->f32.objx.p;
@@ -812,6 +939,10 @@ void fill_fast(rt_scene* s, const rt_options* o, const Mapping& mp, float* fb, F
   // 5.22 vs 4.69 ms per half). With 8 sharded heads the dequeue rate stays
   // far below the ~90/us a head sustains.
   p.shards = std::min(kQueueShards, pl.blocks);
+  const OrderUse ou = group_order(s, o, mp, p, pl.blocks);
+  p.order = ou.order;
+  p.cost = ou.cost;
+  *measuring = ou.entry;
   *blocks = pl.blocks;
 }
 
@@ -912,10 +1043,12 @@ int launch(rt_scene* s, const rt_options* o, const Mapping& mp, float* d_out, hi
     if (e) return fail(RT_E_DEVICE, "render kernel launch failed: %s", hipGetErrorString((hipError_t)e));
   } else {
     FastParams p;
-    fill_fast(s, o, mp, d_out, p, &blocks);
+    rt_scene::Order* measuring = nullptr;
+    fill_fast(s, o, mp, d_out, p, &blocks, &measuring);
     if (p.ngroups == 0) return RT_OK;
     const int e = rtmi_launch_render_f32(&p, f32_subset(s, o), blocks, f32_table_lds(o), st);
     if (e) return fail(RT_E_DEVICE, "render kernel launch failed: %s", hipGetErrorString((hipError_t)e));
+    if (measuring) HIP_TRY(hipEventRecord(measuring->measured, st));
   }
   const int e = rtmi_launch_reduce_stats(s->partials.p, blocks * 4, s->acc.p, st);
   if (e) return fail(RT_E_DEVICE, "stats reduction launch failed: %s", hipGetErrorString((hipError_t)e));

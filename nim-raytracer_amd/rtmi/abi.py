@@ -20,6 +20,7 @@ RT_AA_NONE, RT_AA_GRID, RT_AA_JITTERED, RT_AA_MULTI_JITTERED, RT_AA_CORRELATED_M
 RT_FP32, RT_FP64 = 0, 1
 RT_FLAG_ANYHIT_SHADOWS = 0x1
 RT_FLAG_COUNT_TRAVERSAL = 0x2
+RT_FLAG_NO_REORDER = 0x4
 
 _d16 = C.c_double * 16
 _d3 = C.c_double * 3

@@ -176,6 +176,35 @@ def test_bands_and_unshard_match_full_frame(gpu):
         assert prim == 173 * 131 * 4
 
 
+def test_launch_order_does_not_change_results(gpu):
+    """The float32 work queue's expensive-first order (rtmi.cpp group_order:
+    the first launch of a mapping measures per-group costs, later ones hand
+    groups out longest-first) is scheduling only: frames and Stats are
+    bit-identical to screen order (RT_FLAG_NO_REORDER), whole frame and
+    bands."""
+    import torch
+    from rtmi.abi import RT_FLAG_NO_REORDER
+    scene = scenes.mesh_bunny()
+    ds = DeviceScene(scene)
+    for m in (8, 4):  # 1 pixel per group / 4 pixels per group
+        plain = _opts(320, 240, Precision.fp32, akGrid, m, flags=RT_FLAG_NO_REORDER)
+        lpt = _opts(320, 240, Precision.fp32, akGrid, m)
+        ref = torch.zeros(320 * 240 * 3, dtype=torch.float32, device="cuda")
+        sref = ds.render_device(plain, ref)
+        for _ in range(3):  # measuring launch, then ordered launches
+            out = torch.zeros_like(ref)
+            assert ds.render_device(lpt, out) == sref
+            assert torch.equal(out, ref)
+        rows = band_rows(240, 4, 2)
+        for r in range(2):
+            a = torch.zeros(rows * 320 * 3, dtype=torch.float32, device="cuda")
+            b = torch.zeros_like(a)
+            sa = ds.render_bands_device(plain, a, 4, r, 2)
+            for _ in range(2):
+                assert ds.render_bands_device(lpt, b, 4, r, 2) == sa
+                assert torch.equal(a, b)
+
+
 def test_full_size_c3_properties(gpu, oracle_mod):
     """BASELINE config C3 at full size (1920x1080, 256 spp, fp32) through
     size-independent properties: determinism, exact primary/shadow ray
