@@ -75,6 +75,8 @@ def parse():
     ap.add_argument("--grid", type=int, default=None, help="akGrid m (spp = m*m)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--bvh", default="sah", choices=["sah", "ploc"],
+                    help="mesh BVH builder: host binned SAH (default) or device PLOC")
     ap.add_argument("--flags", type=int, default=0, help="rt_options.flags (1 = any-hit shadows)")
     return ap.parse_args()
 
@@ -166,7 +168,8 @@ def main():
     m = args.grid or m
     scene = _scene(scene_name)
     t0 = time.time()
-    ds = DeviceScene(scene, device=local)
+    from rtmi.abi import RT_BVH_PLOC, RT_BVH_SAH
+    ds = DeviceScene(scene, device=local, bvh_builder=RT_BVH_PLOC if args.bvh == "ploc" else RT_BVH_SAH)
     info = ds.info()
     setup_s = time.time() - t0
     opts = Options(width=W, height=H, antialias=Antialias(akGrid, m), bias=1e-4,
@@ -268,7 +271,8 @@ def main():
                 "width": W, "height": H, "spp": m * m, "triangles": info["num_triangles"],
                 "bvh_nodes": info["num_bvh_nodes"], "primary_rays_per_frame": prim_frame,
                 "shadow_rays_per_frame": shadow_frame, "parallelism": f"bands{world}",
-                "scene_setup_s": round(setup_s, 3), "bvh_build_ms": round(info["build_ms"], 1),
+                "scene_setup_s": round(setup_s, 3), "scene_setup_ms_lib": round(info["build_ms"], 1),
+                "bvh_builder": {"sah": "host binned SAH", "ploc": "device PLOC"}[args.bvh],
             },
             "roofline": {
                 "bound": "hbm",

@@ -112,6 +112,14 @@ typedef struct rt_light_desc {
   double pos[3];               /* PointLight.pos                         */
 } rt_light_desc;
 
+/* Mesh BVH builder. Either tree gives the brute-force answer (closest t,
+ * lowest face index on ties), so images and Stats do not depend on it. */
+typedef enum rt_bvh_builder {
+  RT_BVH_SAH = 0,  /* host binned SAH (32 bins, leaves <= 4 faces): best tracing */
+  RT_BVH_PLOC = 1  /* on the device: Morton sort + PLOC clustering + SAH leaf
+                      collapse, same node format; ~100x faster to build      */
+} rt_bvh_builder;
+
 /* Scene (src/renderer/scene.nim:11-18). */
 typedef struct rt_scene_desc {
   const rt_object_desc *objects;
@@ -120,7 +128,7 @@ typedef struct rt_scene_desc {
   const rt_light_desc *lights;
   const rt_mesh_desc *meshes;
   int32_t num_meshes;
-  int32_t reserved;
+  int32_t bvh_builder;         /* rt_bvh_builder (0 = host binned SAH)    */
   double fov;                  /* degrees, Scene.fov                     */
   double camera_to_world[16];  /* Scene.cameraToWorld                    */
   double bg_color[3];          /* Scene.bgColor                          */

@@ -268,9 +268,20 @@ bool build_bvh(const double* v, const int32_t* f, int64_t nf, const BvhBuildPara
     *err = "BVH deeper than the traversal stack";
     return false;
   }
-  // structural validation: every reference in range
-  const int32_t nn = (int32_t)out->nodes.size();
-  for (const BvhNode& nd : out->nodes) {
+  return validate_bvh(*out, nf, err);
+}
+
+bool validate_bvh(const BvhResult& r, int64_t nf, const char** err) {
+  const int32_t nn = (int32_t)r.nodes.size();
+  if (nf > 0 && nn == 0) {
+    *err = "BVH has no root";
+    return false;
+  }
+  std::vector<unsigned char> seen((size_t)nf, 0);
+  int64_t covered = 0;
+  const bool single = nn == 1 && r.nodes[0].n0 > 0 && r.nodes[0].c0 == r.nodes[0].c1 &&
+                      r.nodes[0].n0 == r.nodes[0].n1;  // one leaf, repeated in both slots
+  for (const BvhNode& nd : r.nodes) {
     const int32_t cs[2] = {nd.c0, nd.c1}, ns[2] = {nd.n0, nd.n1};
     for (int k = 0; k < 2; ++k) {
       if (ns[k] > 0) {
@@ -278,11 +289,32 @@ bool build_bvh(const double* v, const int32_t* f, int64_t nf, const BvhBuildPara
           *err = "BVH leaf out of range";
           return false;
         }
+        if (single && k == 1) continue;
+        for (int32_t i = cs[k]; i < cs[k] + ns[k]; ++i) {
+          if (seen[(size_t)i]) {
+            *err = "BVH leaves overlap";
+            return false;
+          }
+          seen[(size_t)i] = 1;
+          ++covered;
+        }
       } else if (cs[k] >= nn || cs[k] <= 0) {  // internal: never the root, never empty
         *err = "BVH child out of range";
         return false;
       }
     }
+  }
+  if (covered != nf || (int64_t)r.order.size() != nf) {
+    *err = "BVH leaves do not cover every face";
+    return false;
+  }
+  std::fill(seen.begin(), seen.end(), 0);
+  for (int32_t f : r.order) {
+    if (f < 0 || f >= nf || seen[(size_t)f]) {
+      *err = "BVH face order is not a permutation";
+      return false;
+    }
+    seen[(size_t)f] = 1;
   }
   return true;
 }

@@ -18,6 +18,7 @@
 #include <cstring>
 #include <memory>
 #include <mutex>
+#include <thread>
 #include <string>
 #include <vector>
 
@@ -62,10 +63,11 @@ struct DevBuf {
     n = count;
     return RT_OK;
   }
-  int upload(const std::vector<T>& h) {
-    int rc = alloc(h.size());
+  int upload(const std::vector<T>& h) { return upload(h.data(), h.size()); }
+  int upload(const T* h, size_t count) {
+    int rc = alloc(count);
     if (rc != RT_OK) return rc;
-    if (!h.empty()) HIP_TRY(hipMemcpy(p, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice));
+    if (count) HIP_TRY(hipMemcpy(p, h, count * sizeof(T), hipMemcpyHostToDevice));
     return RT_OK;
   }
   void release() {
@@ -297,6 +299,23 @@ namespace {
 
 bool affine(const double* m) { return m[3] == 0.0 && m[7] == 0.0 && m[11] == 0.0 && m[15] == 1.0; }
 
+// fn(begin, end) over [0, n) in contiguous chunks on up to 16 host threads
+// (scene setup of million-face meshes: per-face record packing).
+template <class Fn>
+void parallel_for(int64_t n, Fn fn) {
+  const int64_t kGrain = 1 << 15;
+  const int hw = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  const int nt = (int)std::min<int64_t>(hw, (n + kGrain - 1) / kGrain);
+  if (nt <= 1) {
+    if (n > 0) fn((int64_t)0, n);
+    return;
+  }
+  std::vector<std::thread> pool;
+  pool.reserve((size_t)nt);
+  for (int t = 0; t < nt; ++t) pool.emplace_back([=, &fn] { fn(n * t / nt, n * (t + 1) / nt); });
+  for (std::thread& th : pool) th.join();
+}
+
 // Identity / pure translation / general (float32 fast paths, DevObject.xf).
 // Translation requires BOTH matrices to have an identity 3x3 block, so the
 // normal transform (object_to_world * n) is the identity too.
@@ -317,7 +336,7 @@ void fill_precision(const rt_scene_desc* d, const std::vector<std::vector<double
                     const std::vector<BvhResult>& bvhs, const std::vector<int32_t>& node_base,
                     const std::vector<std::vector<double>>& aabbs, std::vector<DevObject<R>>& objs,
                     std::vector<DevLight<R>>& lights, std::vector<DevMesh<R>>& meshes,
-                    std::vector<typename TriOf<R>::type>& tris, std::vector<R>& nrm) {
+                    std::vector<typename TriOf<R>::type>* tris, std::vector<R>& nrm) {
   objs.assign((size_t)d->num_objects, DevObject<R>{});
   for (int i = 0; i < d->num_objects; ++i) {
     const rt_object_desc& s = d->objects[i];
@@ -348,8 +367,10 @@ void fill_precision(const rt_scene_desc* d, const std::vector<std::vector<double
     l.type = s.type == RT_POINT_LIGHT ? LIGHT_POINT : LIGHT_DISTANT;
   }
   meshes.assign((size_t)d->num_meshes, DevMesh<R>{});
-  tris.clear();
-  nrm.clear();
+  int64_t total = 0;
+  for (int m = 0; m < d->num_meshes; ++m) total += d->meshes[m].num_faces;
+  if (tris) tris->assign((size_t)total, typename TriOf<R>::type{});
+  nrm.resize((size_t)total * 3);
   int32_t normal_base = 0;
   for (int m = 0; m < d->num_meshes; ++m) {
     const rt_mesh_desc& md = d->meshes[m];
@@ -361,62 +382,40 @@ void fill_precision(const rt_scene_desc* d, const std::vector<std::vector<double
     dm.num_faces = (int32_t)md.num_faces;
     dm.normal_base = normal_base;
     dm.root = bvhs[(size_t)m].nodes.empty() ? -1 : node_base[(size_t)m];
-    const int32_t tri_base = (int32_t)tris.size();
-    (void)tri_base;
-    for (int32_t face : bvhs[(size_t)m].order) {
-      typename TriOf<R>::type t{};
-      const int32_t* fi = &md.faces[3 * (size_t)face];
-      const double* v0 = &md.vertices[3 * (size_t)fi[0]];
-      const double* v1 = &md.vertices[3 * (size_t)fi[1]];
-      const double* v2 = &md.vertices[3 * (size_t)fi[2]];
-      for (int k = 0; k < 3; ++k) {
-        t.v0[k] = (R)v0[k];
-        t.e1[k] = (R)(v1[k] - v0[k]);  // v0v1 exactly as geom.nim:286-288
-        t.e2[k] = (R)(v2[k] - v0[k]);  // v0v2 exactly as geom.nim:292-294
-      }
-      t.id = face;
-      tris.push_back(t);
+    const std::vector<int32_t>& order = bvhs[(size_t)m].order;
+    if (tris) {
+      typename TriOf<R>::type* out = tris->data() + normal_base;
+      parallel_for((int64_t)order.size(), [&](int64_t b, int64_t e) {
+        for (int64_t i = b; i < e; ++i) {
+          const int32_t face = order[(size_t)i];
+          typename TriOf<R>::type& t = out[i];
+          const int32_t* fi = &md.faces[3 * (size_t)face];
+          const double* v0 = &md.vertices[3 * (size_t)fi[0]];
+          const double* v1 = &md.vertices[3 * (size_t)fi[1]];
+          const double* v2 = &md.vertices[3 * (size_t)fi[2]];
+          for (int k = 0; k < 3; ++k) {
+            t.v0[k] = (R)v0[k];
+            t.e1[k] = (R)(v1[k] - v0[k]);  // v0v1 exactly as geom.nim:286-288
+            t.e2[k] = (R)(v2[k] - v0[k]);  // v0v2 exactly as geom.nim:292-294
+          }
+          t.id = face;
+        }
+      });
     }
-    for (double x : normals[(size_t)m]) nrm.push_back((R)x);
+    const std::vector<double>& src = normals[(size_t)m];
+    R* dst = nrm.data() + 3 * (size_t)normal_base;
+    parallel_for((int64_t)src.size(), [&](int64_t b, int64_t e) {
+      for (int64_t i = b; i < e; ++i) dst[i] = (R)src[(size_t)i];
+    });
     normal_base += (int32_t)md.num_faces;
   }
   // pad so a kernel may read kLeafMax records from any leaf start
-  for (int k = 0; k < kLeafMax - 1; ++k) {
-    typename TriOf<R>::type t{};
-    t.id = -1;
-    tris.push_back(t);
-  }
-}
-
-// float32 kernel triangles (rt_common.h TriFast) in BVH leaf order; edges and
-// the negated face normal formed in float64, then rounded once.
-void fill_fast_tris(const rt_scene_desc* d, const std::vector<BvhResult>& bvhs, std::vector<TriFast>& tris) {
-  tris.clear();
-  for (int m = 0; m < d->num_meshes; ++m) {
-    const rt_mesh_desc& md = d->meshes[m];
-    for (int32_t face : bvhs[(size_t)m].order) {
-      TriFast t{};
-      const int32_t* fi = &md.faces[3 * (size_t)face];
-      const double* v0 = &md.vertices[3 * (size_t)fi[0]];
-      const double* v1 = &md.vertices[3 * (size_t)fi[1]];
-      const double* v2 = &md.vertices[3 * (size_t)fi[2]];
-      double e1[3], e2[3];
-      for (int k = 0; k < 3; ++k) {
-        e1[k] = v1[k] - v0[k];
-        e2[k] = v2[k] - v0[k];
-      }
-      const double n[3] = {e1[1] * e2[2] - e1[2] * e2[1], e1[2] * e2[0] - e1[0] * e2[2],
-                           e1[0] * e2[1] - e1[1] * e2[0]};
-      for (int k = 0; k < 3; ++k) {
-        t.v0[k] = (float)v0[k];
-        t.e2[k] = (float)e2[k];
-        t.e1n[k] = (float)-e1[k];
-        t.nn[k] = (float)-n[k];
-      }
-      t.id = face;
-      tris.push_back(t);
+  if (tris)
+    for (int k = 0; k < kLeafMax - 1; ++k) {
+      typename TriOf<R>::type t{};
+      t.id = -1;
+      tris->push_back(t);
     }
-  }
 }
 
 // float32 kernel records (rt_common.h FObj/FObjX/FMesh/FLight).
@@ -478,6 +477,16 @@ extern "C" int rt_scene_create(const rt_scene_desc* d, rt_scene** out_scene) {
     return fail(RT_E_INVALID, "null array with nonzero count");
   if (!affine(d->camera_to_world)) return fail(RT_E_UNSUPPORTED, "camera_to_world is not affine");
   const auto t0 = std::chrono::steady_clock::now();
+  // RTMI_SETUP_PROFILE=1: per-phase wall times of scene setup on stderr
+  static const bool profile = std::getenv("RTMI_SETUP_PROFILE") != nullptr;
+  auto tp = t0;
+  const auto mark = [&](const char* phase) {
+    if (!profile) return;
+    const auto now = std::chrono::steady_clock::now();
+    std::fprintf(stderr, "[rtmi setup] %-22s %9.3f ms\n", phase,
+                 std::chrono::duration<double, std::milli>(now - tp).count());
+    tp = now;
+  };
   bool any_reflective = false;
   for (int i = 0; i < d->num_objects; ++i) {
     const rt_object_desc& o = d->objects[i];
@@ -491,8 +500,28 @@ extern "C" int rt_scene_create(const rt_scene_desc* d, rt_scene** out_scene) {
   for (int i = 0; i < d->num_lights; ++i)
     if (d->lights[i].type != RT_DISTANT_LIGHT && d->lights[i].type != RT_POINT_LIGHT)
       return fail(RT_E_INVALID, "light %d: bad type", i);
+  if (d->bvh_builder != RT_BVH_SAH && d->bvh_builder != RT_BVH_PLOC)
+    return fail(RT_E_INVALID, "bad bvh_builder %d", d->bvh_builder);
+  int dev = device_of_current();
+  if (dev < 0 || rt_device_count() <= 0) return fail(RT_E_DEVICE, "no HIP device (call rt_init)");
+  hipDeviceProp_t prop;
+  HIP_TRY(hipGetDeviceProperties(&prop, dev));
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+    return fail(RT_E_DEVICE, "device %d is %s; librtmi.so is built for gfx950 only", dev, prop.gcnArchName);
   std::vector<std::vector<double>> normals((size_t)d->num_meshes), aabbs((size_t)d->num_meshes);
   std::vector<BvhResult> bvhs((size_t)d->num_meshes);
+  // device copies of every mesh's arrays: the device builder and the
+  // triangle-record packing (rt_bvh_gpu.hip) read them
+  std::vector<DevBuf<double>> d_verts((size_t)d->num_meshes);
+  std::vector<DevBuf<int32_t>> d_faces((size_t)d->num_meshes);
+  struct FreeAll {
+    std::vector<DevBuf<double>>& v;
+    std::vector<DevBuf<int32_t>>& f;
+    ~FreeAll() {
+      for (auto& b : v) b.release();
+      for (auto& b : f) b.release();
+    }
+  } free_all{d_verts, d_faces};
   std::vector<int32_t> node_base((size_t)d->num_meshes, 0);
   int64_t ntri = 0, nnodes = 0;
   int maxdepth = 0;
@@ -507,7 +536,8 @@ extern "C" int rt_scene_create(const rt_scene_desc* d, rt_scene** out_scene) {
     // face normals: given, or calcNormals (src/loaders/obj.nim:65-84)
     std::vector<double>& nr = normals[(size_t)m];
     nr.resize((size_t)md.num_faces * 3);
-    for (int64_t fidx = 0; fidx < md.num_faces; ++fidx) {
+    parallel_for(md.num_faces, [&](int64_t fb, int64_t fe) {
+    for (int64_t fidx = fb; fidx < fe; ++fidx) {
       if (md.normals) {
         for (int k = 0; k < 3; ++k) nr[3 * (size_t)fidx + k] = md.normals[3 * fidx + k];
         continue;
@@ -527,6 +557,7 @@ extern "C" int rt_scene_create(const rt_scene_desc* d, rt_scene** out_scene) {
       nr[3 * (size_t)fidx + 1] = cy / len;
       nr[3 * (size_t)fidx + 2] = cz / len;
     }
+    });
     // calcAABB (geom.nim:175-188) over every vertex
     std::vector<double>& bb = aabbs[(size_t)m];
     bb = {INFINITY, INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY};
@@ -536,10 +567,20 @@ extern "C" int rt_scene_create(const rt_scene_desc* d, rt_scene** out_scene) {
         if (x < bb[(size_t)k]) bb[(size_t)k] = x;
         if (x > bb[3 + (size_t)k]) bb[3 + (size_t)k] = x;
       }
+    mark("normals + bounds");
+    int urc;
+    if ((urc = d_verts[(size_t)m].upload(md.vertices, (size_t)md.num_vertices * 3)) ||
+        (urc = d_faces[(size_t)m].upload(md.faces, (size_t)md.num_faces * 3)))
+      return urc;
+    mark("mesh upload");
     const char* err = "BVH build failed";
     BvhBuildParams prm;
-    if (!build_bvh(md.vertices, md.faces, md.num_faces, prm, &bvhs[(size_t)m], &err))
-      return fail(RT_E_INVALID, "mesh %d: %s", m, err);
+    const bool ok = d->bvh_builder == RT_BVH_PLOC
+                        ? build_bvh_device(d_verts[(size_t)m].p, d_faces[(size_t)m].p, md.num_faces, prm,
+                                           &bvhs[(size_t)m], &err)
+                        : build_bvh(md.vertices, md.faces, md.num_faces, prm, &bvhs[(size_t)m], &err);
+    if (!ok) return fail(d->bvh_builder == RT_BVH_PLOC ? RT_E_DEVICE : RT_E_INVALID, "mesh %d: %s", m, err);
+    mark("bvh build");
     node_base[(size_t)m] = (int32_t)all_nodes.size();
     for (BvhNode nd : bvhs[(size_t)m].nodes) {
       if (nd.n0 == 0 && nd.c0 >= 0) nd.c0 += node_base[(size_t)m];
@@ -554,12 +595,6 @@ extern "C" int rt_scene_create(const rt_scene_desc* d, rt_scene** out_scene) {
   }
   if (ntri > INT32_MAX / 2) return fail(RT_E_UNSUPPORTED, "too many triangles");
 
-  int dev = device_of_current();
-  if (dev < 0 || rt_device_count() <= 0) return fail(RT_E_DEVICE, "no HIP device (call rt_init)");
-  hipDeviceProp_t prop;
-  HIP_TRY(hipGetDeviceProperties(&prop, dev));
-  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
-    return fail(RT_E_DEVICE, "device %d is %s; librtmi.so is built for gfx950 only", dev, prop.gcnArchName);
 
   std::unique_ptr<rt_scene> s(new rt_scene());
   s->device = dev;
@@ -599,11 +634,9 @@ extern "C" int rt_scene_create(const rt_scene_desc* d, rt_scene** out_scene) {
     std::vector<DevObject<float>> o;
     std::vector<DevLight<float>> l;
     std::vector<DevMesh<float>> m;
-    std::vector<TriF32> t32;
     std::vector<float> n;
-    fill_precision<float>(d, normals, bvhs, node_base, aabbs, o, l, m, t32, n);
-    std::vector<TriFast> t;
-    fill_fast_tris(d, bvhs, t);
+    fill_precision<float>(d, normals, bvhs, node_base, aabbs, o, l, m, nullptr, n);
+    mark("fp32 records");
     std::vector<FObj> fo;
     std::vector<FObjX> fx;
     std::vector<FMesh> fm;
@@ -611,21 +644,49 @@ extern "C" int rt_scene_create(const rt_scene_desc* d, rt_scene** out_scene) {
     fill_fast_records(d, m, fo, fx, fm, fl);
     int rc;
     if ((rc = s->f32.objs.upload(fo)) || (rc = s->f32.objx.upload(fx)) || (rc = s->f32.meshes.upload(fm)) ||
-        (rc = s->f32.lights.upload(fl)) || (rc = s->f32.tris.upload(t)) || (rc = s->f32.normals.upload(n)))
+        (rc = s->f32.lights.upload(fl)) || (rc = s->f32.normals.upload(n)))
       return rc;
+    mark("fp32 upload");
   }
   {
     std::vector<DevObject<double>> o;
     std::vector<DevLight<double>> l;
     std::vector<DevMesh<double>> m;
-    std::vector<TriF64> t;
     std::vector<double> n;
-    fill_precision<double>(d, normals, bvhs, node_base, aabbs, o, l, m, t, n);
+    fill_precision<double>(d, normals, bvhs, node_base, aabbs, o, l, m, nullptr, n);
+    mark("fp64 records");
     int rc;
     if ((rc = s->f64.objects.upload(o)) || (rc = s->f64.lights.upload(l)) || (rc = s->f64.meshes.upload(m)) ||
-        (rc = s->f64.tris.upload(t)) || (rc = s->f64.normals.upload(n)))
+        (rc = s->f64.normals.upload(n)))
       return rc;
   }
+  mark("fp64 upload");
+  {
+    // triangle records in BVH leaf order, packed on the device; the float64
+    // array carries kLeafMax - 1 padding records (id -1) so a kernel may
+    // read kLeafMax records from any leaf start
+    int rc;
+    if ((rc = s->f32.tris.alloc((size_t)ntri)) || (rc = s->f64.tris.alloc((size_t)ntri + kLeafMax - 1))) return rc;
+    std::vector<TriF64> pad((size_t)kLeafMax - 1);
+    for (TriF64& t : pad) {
+      std::memset(&t, 0, sizeof t);
+      t.id = -1;
+    }
+    HIP_TRY(hipMemcpy(s->f64.tris.p + ntri, pad.data(), pad.size() * sizeof(TriF64), hipMemcpyHostToDevice));
+    int64_t base = 0;
+    for (int m = 0; m < d->num_meshes; ++m) {
+      const int64_t nf = d->meshes[m].num_faces;
+      DevBuf<int32_t> order;
+      if ((rc = order.upload(bvhs[(size_t)m].order))) return rc;
+      const bool ok = pack_triangles_device(d_verts[(size_t)m].p, d_faces[(size_t)m].p, order.p, nf,
+                                            s->f32.tris.p + base, s->f64.tris.p + base, s->stream);
+      HIP_TRY(hipStreamSynchronize(s->stream));
+      order.release();
+      if (!ok) return fail(RT_E_DEVICE, "mesh %d: triangle packing failed", m);
+      base += nf;
+    }
+  }
+  mark("triangle packing");
   int rc = s->nodes.upload(all_nodes);
   if (rc) return rc;
   s->max_waves = s->num_cus * 8 * 4;  // 8 blocks of 4 waves per CU at most
@@ -634,6 +695,7 @@ extern "C" int rt_scene_create(const rt_scene_desc* d, rt_scene** out_scene) {
   if ((rc = s->queue.alloc((size_t)kQueueShards * kQueueStride))) return rc;
   HIP_TRY(hipMemset(s->acc.p, 0, kStatSlots * sizeof(unsigned long long)));
   HIP_TRY(hipDeviceSynchronize());
+  mark("nodes + buffers");
   s->num_triangles = ntri;
   s->num_nodes = nnodes;
   s->max_depth = maxdepth;

@@ -21,6 +21,8 @@ RT_FP32, RT_FP64 = 0, 1
 RT_FLAG_ANYHIT_SHADOWS = 0x1
 RT_FLAG_COUNT_TRAVERSAL = 0x2
 RT_FLAG_NO_REORDER = 0x4
+RT_BVH_SAH = 0
+RT_BVH_PLOC = 1
 
 _d16 = C.c_double * 16
 _d3 = C.c_double * 3
@@ -69,7 +71,7 @@ class rt_scene_desc(C.Structure):
         ("lights", C.POINTER(rt_light_desc)),
         ("meshes", C.POINTER(rt_mesh_desc)),
         ("num_meshes", C.c_int32),
-        ("reserved", C.c_int32),
+        ("bvh_builder", C.c_int32),
         ("fov", C.c_double),
         ("camera_to_world", _d16),
         ("bg_color", _d3),

@@ -29,11 +29,14 @@ def device_count():
 class DeviceScene:
     """A Scene resident in HBM on one GPU (objects, lights, BVH, triangles)."""
 
-    def __init__(self, scene: Scene, device=0):
+    def __init__(self, scene: Scene, device=0, bvh_builder=abi.RT_BVH_SAH):
+        """bvh_builder: abi.RT_BVH_SAH (host binned SAH, default) or
+        abi.RT_BVH_PLOC (built on the GPU); images and Stats are the same."""
         initRenderer(device)
         self.device = device
         self.scene = scene
         flat = flatten(scene)
+        flat.desc.bvh_builder = int(bvh_builder)
         h = C.c_void_p()
         check(lib().rt_scene_create(C.byref(flat.desc), C.byref(h)))
         self.h = h
