@@ -12,7 +12,7 @@ import os
 import sys
 
 
-def means(path, kernel="k_render_fast<false>"):
+def means(path, kernel="k_render_fast<false"):
     agg = collections.defaultdict(float)
     for r in csv.DictReader(open(path)):
         if kernel not in r["Kernel_Name"]:
