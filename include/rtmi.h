@@ -262,6 +262,64 @@ int rt_unshard_bands_device(const float *d_gathered, float *d_fb,
 int rt_band_rows(int32_t height, int32_t band_h, int32_t world,
                  int32_t *out_rows);
 
+/* ---- render queue (workerpool.nim WorkerPool[WorkMsg, ResponseMsg]) ---- */
+
+/* The pool raytracer.nim and gui.nim drive (src/concurrency/workerpool.nim;
+ * WorkMsg / ResponseMsg, src/raytracer.nim:13-32; gui.nim:98-122,206-280),
+ * over the GPU: one host thread per queue takes the longest run of queued
+ * lines that share options, framebuffer, step and max_step and follow each
+ * other at `step`, and renders it with ONE rt_render_lines call (one launch
+ * per refinement level when the caller queues a whole level, as gui.nim
+ * does). Every message gets its own response, in queue order; a run's Stats
+ * ride on its last line's response, the others carry zero Stats (callers sum
+ * them). States and return values follow workerpool.nim; every command has
+ * completed when it returns, so the queue is always ready (isReady). The
+ * queue must be destroyed before its scene. */
+typedef struct rt_queue rt_queue;
+
+typedef enum rt_queue_state_kind {
+  RT_QUEUE_STOPPED = 0, /* wsStopped: work is queued, not started */
+  RT_QUEUE_RUNNING = 1, /* wsRunning                             */
+  RT_QUEUE_SHUTDOWN = 2 /* wsShutdown: no more work accepted       */
+} rt_queue_state_kind;
+
+typedef struct rt_response { /* ResponseMsg (raytracer.nim:21-23) + the line */
+  int32_t line;
+  int32_t status;            /* RT_OK, or the render call's error code    */
+  rt_stats stats;
+  char error[128];           /* rt_last_error() text when status != 0     */
+} rt_response;
+
+/* initRenderWorkers (raytracer.nim:35-38); starts stopped. */
+int rt_queue_create(rt_scene *scene, rt_queue **out);
+/* start / stop (workerpool.nim:253-275): 1 done, 0 not in the required
+ * state (stopped / running). stop lets the batch in flight finish and
+ * keeps queued lines queued. */
+int rt_queue_start(rt_queue *q);
+int rt_queue_stop(rt_queue *q);
+int rt_queue_state(rt_queue *q);    /* rt_queue_state_kind, or < 0 */
+int rt_queue_is_ready(rt_queue *q); /* 1 */
+/* queueWork (workerpool.nim:235): renderLine(line, step, maxStep) into the
+ * caller's host framebuffer fb (fb_w*fb_h*3 floats, written by the queue's
+ * thread until the line's response arrives); step / max_step 0 mean 1
+ * (raytracer.nim:26-27). */
+int rt_queue_work(rt_queue *q, const rt_options *opts, float *fb,
+                  int32_t fb_w, int32_t fb_h, int32_t line, int32_t step,
+                  int32_t max_step);
+/* tryRecvResult (workerpool.nim:240): 1 and *out filled, or 0 if no
+ * response is waiting. A failed line's message is also set as this
+ * thread's rt_last_error(). */
+int rt_queue_try_recv(rt_queue *q, rt_response *out);
+/* Lines queued or in flight. */
+int rt_queue_pending(rt_queue *q);
+/* reset (workerpool.nim:285-314): stop, drop queued work and undelivered
+ * responses; 1 done, 0 after shutdown. */
+int rt_queue_reset(rt_queue *q);
+/* shutdown (workerpool.nim:359): 1 done, 0 if already shut down. */
+int rt_queue_shutdown(rt_queue *q);
+/* close (workerpool.nim:371) + free, from any state. */
+int rt_queue_destroy(rt_queue *q);
+
 /* ---- output (framebuf.nim:55-93 writePpm) ------------------------------ */
 
 /* The P6 payload of writePpm for a device framebuffer (width*height*3
@@ -280,6 +338,16 @@ int64_t rt_ppm_payload_bytes(int32_t width, int32_t height, int32_t bits);
  * its length (excluding the NUL), or < 0 if buf_len is too small. */
 int rt_ppm_header(int32_t width, int32_t height, int32_t bits, char *buf,
                   int32_t buf_len);
+
+/* ImageRGBA.copyFrom (src/utils/image.nim:45-54) as a GPU post-pass: the
+ * width*height*3 float32 device framebuffer -> width*height RGBA8 pixels at
+ * d_out (device memory, 4-B aligned), round(c * 0xff).uint8 per component
+ * and `alpha`, for the GUI's texture upload without a float32 round trip.
+ * No clamp, like the reference: components outside [0, 255] after rounding
+ * keep the low 8 bits of the x86-64 int32 conversion (the reference's
+ * release build). Asynchronous on `stream`. */
+int rt_rgba_encode_device(const float *d_fb, int32_t width, int32_t height,
+                          uint8_t alpha, void *d_out, void *stream);
 
 /* Traversal counters of the last render call on this scene (waits for it).
  * Zero unless that call set RT_FLAG_COUNT_TRAVERSAL. */

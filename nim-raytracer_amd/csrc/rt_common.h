@@ -233,6 +233,9 @@ int rtmi_launch_render_f32(const rtmi::FastParams* p, unsigned subset, int block
 int rtmi_launch_render_f64(const rtmi::RenderParams<double>* p, int blocks, void* stream);
 int rtmi_render_f32_blocks_per_cu(int count, unsigned subset, size_t shmem);
 int rtmi_launch_ppm_encode(const float* fb, long long n, int bits, int srgb, void* out, void* stream);
+int rtmi_launch_rgba_encode(const float* fb, long long npix, unsigned int alpha, void* out, void* stream);
+// Sets this thread's rt_last_error() text; returns code (rtmi.cpp).
+int rtmi_fail_msg(int code, const char* msg);
 int rtmi_launch_reduce_stats(const unsigned long long* partials, int num_waves,
                              unsigned long long* acc, void* stream);
 int rtmi_launch_unshard(const float* gathered, float* fb, int width, int height, int band_h,

@@ -51,7 +51,33 @@ __global__ __launch_bounds__(256) void k_ppm_encode(const float* __restrict__ fb
   }
 }
 
+// ImageRGBA.copyFrom (src/utils/image.nim:45-54): round(c * 0xff).uint8 per
+// component, no clamp (oracle_rgba_component: out-of-range keeps the low 8
+// bits of the x86 int32 conversion, NaN -> INT32_MIN), alpha constant. One
+// pixel per thread: three float loads, one 4-byte store.
+__device__ __forceinline__ unsigned int rgba_component(float v) {
+  const float r = roundf(v * 255.0f);
+  const int i = (r >= -2147483648.0f && r < 2147483648.0f) ? (int)r : (int)0x80000000u;
+  return (unsigned int)i & 0xffu;
+}
+
+__global__ __launch_bounds__(256) void k_rgba_encode(const float* __restrict__ fb, long long npix, unsigned int alpha,
+                                                     unsigned int* __restrict__ out) {
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < npix; i += stride) {
+    const float* c = fb + 3 * i;
+    out[i] = rgba_component(c[0]) | (rgba_component(c[1]) << 8) | (rgba_component(c[2]) << 16) | (alpha << 24);
+  }
+}
+
 }  // namespace rtmi
+
+extern "C" int rtmi_launch_rgba_encode(const float* fb, long long npix, unsigned int alpha, void* out, void* stream) {
+  const int blocks = (int)(npix < 256LL * 2048 ? (npix + 255) / 256 : 2048);
+  hipLaunchKernelGGL(rtmi::k_rgba_encode, dim3(blocks > 0 ? blocks : 1), dim3(256), 0, (hipStream_t)stream, fb, npix,
+                     alpha & 0xffu, (unsigned int*)out);
+  return (int)hipGetLastError();
+}
 
 extern "C" int rtmi_launch_ppm_encode(const float* fb, long long n, int bits, int srgb, void* out, void* stream) {
   const long long n4 = (n + 3) / 4;

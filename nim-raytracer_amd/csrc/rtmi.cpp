@@ -180,6 +180,8 @@ struct rt_scene {
   }
 };
 
+int rtmi_fail_msg(int code, const char* msg) { return fail(code, "%s", msg ? msg : ""); }
+
 extern "C" {
 
 int rt_version(void) { return RTMI_ABI_VERSION; }
@@ -1276,6 +1278,17 @@ extern "C" int rt_ppm_encode_device(const float* d_fb, int32_t width, int32_t he
   if (((uintptr_t)d_fb & 15) || ((uintptr_t)d_out & 7)) return fail(RT_E_INVALID, "buffers must be 16-B (fb) / 8-B (out) aligned");
   const int e = rtmi_launch_ppm_encode(d_fb, (long long)width * height * 3, bits, srgb ? 1 : 0, d_out, stream);
   if (e) return fail(RT_E_DEVICE, "ppm encode launch failed: %s", hipGetErrorString((hipError_t)e));
+  return RT_OK;
+}
+
+extern "C" int rt_rgba_encode_device(const float* d_fb, int32_t width, int32_t height, uint8_t alpha, void* d_out,
+                                     void* stream) {
+  if (!d_fb || !d_out) return fail(RT_E_INVALID, "null buffer");
+  if (width <= 0 || height <= 0 || width > 65536 || height > 65536)
+    return fail(RT_E_INVALID, "bad image size %dx%d", width, height);
+  if (((uintptr_t)d_fb & 3) || ((uintptr_t)d_out & 3)) return fail(RT_E_INVALID, "buffers must be 4-B aligned");
+  const int e = rtmi_launch_rgba_encode(d_fb, (long long)width * height, alpha, d_out, stream);
+  if (e) return fail(RT_E_DEVICE, "rgba encode launch failed: %s", hipGetErrorString((hipError_t)e));
   return RT_OK;
 }
 

@@ -106,6 +106,18 @@ class rt_stats(C.Structure):
         return {f: int(getattr(self, f)) for f, _ in self._fields_}
 
 
+class rt_response(C.Structure):
+    _fields_ = [
+        ("line", C.c_int32),
+        ("status", C.c_int32),
+        ("stats", rt_stats),
+        ("error", C.c_char * 128),
+    ]
+
+
+RT_QUEUE_STOPPED, RT_QUEUE_RUNNING, RT_QUEUE_SHUTDOWN = 0, 1, 2
+
+
 class rt_traversal_counters(C.Structure):
     _fields_ = [
         ("wave_node_fetches", C.c_uint64),
@@ -159,7 +171,20 @@ SIGNATURES = {
     "rt_load_geom": (C.c_int, [C.c_char_p, C.POINTER(C.c_int64), C.POINTER(C.c_double)]),
     "rt_ppm_encode_device": (C.c_int, [_P, C.c_int32, C.c_int32, C.c_int32, C.c_int32, _P, _P]),
     "rt_ppm_payload_bytes": (C.c_int64, [C.c_int32, C.c_int32, C.c_int32]),
+    "rt_rgba_encode_device": (C.c_int, [_P, C.c_int32, C.c_int32, C.c_uint8, _P, _P]),
     "rt_ppm_header": (C.c_int, [C.c_int32, C.c_int32, C.c_int32, C.c_char_p, C.c_int32]),
+    "rt_queue_create": (C.c_int, [_P, C.POINTER(_P)]),
+    "rt_queue_start": (C.c_int, [_P]),
+    "rt_queue_stop": (C.c_int, [_P]),
+    "rt_queue_state": (C.c_int, [_P]),
+    "rt_queue_is_ready": (C.c_int, [_P]),
+    "rt_queue_work": (C.c_int, [_P, C.POINTER(rt_options), C.POINTER(C.c_float), C.c_int32, C.c_int32,
+                                C.c_int32, C.c_int32, C.c_int32]),
+    "rt_queue_try_recv": (C.c_int, [_P, C.POINTER(rt_response)]),
+    "rt_queue_pending": (C.c_int, [_P]),
+    "rt_queue_reset": (C.c_int, [_P]),
+    "rt_queue_shutdown": (C.c_int, [_P]),
+    "rt_queue_destroy": (C.c_int, [_P]),
 }
 
 

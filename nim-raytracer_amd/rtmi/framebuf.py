@@ -55,6 +55,28 @@ def to_uint(data, bits=8, sRGB=True):
     return r.astype(np.uint16 if bits > 8 else np.uint8)
 
 
+def to_rgba(data, alpha=0xFF):
+    """ImageRGBA.copyFrom (src/utils/image.nim:45-54): (h, w, 3) float32 ->
+    (h, w, 4) uint8, round(c * 0xff) as a float32 product rounded half away
+    from zero, no clamp; out-of-range results keep the low 8 bits of the
+    x86-64 int32 conversion (NaN and |x| >= 2^31 -> INT32_MIN), as the
+    reference's release build does (oracle_rgba_component)."""
+    x = np.asarray(data, dtype=np.float32) * np.float32(255.0)
+    with np.errstate(invalid="ignore"):
+        a = np.abs(x)
+        r = np.floor(a)
+        r = r + (a - r >= np.float32(0.5))
+        r = np.copysign(r, x)
+        ok = (r >= -2147483648.0) & (r < 2147483648.0)
+        i = np.where(ok, r, -2147483648.0).astype(np.int64)
+    q = (i & 0xFF).astype(np.uint8)
+    h, w = q.shape[0], q.shape[1]
+    out = np.empty((h, w, 4), np.uint8)
+    out[..., :3] = q
+    out[..., 3] = alpha
+    return out
+
+
 def writePpm(data, filename, bits=8, sRGB=True):
     """P6 writer of framebuf.nim:55-93 (8-bit or big-endian 16-bit)."""
     data = np.asarray(data)

@@ -145,6 +145,109 @@ def ppm_encode_device(d_fb, width, height, bits=8, sRGB=True, stream=None):
     return buf.raw[:hl], out
 
 
+class ResponseMsg:
+    """ResponseMsg (raytracer.nim:21-23) plus the line it answers."""
+
+    def __init__(self, line, stats):
+        self.line = line
+        self.stats = stats
+
+
+class RenderQueue:
+    """WorkerPool[WorkMsg, ResponseMsg] (src/concurrency/workerpool.nim) as
+    raytracer.nim / gui.nim drive it, over the GPU (rt_queue_*): queued
+    lines that form a run at one step become one launch; every line gets its
+    response; a run's Stats ride on its last response (callers sum them)."""
+
+    numActiveWorkers = 1  # one device "worker"; the pool size has no GPU meaning
+    poolSize = 1
+
+    def __init__(self, ds: DeviceScene):
+        self.ds = ds
+        h = C.c_void_p()
+        check(lib().rt_queue_create(ds.h, C.byref(h)))
+        self.h = h
+        self._fbs = {}  # framebuffers the queue's thread may still write
+
+    def state(self):
+        return lib().rt_queue_state(self.h)
+
+    def isReady(self):
+        return lib().rt_queue_is_ready(self.h) == 1
+
+    def waitForReady(self, timeout=1):
+        """Commands complete before they return: always ready."""
+
+    def start(self):
+        return lib().rt_queue_start(self.h) == 1
+
+    def stop(self):
+        return lib().rt_queue_stop(self.h) == 1
+
+    def queueWork(self, opts: Options, framebuf, line, step=0, maxStep=0):
+        """WorkMsg{opts, framebuf, line, step, maxStep}: framebuf is the
+        (h, w, 3) float32 array the line is rendered into."""
+        if not (isinstance(framebuf, np.ndarray) and framebuf.dtype == np.float32 and framebuf.flags.c_contiguous
+                and framebuf.shape == (opts.height, opts.width, 3)):
+            raise ValueError("framebuf must be a C-contiguous float32 array of shape (height, width, 3)")
+        o = opts.to_c()
+        check(lib().rt_queue_work(self.h, C.byref(o), framebuf.ctypes.data_as(C.POINTER(C.c_float)),
+                                  opts.width, opts.height, int(line), int(step), int(maxStep)))
+        self._fbs[framebuf.ctypes.data] = framebuf
+
+    def tryRecvResult(self):
+        """(available, ResponseMsg); a failed line raises RtmiError."""
+        r = abi.rt_response()
+        n = lib().rt_queue_try_recv(self.h, C.byref(r))
+        if n < 0:
+            raise RtmiError(n, lib().rt_last_error().decode())
+        if n == 0:
+            return False, None
+        if r.status != 0:
+            raise RtmiError(r.status, r.error.decode(errors="replace"))
+        if lib().rt_queue_pending(self.h) == 0:
+            self._fbs.clear()
+        return True, ResponseMsg(r.line, Stats.from_c(r.stats))
+
+    def reset(self):
+        return lib().rt_queue_reset(self.h) == 1
+
+    def shutdown(self):
+        return lib().rt_queue_shutdown(self.h) == 1
+
+    def close(self):
+        """workerpool.nim close: only after shutdown."""
+        if self.h is None or self.state() != abi.RT_QUEUE_SHUTDOWN:
+            return False
+        check(lib().rt_queue_destroy(self.h))
+        self.h = None
+        self._fbs.clear()
+        return True
+
+    def __del__(self):
+        try:
+            if self.h is not None:
+                lib().rt_queue_destroy(self.h)
+                self.h = None
+        except Exception:
+            pass
+
+
+def initRenderWorkers(ds: DeviceScene, numActiveWorkers=0, poolSize=0):
+    """initRenderWorkers (raytracer.nim:35-38) -> a RenderQueue."""
+    return RenderQueue(ds)
+
+
+def rgba_encode_device(d_fb, width, height, alpha=0xFF, stream=None):
+    """ImageRGBA.copyFrom (image.nim:45-54) of a device framebuffer on the
+    GPU; returns a (height, width, 4) uint8 CUDA tensor."""
+    import torch
+    out = torch.empty((int(height), int(width), 4), dtype=torch.uint8, device=d_fb.device)
+    check(lib().rt_rgba_encode_device(C.c_void_p(_ptr(d_fb, width * height * 3)), int(width), int(height),
+                                      int(alpha) & 0xFF, C.c_void_p(int(out.data_ptr())), _stream(stream)))
+    return out
+
+
 def write_ppm_device(d_fb, width, height, filename, bits=8, sRGB=True, stream=None):
     """Framebuf.writePpm for a device framebuffer: the quantisation runs on
     the GPU and only the 8/16-bit payload crosses PCIe."""

@@ -64,6 +64,8 @@ def _load():
     lib.oracle_calc_pixel.restype = None
     lib.oracle_calc_pixel.argtypes = [P, C.POINTER(abi.rt_options), C.c_int32, C.c_int32, dp,
                                       C.POINTER(abi.rt_stats)]
+    lib.oracle_rgba_component.restype = C.c_uint8
+    lib.oracle_rgba_component.argtypes = [C.c_float]
     lib.oracle_ppm_outvalue.restype = C.c_int32
     lib.oracle_ppm_outvalue.argtypes = [C.c_float, C.c_int32, C.c_int32]
     return lib
@@ -189,6 +191,11 @@ def aabb_intersect(vmin, vmax, orig, dir):
 def sphere_intersect(r, orig, dir):
     (oa, op), (da, dpp) = _dp(orig), _dp(dir)
     return lib().oracle_sphere_intersect(r, op, dpp)
+
+
+def rgba_component(v):
+    """ImageRGBA.copyFrom's component (image.nim:45-54), oracle_rgba_component."""
+    return lib().oracle_rgba_component(float(v))
 
 
 def ppm_outvalue(v, bits=8, srgb=True):

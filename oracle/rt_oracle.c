@@ -951,6 +951,19 @@ int32_t oracle_trace(const oracle_scene *s, const double orig[4], const double d
 }
 
 /* linearToSRGB (color.nim:17-22) + writePpm.outvalue (framebuf.nim:74-78). */
+uint8_t oracle_rgba_component(float v) {
+  /* image.nim:51-53: round(fb.data[i] * 0xff).uint8 — a float32 product
+   * (the literal converts to float32), Nim round on float32 (roundf), then
+   * the uint8 conversion. No clamp: for results outside [0, 255] the
+   * reference either raises (range checks on) or, in a release build on
+   * x86-64, keeps the low 8 bits of the int32 conversion (cvttss2si: NaN and
+   * |x| >= 2^31 give INT32_MIN). That release behaviour is restated here;
+   * no reference test pins it. */
+  const float r = roundf(v * 255.0f);
+  const int32_t i = (r >= -2147483648.0f && r < 2147483648.0f) ? (int32_t)r : INT32_MIN;
+  return (uint8_t)((uint32_t)i & 0xffu);
+}
+
 int32_t oracle_ppm_outvalue(float v, int32_t bits, int32_t srgb) {
   /* maxval = float32(2^bits - 1) (framebuf.nim:58); c = clamp(v, 0, 1) is
    * float32; linearToSRGB (color.nim:17-22) evaluates in float64 (its `a` is

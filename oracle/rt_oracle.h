@@ -70,6 +70,8 @@ void oracle_calc_pixel(const oracle_scene *s, const rt_options *o, int32_t x,
 /* linearToSRGB (color.nim:17-22) + writePpm's outvalue (framebuf.nim:64-68)
  * for one component: clamp, optional sRGB, round(c * maxval). */
 int32_t oracle_ppm_outvalue(float v, int32_t bits, int32_t srgb);
+/* ImageRGBA.copyFrom's per-component value (src/utils/image.nim:45-54). */
+uint8_t oracle_rgba_component(float v);
 
 #ifdef __cplusplus
 }

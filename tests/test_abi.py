@@ -136,6 +136,9 @@ def test_scene_create_validates_before_touching_a_device():
     flat = flatten(scenes.spheres_warm(3))
     flat._objs[1].object_to_world[3] = 0.5  # projective row: unsupported
     assert L.rt_scene_create(C.byref(flat.desc), C.byref(h)) == abi.RT_E_UNSUPPORTED
+    flat = flatten(scenes.mesh_bunny())
+    flat.desc.bvh_builder = 9
+    assert L.rt_scene_create(C.byref(flat.desc), C.byref(h)) == abi.RT_E_INVALID
     assert not h.value
 
 
@@ -155,6 +158,22 @@ def test_ppm_header_and_sizes():
     assert L.rt_ppm_payload_bytes(1920, 1080, 8) == 1920 * 1080 * 3
     assert L.rt_ppm_payload_bytes(3, 5, 16) == 3 * 5 * 6
     assert L.rt_ppm_payload_bytes(3, 5, 0) < 0 and L.rt_ppm_payload_bytes(3, 5, 17) < 0
+
+
+def test_rgba_copy_matches_oracle(oracle_mod):
+    """rtmi.framebuf.to_rgba (ImageRGBA.copyFrom, image.nim:45-54; the GPU
+    pass's reference) equals the oracle's component on edge and random
+    values, including the unclamped out-of-range cases."""
+    from rtmi.framebuf import to_rgba
+    rng = np.random.default_rng(11)
+    v = np.concatenate([rng.random(20000).astype(np.float32) * 1.6 - 0.3,
+                        np.array([0.0, -0.0, 0.5 / 255, 1.5 / 255, 254.5 / 255, 1.0, 1.002, 1.5, 2.0, -0.5 / 255,
+                                  -0.3, 255.0, 1e7, -1e7, 1e30, -1e30, np.inf, -np.inf, np.nan], np.float32)])
+    img = to_rgba(v.reshape(1, -1, 1).repeat(3, axis=2), alpha=0x7F)
+    o = np.array([oracle_mod.rgba_component(float(x)) for x in v], np.uint8)
+    assert np.array_equal(img[0, :, 0], o)
+    assert np.array_equal(img[0, :, 2], o)
+    assert (img[..., 3] == 0x7F).all()
 
 
 def test_ppm_quantisation_matches_oracle(oracle_mod):

@@ -28,6 +28,24 @@ def test_ppm_encode_exact(gpu, bits, srgb, w, h):
     assert np.array_equal(got, want)
 
 
+@pytest.mark.parametrize("w,h", [(64, 48), (7, 3), (1, 1)])
+def test_rgba_encode_exact(gpu, w, h):
+    """ImageRGBA.copyFrom on the GPU (rt_rgba_encode_device) byte-exact
+    against the host mirror, which test_abi.py pins to the oracle."""
+    import torch
+
+    from rtmi.framebuf import to_rgba
+    from rtmi.renderer import rgba_encode_device
+    rng = np.random.default_rng(w * 7 + h)
+    data = (rng.random((h, w, 3)) * 1.6 - 0.3).astype(np.float32)
+    flat = data.reshape(-1)
+    specials = np.array([0.5 / 255, 254.5 / 255, 1.0, np.nan, np.inf, -1e30, 2.0, -0.0, 1e7], np.float32)
+    flat[:min(len(specials), flat.size)] = specials[:flat.size]
+    out = rgba_encode_device(torch.from_numpy(flat).cuda(), w, h, alpha=0xC8)
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy(), to_rgba(data, 0xC8))
+
+
 def test_write_ppm_device_matches_host_writer(gpu, tmp_path):
     import torch
 
