@@ -365,6 +365,25 @@ int rt_mat4_inverse(const double m[16], double out[16]);
  * buffer of num_triangles*9 doubles. */
 int rt_load_geom(const char *path, int64_t *num_triangles, double *vertices);
 
+/* OBJ reader of src/loaders/obj.nim:87-126: "v x y z" and "f a b c" lines
+ * (1-based indices; a 4th face vertex is ignored), other lines skipped;
+ * tokens that do not parse entirely leave 0 (a coordinate) or index 0 (a
+ * face vertex), as the reference's try/except defaults do — so "f 1//2 ..."
+ * gives index 0 unless RT_OBJ_SLASH_INDICES takes the integer before the
+ * first '/'. Face normals are not read (the reference computes them:
+ * calcNormals, done by rt_scene_create when rt_mesh_desc.normals is NULL).
+ * Query form: vertices == faces == NULL sets the two counts; then pass
+ * buffers of num_vertices*3 doubles and num_faces*3 int32 (0-based). */
+#define RT_OBJ_SLASH_INDICES 0x1u
+int rt_load_obj(const char *path, uint32_t flags, int64_t *num_vertices,
+                double *vertices, int64_t *num_faces, int32_t *faces);
+
+/* objconv's writeGeom (src/loaders/objconv.nim:139-153): int32 face count,
+ * then each face's three vertices as float32 x, y, z. */
+int rt_write_geom(const char *path, const double *vertices,
+                  int64_t num_vertices, const int32_t *faces,
+                  int64_t num_faces);
+
 #ifdef __cplusplus
 }
 #endif

@@ -22,6 +22,7 @@ RT_FLAG_ANYHIT_SHADOWS = 0x1
 RT_FLAG_COUNT_TRAVERSAL = 0x2
 RT_FLAG_NO_REORDER = 0x4
 RT_BVH_SAH = 0
+RT_OBJ_SLASH_INDICES = 0x1
 RT_BVH_PLOC = 1
 
 _d16 = C.c_double * 16
@@ -173,6 +174,9 @@ SIGNATURES = {
     "rt_ppm_payload_bytes": (C.c_int64, [C.c_int32, C.c_int32, C.c_int32]),
     "rt_rgba_encode_device": (C.c_int, [_P, C.c_int32, C.c_int32, C.c_uint8, _P, _P]),
     "rt_ppm_header": (C.c_int, [C.c_int32, C.c_int32, C.c_int32, C.c_char_p, C.c_int32]),
+    "rt_load_obj": (C.c_int, [C.c_char_p, C.c_uint32, C.POINTER(C.c_int64), C.POINTER(C.c_double),
+                              C.POINTER(C.c_int64), C.POINTER(C.c_int32)]),
+    "rt_write_geom": (C.c_int, [C.c_char_p, C.POINTER(C.c_double), C.c_int64, C.POINTER(C.c_int32), C.c_int64]),
     "rt_queue_create": (C.c_int, [_P, C.POINTER(_P)]),
     "rt_queue_start": (C.c_int, [_P]),
     "rt_queue_stop": (C.c_int, [_P]),

@@ -4,9 +4,11 @@
   and read by test/test.nim:14-26 — little-endian int32 N, then N triangles of
   3 vertices of 3 float32. (The reference's own src/loaders/geomloader.nim is
   broken: it reads no triangle data, geomloader.nim:38-45.)
-- loadObj: `v` / `f` OBJ subset of src/loaders/obj.nim:87-126 (1-based face
-  indices, first three indices of each `f`, normals computed per face by the
-  library exactly as calcNormals obj.nim:65-84).
+- loadObj: the native OBJ reader (rt_load_obj, csrc/rt_obj.cpp) with
+  src/loaders/obj.nim:87-126's semantics (1-based face indices, first three
+  of each `f`, unparsable tokens -> 0), normals computed per face by the
+  library exactly as calcNormals obj.nim:65-84.
+- objconv: objconv.nim's OBJ -> .geom conversion (rt_write_geom).
 """
 import os
 
@@ -45,20 +47,41 @@ def writeGeom(path, vertices, faces):
         fh.write(v[f].astype("<f4").tobytes())
 
 
-def loadObj(path, objectToWorld=None):
-    """obj.nim loadObj: vertices from `v x y z`, faces from `f a b c`."""
-    verts, faces = [], []
-    with open(path, "r") as fh:
-        for line in fh:
-            c = line.split()
-            if not c:
-                continue
-            if c[0] == "v":
-                verts.append([float(c[1]), float(c[2]), float(c[3])])
-            elif c[0] == "f":
-                faces.append([int(c[k].split("/")[0]) - 1 for k in (1, 2, 3)])
-    return TriangleMesh(np.array(verts, dtype=np.float64), np.array(faces, dtype=np.int32), None,
-                        mat4(1.0) if objectToWorld is None else objectToWorld)
+def loadObjArrays(path, slash_indices=False):
+    """obj.nim loadObj's vertex / face arrays through the native reader
+    (rt_load_obj): (V, 3) float64, (F, 3) int32 0-based."""
+    import ctypes as C
+
+    from . import abi
+    from ._lib import check, lib
+    flags = abi.RT_OBJ_SLASH_INDICES if slash_indices else 0
+    nv, nf = C.c_int64(0), C.c_int64(0)
+    p = os.fsencode(path)
+    check(lib().rt_load_obj(p, flags, C.byref(nv), None, C.byref(nf), None))
+    v = np.zeros((max(nv.value, 1), 3), np.float64)
+    f = np.zeros((max(nf.value, 1), 3), np.int32)
+    check(lib().rt_load_obj(p, flags, C.byref(nv), v.ctypes.data_as(C.POINTER(C.c_double)), C.byref(nf),
+                            f.ctypes.data_as(C.POINTER(C.c_int32))))
+    return v[:nv.value], f[:nf.value]
+
+
+def loadObj(path, objectToWorld=None, slash_indices=False):
+    """obj.nim loadObj (87-126): a TriangleMesh of the file's `v` / `f`
+    lines; face normals are computed by the library (calcNormals)."""
+    v, f = loadObjArrays(path, slash_indices)
+    return TriangleMesh(v, f, None, mat4(1.0) if objectToWorld is None else objectToWorld)
+
+
+def objconv(obj_path, geom_path, slash_indices=False):
+    """objconv.nim main: loadObj then writeGeom (native rt_write_geom)."""
+    import ctypes as C
+
+    from ._lib import check, lib
+    v, f = loadObjArrays(obj_path, slash_indices)
+    v = np.ascontiguousarray(v)
+    f = np.ascontiguousarray(f)
+    check(lib().rt_write_geom(os.fsencode(geom_path), v.ctypes.data_as(C.POINTER(C.c_double)), v.shape[0],
+                              f.ctypes.data_as(C.POINTER(C.c_int32)), f.shape[0]))
 
 
 def default_geom_path():
