@@ -262,6 +262,31 @@ int rt_unshard_bands_device(const float *d_gathered, float *d_fb,
 int rt_band_rows(int32_t height, int32_t band_h, int32_t world,
                  int32_t *out_rows);
 
+/* Stats of the last render call on this scene (waits for it): for
+ * asynchronous _device calls made with out == NULL. */
+int rt_scene_last_stats(rt_scene *scene, rt_stats *out);
+
+/* ---- one process, several GPUs (SURVEY.md 8(b) rt_render_frame_multi) ---- */
+
+/* The scene replicated on every listed device (a device may repeat: several
+ * ranks on one GPU); rows cut into band_h-row bands dealt round-robin
+ * (band b -> rank b % num_devices; band_h 0 means 4); every rank renders its
+ * bands on its own device at the same time, the compact band buffers move to
+ * devices[0] over xGMI (peer copies) and are un-interleaved there. Images and
+ * Stats equal the single-device frame. For one process per GPU use
+ * rt_render_bands_device + rt_unshard_bands_device with RCCL instead. */
+typedef struct rt_multi rt_multi;
+int rt_multi_create(const rt_scene_desc *desc, const int32_t *devices,
+                    int32_t num_devices, int32_t band_h, rt_multi **out);
+/* Whole frame (step 1) into d_fb, a width*height*3 float32 buffer on
+ * devices[0]; out != NULL waits for the frame and sums the Stats. */
+int rt_render_frame_multi_device(rt_multi *m, const rt_options *opts,
+                                 float *d_fb, rt_stats *out);
+/* Whole frame into the caller's host framebuffer (fb_w*fb_h*3 floats). */
+int rt_render_frame_multi(rt_multi *m, const rt_options *opts, float *fb,
+                          int32_t fb_w, int32_t fb_h, rt_stats *out);
+int rt_multi_destroy(rt_multi *m);
+
 /* ---- render queue (workerpool.nim WorkerPool[WorkMsg, ResponseMsg]) ---- */
 
 /* The pool raytracer.nim and gui.nim drive (src/concurrency/workerpool.nim;

@@ -1250,6 +1250,14 @@ extern "C" int rt_render_bands_device(rt_scene* s, const rt_options* o, float* d
   return render_device(s, o, mp, d_bands, (hipStream_t)stream, out);
 }
 
+extern "C" int rt_scene_last_stats(rt_scene* s, rt_stats* out) {
+  if (!s || !out) return fail(RT_E_INVALID, "null argument");
+  std::lock_guard<std::mutex> lk(s->mu);
+  DeviceGuard g(s->device);
+  HIP_TRY(hipStreamWaitEvent(s->stream, s->done, 0));
+  return read_stats(s, s->stream, out);
+}
+
 extern "C" int rt_unshard_bands_device(const float* d_gathered, float* d_fb, int32_t width, int32_t height,
                                        int32_t band_h, int32_t world, void* stream) {
   if (!d_gathered || !d_fb || width <= 0 || height <= 0 || band_h <= 0 || world <= 0)

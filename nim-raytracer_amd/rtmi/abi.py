@@ -177,6 +177,13 @@ SIGNATURES = {
     "rt_load_obj": (C.c_int, [C.c_char_p, C.c_uint32, C.POINTER(C.c_int64), C.POINTER(C.c_double),
                               C.POINTER(C.c_int64), C.POINTER(C.c_int32)]),
     "rt_write_geom": (C.c_int, [C.c_char_p, C.POINTER(C.c_double), C.c_int64, C.POINTER(C.c_int32), C.c_int64]),
+    "rt_scene_last_stats": (C.c_int, [_P, C.POINTER(rt_stats)]),
+    "rt_multi_create": (C.c_int, [C.POINTER(rt_scene_desc), C.POINTER(C.c_int32), C.c_int32, C.c_int32,
+                                  C.POINTER(_P)]),
+    "rt_render_frame_multi_device": (C.c_int, [_P, C.POINTER(rt_options), _P, C.POINTER(rt_stats)]),
+    "rt_render_frame_multi": (C.c_int, [_P, C.POINTER(rt_options), C.POINTER(C.c_float), C.c_int32, C.c_int32,
+                                        C.POINTER(rt_stats)]),
+    "rt_multi_destroy": (C.c_int, [_P]),
     "rt_queue_create": (C.c_int, [_P, C.POINTER(_P)]),
     "rt_queue_start": (C.c_int, [_P]),
     "rt_queue_stop": (C.c_int, [_P]),

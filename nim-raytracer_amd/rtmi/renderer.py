@@ -145,6 +145,51 @@ def ppm_encode_device(d_fb, width, height, bits=8, sRGB=True, stream=None):
     return buf.raw[:hl], out
 
 
+class MultiDeviceScene:
+    """One process, several GPUs (rt_multi_*, SURVEY.md 8(b)
+    rt_render_frame_multi): the scene replicated on every listed device
+    (repeats allowed), bands dealt round-robin, gathered on devices[0]."""
+
+    def __init__(self, scene: Scene, devices=(0,), band_h=4):
+        initRenderer(devices[0])
+        self.devices = list(devices)
+        flat = flatten(scene)
+        arr = (C.c_int32 * len(self.devices))(*self.devices)
+        h = C.c_void_p()
+        check(lib().rt_multi_create(C.byref(flat.desc), arr, len(self.devices), int(band_h), C.byref(h)))
+        self.h = h
+
+    def render_frame(self, opts: Options, fb) -> Stats:
+        """Whole frame into a host (h, w, 3) float32 array."""
+        if not (isinstance(fb, np.ndarray) and fb.dtype == np.float32 and fb.flags.c_contiguous
+                and fb.shape == (opts.height, opts.width, 3)):
+            raise ValueError("fb must be a C-contiguous float32 array of shape (height, width, 3)")
+        o = opts.to_c()
+        st = abi.rt_stats()
+        check(lib().rt_render_frame_multi(self.h, C.byref(o), fb.ctypes.data_as(C.POINTER(C.c_float)),
+                                          opts.width, opts.height, C.byref(st)))
+        return Stats.from_c(st)
+
+    def render_frame_device(self, opts: Options, d_fb) -> Stats:
+        """Whole frame into a device buffer on devices[0]; waits, returns Stats."""
+        ptr = _ptr(d_fb, opts.width * opts.height * 3)
+        o = opts.to_c()
+        st = abi.rt_stats()
+        check(lib().rt_render_frame_multi_device(self.h, C.byref(o), C.c_void_p(ptr), C.byref(st)))
+        return Stats.from_c(st)
+
+    def close(self):
+        if getattr(self, "h", None) is not None and self.h.value:
+            lib().rt_multi_destroy(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class ResponseMsg:
     """ResponseMsg (raytracer.nim:21-23) plus the line it answers."""
 
