@@ -148,12 +148,13 @@ struct RenderParams {
 // ---- float32 performance-kernel records (rt_fast.h) -------------------------
 // One 64-byte hot record per object: everything trace() needs, one s_load.
 struct alignas(16) FObj {
-  int32_t type, xf, mesh, pad0;
+  int32_t type, xf, mesh;
+  int32_t root;   // mesh: BVH2 root node (FMesh.root), so a trace needs no FMesh fetch
   float t[3];     // world_to_object translation (XF_TRANSLATE)
   float r;        // sphere radius
-  float lo[3];    // box vmin
+  float lo[3];    // box vmin; mesh: its AABB (calcAABB, object space)
   float pad1;
-  float hi[3];    // box vmax
+  float hi[3];    // box vmax; mesh: its AABB
   float pad2;
 };
 static_assert(sizeof(FObj) == 64, "FObj must be 64 bytes");

@@ -382,6 +382,7 @@ __device__ __forceinline__ float analytic_t(KP p, const FObj& ob, int i, F3 o, F
 template <bool COUNT, unsigned F>
 __device__ __forceinline__ Hit trace(KP p, F3 o, F3 d, float tmax, bool active, bool shadow,
                                      Stats32& ws) {
+  RT_STAMP(t_trace0);
   Hit h{-1, -1, tmax};
   const bool early = (F & F_MESH) && shadow && p->shadow_mesh >= 0;
   float stop = -1.0f;
@@ -401,14 +402,14 @@ __device__ __forceinline__ Hit trace(KP p, F3 o, F3 d, float tmax, bool active, 
     } else {
       F3 ro, rd;
       to_object<F>(p, ob, i, o, d, ro, rd);
-      const FMesh m = cp(p->meshes)[ob.mesh];
       // TriangleMesh.intersect (geom.nim:339-358): a ray starting inside
-      // the mesh AABB misses; otherwise the closest face.
-      const float gate = aabb(m.lo, m.hi, ro, f3(rcp(rd.x), rcp(rd.y), rcp(rd.z)));
+      // the mesh AABB misses; otherwise the closest face. (The AABB and the
+      // root ride in the object record: no dependent FMesh fetch.)
+      const float gate = aabb(ob.lo, ob.hi, ro, f3(rcp(rd.x), rcp(rd.y), rcp(rd.z)));
       const bool in = gate >= 0.0f;
       float tb = h.t;
       int best = -1;
-      if (m.root >= 0) traverse<COUNT>(p, m.root, ro, rd, active && in, early && i == p->shadow_mesh, stop, tb, best, ws);
+      if (ob.root >= 0) traverse<COUNT>(p, ob.root, ro, rd, active && in, early && i == p->shadow_mesh, stop, tb, best, ws);
       t = !in ? -finf() : (best >= 0 ? tb : finf());
       tri = best;
     }
@@ -420,6 +421,9 @@ __device__ __forceinline__ Hit trace(KP p, F3 o, F3 d, float tmax, bool active, 
       h.tri = tri;
     }
   }
+#ifdef RTMI_STAMPS
+  { RT_STAMP(t_trace1); RT_ACC(6, t_trace0, t_trace1); }
+#endif
   return h;
 }
 
@@ -697,6 +701,7 @@ __global__ __launch_bounds__(256) RTMI_OCC void k_render_fast(const FastParams p
     const int iters = (p->spp + L - 1) / L;
     const int gg = p->order ? cp(p->order)[g] : g;
     const unsigned t_item = (unsigned)__builtin_amdgcn_s_memtime();
+    RT_STAMP(t_it0);
     const GroupPix gp = group_pixel(p, gg, lane_id_fresh());
     // multiJittered / correlatedMultiJittered (sampling.nim:39-113): the
     // wave builds each of its pixels' (m, m) tables in LDS — canonical
@@ -797,6 +802,9 @@ __global__ __launch_bounds__(256) RTMI_OCC void k_render_fast(const FastParams p
       }
     }
     if (p->cost && lane == 0) p->cost[gg] = (unsigned)__builtin_amdgcn_s_memtime() - t_item;
+#ifdef RTMI_STAMPS
+    { RT_STAMP(t_it1); RT_ACC(8, t_it0, t_it1); }
+#endif
     // 32-bit wave counters -> the wave's 64-bit LDS totals
     if (lane < kStatSlots) {
       unsigned int v = 0u;

@@ -435,9 +435,10 @@ void fill_fast_records(const rt_scene_desc* d, const std::vector<DevMesh<float>>
     o.mesh = s.type == RT_MESH ? s.mesh : 0;
     for (int k = 0; k < 3; ++k) {
       o.t[k] = (float)s.world_to_object[12 + k];
-      o.lo[k] = (float)s.box_min[k];
-      o.hi[k] = (float)s.box_max[k];
+      o.lo[k] = (float)(s.type == RT_MESH ? dm[(size_t)s.mesh].lo[k] : s.box_min[k]);
+      o.hi[k] = (float)(s.type == RT_MESH ? dm[(size_t)s.mesh].hi[k] : s.box_max[k]);
     }
+    o.root = s.type == RT_MESH ? dm[(size_t)s.mesh].root : -1;
     o.r = (float)s.radius;
     for (int c = 0; c < 4; ++c)
       for (int r = 0; r < 3; ++r) x.w2o[c * 3 + r] = (float)s.world_to_object[c * 4 + r];
