@@ -386,6 +386,7 @@ __device__ __forceinline__ Hit trace(KP p, F3 o, F3 d, float tmax, bool active, 
   Hit h{-1, -1, tmax};
   const bool early = (F & F_MESH) && shadow && p->shadow_mesh >= 0;
   float stop = -1.0f;
+  RT_STAMP(t_st0);
   if (early) {
     stop = finf();
     for (int i = p->shadow_mesh + 1; i < p->nobj; ++i) {
@@ -393,6 +394,9 @@ __device__ __forceinline__ Hit trace(KP p, F3 o, F3 d, float tmax, bool active, 
       stop = t >= 0.0f ? fminf(stop, t) : stop;
     }
   }
+#if RTMI_STAMPS == 2
+  { RT_STAMP(t_st1); RT_ACC(7, t_st0, t_st1); }
+#endif
   for (int i = 0; i < p->nobj; ++i) {
     const FObj ob = cp(p->objs)[i];
     float t;
@@ -400,6 +404,7 @@ __device__ __forceinline__ Hit trace(KP p, F3 o, F3 d, float tmax, bool active, 
     if (!(F & F_MESH) || ob.type != GEOM_MESH) {
       t = analytic_t<F>(p, ob, i, o, d);
     } else {
+      RT_STAMP(t_g0);
       F3 ro, rd;
       to_object<F>(p, ob, i, o, d, ro, rd);
       // TriangleMesh.intersect (geom.nim:339-358): a ray starting inside
@@ -409,6 +414,9 @@ __device__ __forceinline__ Hit trace(KP p, F3 o, F3 d, float tmax, bool active, 
       const bool in = gate >= 0.0f;
       float tb = h.t;
       int best = -1;
+#if RTMI_STAMPS == 2
+      { RT_STAMP(t_g1); RT_ACC(8, t_g0, t_g1); }
+#endif
       if (ob.root >= 0) traverse<COUNT>(p, ob.root, ro, rd, active && in, early && i == p->shadow_mesh, stop, tb, best, ws);
       t = !in ? -finf() : (best >= 0 ? tb : finf());
       tri = best;
@@ -775,7 +783,7 @@ __global__ __launch_bounds__(256) RTMI_OCC void k_render_fast(const FastParams p
       ws.v[STAT_PRIMARY] += pc(bal(sv));
       RT_STAMP(t_s0);
       shade_path<COUNT, F>(p, o, d, sv, ls, pacc, ws);
-#ifdef RTMI_STAMPS
+#if RTMI_STAMPS == 1
       { RT_STAMP(t_s1); RT_ACC(7, t_s0, t_s1); }
 #endif
     }
@@ -802,7 +810,7 @@ __global__ __launch_bounds__(256) RTMI_OCC void k_render_fast(const FastParams p
       }
     }
     if (p->cost && lane == 0) p->cost[gg] = (unsigned)__builtin_amdgcn_s_memtime() - t_item;
-#ifdef RTMI_STAMPS
+#if RTMI_STAMPS == 1
     { RT_STAMP(t_it1); RT_ACC(8, t_it0, t_it1); }
 #endif
     // 32-bit wave counters -> the wave's 64-bit LDS totals
