@@ -55,6 +55,16 @@ __device__ __forceinline__ const RT_CONST T* cp(const T* p) {
 }
 
 __device__ __forceinline__ unsigned long long bal(bool p) { return __builtin_amdgcn_ballot_w64(p); }
+// Lane masks straight from a v_cmp (llvm.amdgcn.fcmp: ordered >= / <) and a
+// mask back to a per-lane predicate (llvm.amdgcn.inverse.ballot): a ballot of
+// a compound bool otherwise materialises it in a VGPR (v_cndmask 0/1 +
+// v_cmp_ne) before the popcount.
+#ifndef RTMI_FCMP_MASKS
+#define RTMI_FCMP_MASKS 1
+#endif
+__device__ __forceinline__ unsigned long long m_ge(float a, float b) { return __builtin_amdgcn_fcmpf(a, b, 3); }
+__device__ __forceinline__ unsigned long long m_lt(float a, float b) { return __builtin_amdgcn_fcmpf(a, b, 4); }
+__device__ __forceinline__ bool lane_in(unsigned long long m) { return __builtin_amdgcn_inverse_ballot_w64(m); }
 __device__ __forceinline__ unsigned int pc(unsigned long long m) { return (unsigned int)__builtin_popcountll(m); }
 __device__ __forceinline__ float rcp(float x) { return __builtin_amdgcn_rcpf(x); }
 __device__ __forceinline__ float rsq(float x) { return __builtin_amdgcn_rsqf(x); }
@@ -217,17 +227,29 @@ __device__ __forceinline__ void leaf(KP p, int first, int n, F3 o, F3 d, unsigne
 // traversal visits each node at most once.
 // early/stop: exact early exit for shadow rays (trace()): a lane
 // retires once its best t <= stop.
-template <bool COUNT>
-__device__ __forceinline__ void traverse(KP p, int root, F3 o, F3 d, bool active, bool early,
-                                         float stop, float& tbest, int& best_id, Stats32& ws) {
-  if (bal(active) == 0ull) return;
-  RT_STAMP(t_enter);
+// Box-test form of a ray: ni = 1/d with components below 1e-20 in magnitude
+// replaced by +-1e-20 (finite slabs, no 0 * inf), oi = o * ni; a slab plane
+// x = c is crossed at fma(c, ni.x, -oi.x).
+struct SlabRay {
+  F3 ni, oi;
+};
+__device__ __forceinline__ SlabRay slab_ray(F3 o, F3 d) {
   const float e = 1e-20f;
   const float dx = fabsf(d.x) < e ? __builtin_copysignf(e, d.x) : d.x;
   const float dy = fabsf(d.y) < e ? __builtin_copysignf(e, d.y) : d.y;
   const float dz = fabsf(d.z) < e ? __builtin_copysignf(e, d.z) : d.z;
-  const F3 ni = f3(rcp(dx), rcp(dy), rcp(dz));
-  const F3 oi = f3(o.x * ni.x, o.y * ni.y, o.z * ni.z);
+  SlabRay r;
+  r.ni = f3(rcp(dx), rcp(dy), rcp(dz));
+  r.oi = f3(o.x * r.ni.x, o.y * r.ni.y, o.z * r.ni.z);
+  return r;
+}
+
+template <bool COUNT>
+__device__ __forceinline__ void traverse(KP p, int root, F3 o, F3 d, SlabRay sr, bool active, bool early,
+                                         float stop, float& tbest, int& best_id, Stats32& ws) {
+  if (bal(active) == 0ull) return;
+  RT_STAMP(t_enter);
+  const F3 ni = sr.ni, oi = sr.oi;
   const int lane = (int)__lane_id();
   float tc = active ? tbest : -1.0f;
   // Retire only on a FOUND hit: accepted t are < the initial limit tbest, so
@@ -378,24 +400,16 @@ __device__ __forceinline__ float analytic_t(KP p, const FObj& ob, int i, F3 o, F
 // its t beats the mesh's closest t. So once a lane has found a mesh hit at
 // t <= stop = min t of the analytic objects after the mesh, every later
 // comparison is decided and the lane retires: exact, not an approximation.
-// Applied when the scene has exactly one mesh object (p->shadow_mesh).
+// Applied when the scene has exactly one mesh object (p->shadow_mesh); stop =
+// min t >= 0 of the analytic objects after the mesh.
 template <bool COUNT, unsigned F>
 __device__ __forceinline__ Hit trace(KP p, F3 o, F3 d, float tmax, bool active, bool shadow,
                                      Stats32& ws) {
   RT_STAMP(t_trace0);
   Hit h{-1, -1, tmax};
   const bool early = (F & F_MESH) && shadow && p->shadow_mesh >= 0;
-  float stop = -1.0f;
-  RT_STAMP(t_st0);
-  if (early) {
-    stop = finf();
-    for (int i = p->shadow_mesh + 1; i < p->nobj; ++i) {
-      const float t = analytic_t<F>(p, cp(p->objs)[i], i, o, d);
-      stop = t >= 0.0f ? fminf(stop, t) : stop;
-    }
-  }
-#if RTMI_STAMPS == 2
-  { RT_STAMP(t_st1); RT_ACC(7, t_st0, t_st1); }
+#if RTMI_FCMP_MASKS
+  const unsigned long long actm = bal(active);
 #endif
   for (int i = 0; i < p->nobj; ++i) {
     const FObj ob = cp(p->objs)[i];
@@ -408,21 +422,50 @@ __device__ __forceinline__ Hit trace(KP p, F3 o, F3 d, float tmax, bool active, 
       F3 ro, rd;
       to_object<F>(p, ob, i, o, d, ro, rd);
       // TriangleMesh.intersect (geom.nim:339-358): a ray starting inside
-      // the mesh AABB misses; otherwise the closest face. (The AABB and the
-      // root ride in the object record: no dependent FMesh fetch.)
-      const float gate = aabb(ob.lo, ob.hi, ro, f3(rcp(rd.x), rcp(rd.y), rcp(rd.z)));
-      const bool in = gate >= 0.0f;
+      // the mesh AABB misses (entry t < 0); otherwise the closest face. The
+      // AABB and the root ride in the object record (no dependent FMesh
+      // fetch); the gate uses the traversal's slab form of the ray.
+      const SlabRay sr = slab_ray(ro, rd);
+      const float ax = __builtin_fmaf(ob.lo[0], sr.ni.x, -sr.oi.x), bx = __builtin_fmaf(ob.hi[0], sr.ni.x, -sr.oi.x);
+      const float ay = __builtin_fmaf(ob.lo[1], sr.ni.y, -sr.oi.y), by = __builtin_fmaf(ob.hi[1], sr.ni.y, -sr.oi.y);
+      const float az = __builtin_fmaf(ob.lo[2], sr.ni.z, -sr.oi.z), bz = __builtin_fmaf(ob.hi[2], sr.ni.z, -sr.oi.z);
+      const float gmin = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
+      const float gmax = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz)) * 1.00000024f;
+      const bool in = gmin <= gmax && gmin >= 0.0f;
+      const bool part = active && in;
       float tb = h.t;
       int best = -1;
 #if RTMI_STAMPS == 2
       { RT_STAMP(t_g1); RT_ACC(8, t_g0, t_g1); }
 #endif
-      if (ob.root >= 0) traverse<COUNT>(p, ob.root, ro, rd, active && in, early && i == p->shadow_mesh, stop, tb, best, ws);
+      // shadow early exit (above): stop is only computed when some lane of
+      // the wave enters the mesh
+      float stop = -1.0f;
+      if (ob.root >= 0 && bal(part) != 0ull) {
+        if (early && i == p->shadow_mesh) {
+          RT_STAMP(t_st0);
+          stop = finf();
+          for (int j = i + 1; j < p->nobj; ++j) {
+            const float tj = analytic_t<F>(p, cp(p->objs)[j], j, o, d);
+            stop = tj >= 0.0f ? fminf(stop, tj) : stop;
+          }
+#if RTMI_STAMPS == 2
+          { RT_STAMP(t_st1); RT_ACC(7, t_st0, t_st1); }
+#endif
+        }
+        traverse<COUNT>(p, ob.root, ro, rd, sr, part, early && i == p->shadow_mesh, stop, tb, best, ws);
+      }
       t = !in ? -finf() : (best >= 0 ? tb : finf());
       tri = best;
     }
+#if RTMI_FCMP_MASKS
+    const unsigned long long um = m_ge(t, 0.0f) & m_lt(t, h.t) & actm;
+    ws.v[STAT_HITS] += pc(um);
+    const bool upd = lane_in(um);
+#else
     const bool upd = active && t >= 0.0f && t < h.t;
     ws.v[STAT_HITS] += pc(bal(upd));
+#endif
     if (upd) {
       h.t = t;
       h.obj = i;
