@@ -189,8 +189,7 @@ struct FastParams {
   const FObjX* objx;
   const FMesh* meshes;
   const FLight* lights;
-  const BvhNode* nodes;
-  const TriFast* tris;
+  const BvhNode* tree;              // nodes (child refs = byte offsets into tree) then TriFast records
   const float* normals;
   float* fb;
   unsigned long long* partials;

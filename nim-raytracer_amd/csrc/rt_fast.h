@@ -30,9 +30,6 @@
 #endif
 
 
-#ifndef RTMI_TRANSITION_ARITH
-#define RTMI_TRANSITION_ARITH 0
-#endif
 
 namespace rtmi {
 namespace fast {
@@ -204,10 +201,19 @@ __device__ __forceinline__ void tri_test(const RT_CONST TriFast& T, F3 o, F3 d, 
   tc = acc ? ts : tc;
 }
 
-// Leaf: the n (1..kLeafMax, wave-uniform) triangles starting at `first`.
+// A record of the float32 tree (FastParams.tree) at a byte offset: one scalar
+// base + a 32-bit SGPR offset (s_load ... soffset), no 64-bit address
+// arithmetic on the traversal's dependent chain.
+template <class T>
+__device__ __forceinline__ const RT_CONST T* rec(KP p, int off) {
+  return (const RT_CONST T*)((const RT_CONST char*)p->tree + (unsigned)off);
+}
+
+// Leaf: the n (1..kLeafMax, wave-uniform) triangles starting at byte offset
+// `first` of the tree.
 __device__ __forceinline__ void leaf(KP p, int first, int n, F3 o, F3 d, unsigned long long& key,
                                      float& tc) {
-  const RT_CONST TriFast* t = cp(p->tris) + first;
+  const RT_CONST TriFast* t = rec<TriFast>(p, first);
   tri_test(t[0], o, d, key, tc);
 #pragma unroll
   for (int k = 1; k < kLeafMax; ++k) {
@@ -268,7 +274,7 @@ __device__ __forceinline__ void traverse(KP p, int root, F3 o, F3 d, SlabRay sr,
   int mlo = 0, mhi = 0;
   if constexpr (COUNT) vm = bal(tc >= 0.0f);
   for (;;) {
-    const BvhNode nd = cp(p->nodes)[node];
+    const BvhNode nd = *rec<BvhNode>(p, node);
     if constexpr (COUNT) {
       ws.v[STAT_NODE_FETCH] += 1u;
       ws.v[STAT_LANE_NODES] += pc(vm);
@@ -307,39 +313,6 @@ __device__ __forceinline__ void traverse(KP p, int root, F3 o, F3 d, SlabRay sr,
       }
       m1 = 0ull;
     }
-#if RTMI_TRANSITION_ARITH
-    // Transition as straight-line scalar arithmetic (one branch): the
-    // if / else-if / else form lowered to flag-passing flow blocks costing
-    // 20-37 SALU per node step.
-    if ((m0 | m1) != 0ull) {
-      const unsigned long long both = m0 & m1;
-      const unsigned int has_both = both != 0ull;
-      // near child: majority vote of the lanes that hit both boxes
-      const unsigned int take1 =
-          (unsigned int)(m0 == 0ull) | (has_both & (unsigned int)(pc(bal(tn0 <= tn1) & both) * 2u < pc(both)));
-      const int next = take1 ? nd.c1 : nd.c0;
-      const int far = take1 ? nd.c0 : nd.c1;
-      const int push_lane = has_both ? sp : 64;  // 64: no lane takes the push
-      stack = (lane == push_lane) ? far : stack;
-      if constexpr (COUNT) {
-        const unsigned long long fm = take1 ? m0 : m1;
-        mlo = (lane == push_lane) ? (int)(unsigned int)fm : mlo;
-        mhi = (lane == push_lane) ? (int)(unsigned int)(fm >> 32) : mhi;
-        vm = take1 ? m1 : m0;
-      }
-      sp += (int)has_both;
-      node = next;
-    } else {
-      if (sp == 0) break;
-      if (early && bal(tc >= 0.0f) == 0ull) break;
-      --sp;
-      node = __builtin_amdgcn_readlane(stack, sp);
-      if constexpr (COUNT)
-        vm = (unsigned long long)(unsigned int)__builtin_amdgcn_readlane(mlo, sp) |
-             ((unsigned long long)(unsigned int)__builtin_amdgcn_readlane(mhi, sp) << 32);
-    }
-  }
-#else
     if (m0 && m1) {
       const unsigned long long both = m0 & m1;
       const bool first0 = pc(bal(tn0 <= tn1) & both) * 2u >= pc(both);
@@ -370,7 +343,6 @@ __device__ __forceinline__ void traverse(KP p, int root, F3 o, F3 d, SlabRay sr,
              ((unsigned long long)(unsigned int)__builtin_amdgcn_readlane(mhi, sp) << 32);
     }
   }
-#endif
   if (key != key0) {
     tbest = __uint_as_float((unsigned int)(key >> 32));
     best_id = (int)(unsigned int)key;

@@ -102,18 +102,22 @@ struct FastData {
   DevBuf<FObjX> objx;
   DevBuf<FMesh> meshes;
   DevBuf<FLight> lights;
-  DevBuf<TriFast> tris;
+  // the float32 kernel's BVH in ONE allocation: the nodes with child refs as
+  // BYTE offsets into this buffer (inner child: its node, leaf: its first
+  // TriFast record), then the TriFast records; one scalar base + a 32-bit
+  // SGPR offset address every record (s_load ... soffset)
+  DevBuf<BvhNode> tree;
   DevBuf<float> normals;
   void release() {
     objs.release();
     objx.release();
     meshes.release();
     lights.release();
-    tris.release();
+    tree.release();
     normals.release();
   }
   size_t bytes() const {
-    return objs.bytes() + objx.bytes() + meshes.bytes() + lights.bytes() + tris.bytes() + normals.bytes();
+    return objs.bytes() + objx.bytes() + meshes.bytes() + lights.bytes() + tree.bytes() + normals.bytes();
   }
 };
 
@@ -438,7 +442,8 @@ void fill_fast_records(const rt_scene_desc* d, const std::vector<DevMesh<float>>
       o.lo[k] = (float)(s.type == RT_MESH ? dm[(size_t)s.mesh].lo[k] : s.box_min[k]);
       o.hi[k] = (float)(s.type == RT_MESH ? dm[(size_t)s.mesh].hi[k] : s.box_max[k]);
     }
-    o.root = s.type == RT_MESH ? dm[(size_t)s.mesh].root : -1;
+    // byte offset of the root node in FastData.tree
+    o.root = s.type == RT_MESH && dm[(size_t)s.mesh].root >= 0 ? dm[(size_t)s.mesh].root * (int32_t)sizeof(BvhNode) : -1;
     o.r = (float)s.radius;
     for (int c = 0; c < 4; ++c)
       for (int r = 0; r < 3; ++r) x.w2o[c * 3 + r] = (float)s.world_to_object[c * 4 + r];
@@ -597,6 +602,10 @@ extern "C" int rt_scene_create(const rt_scene_desc* d, rt_scene** out_scene) {
     maxdepth = std::max(maxdepth, bvhs[(size_t)m].max_depth);
   }
   if (ntri > INT32_MAX / 2) return fail(RT_E_UNSUPPORTED, "too many triangles");
+  // the float32 kernel addresses its tree with signed 32-bit byte offsets
+  if ((nnodes + ntri + kLeafMax) * (int64_t)sizeof(BvhNode) > (int64_t)INT32_MAX)
+    return fail(RT_E_UNSUPPORTED, "%lld BVH nodes + %lld triangles exceed the float32 tree's 2 GiB offset range",
+                (long long)nnodes, (long long)ntri);
 
 
   std::unique_ptr<rt_scene> s(new rt_scene());
@@ -669,7 +678,9 @@ extern "C" int rt_scene_create(const rt_scene_desc* d, rt_scene** out_scene) {
     // array carries kLeafMax - 1 padding records (id -1) so a kernel may
     // read kLeafMax records from any leaf start
     int rc;
-    if ((rc = s->f32.tris.alloc((size_t)ntri)) || (rc = s->f64.tris.alloc((size_t)ntri + kLeafMax - 1))) return rc;
+    if ((rc = s->f32.tree.alloc((size_t)(nnodes + ntri))) || (rc = s->f64.tris.alloc((size_t)ntri + kLeafMax - 1)))
+      return rc;
+    TriFast* f32_tris = reinterpret_cast<TriFast*>(s->f32.tree.p + nnodes);
     std::vector<TriF64> pad((size_t)kLeafMax - 1);
     for (TriF64& t : pad) {
       std::memset(&t, 0, sizeof t);
@@ -682,7 +693,7 @@ extern "C" int rt_scene_create(const rt_scene_desc* d, rt_scene** out_scene) {
       DevBuf<int32_t> order;
       if ((rc = order.upload(bvhs[(size_t)m].order))) return rc;
       const bool ok = pack_triangles_device(d_verts[(size_t)m].p, d_faces[(size_t)m].p, order.p, nf,
-                                            s->f32.tris.p + base, s->f64.tris.p + base, s->stream);
+                                            f32_tris + base, s->f64.tris.p + base, s->stream);
       HIP_TRY(hipStreamSynchronize(s->stream));
       order.release();
       if (!ok) return fail(RT_E_DEVICE, "mesh %d: triangle packing failed", m);
@@ -692,6 +703,16 @@ extern "C" int rt_scene_create(const rt_scene_desc* d, rt_scene** out_scene) {
   mark("triangle packing");
   int rc = s->nodes.upload(all_nodes);
   if (rc) return rc;
+  {  // float32 tree: child refs -> byte offsets (leaves: past the nnodes node records)
+    std::vector<BvhNode> fn(all_nodes);
+    const int32_t kB = (int32_t)sizeof(BvhNode);
+    for (BvhNode& nd : fn) {
+      nd.c0 = (nd.n0 > 0 ? (int32_t)nnodes + nd.c0 : nd.c0) * kB;
+      nd.c1 = (nd.n1 > 0 ? (int32_t)nnodes + nd.c1 : nd.c1) * kB;
+    }
+    if (!fn.empty())
+      HIP_TRY(hipMemcpy(s->f32.tree.p, fn.data(), fn.size() * sizeof(BvhNode), hipMemcpyHostToDevice));
+  }
   s->max_waves = s->num_cus * 8 * 4;  // 8 blocks of 4 waves per CU at most
   if ((rc = s->partials.alloc((size_t)s->max_waves * kStatSlots))) return rc;
   if ((rc = s->acc.alloc(kStatSlots))) return rc;
@@ -941,8 +962,7 @@ void fill_fast(rt_scene* s, const rt_options* o, const Mapping& mp, float* fb, F
   p.objx = s->f32.objx.p;
   p.meshes = s->f32.meshes.p;
   p.lights = s->f32.lights.p;
-  p.nodes = s->nodes.p;
-  p.tris = s->f32.tris.p;
+  p.tree = s->f32.tree.p;
   p.normals = s->f32.normals.p;
   p.fb = fb;
   p.partials = s->partials.p;
