@@ -158,7 +158,9 @@ def main():
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     torch.cuda.set_device(local)
-    if world > 1:
+    # launched by torchrun (even with one rank): the band + RCCL-gather path
+    distributed = world > 1 or "TORCHELASTIC_RUN_ID" in os.environ or "LOCAL_WORLD_SIZE" in os.environ
+    if distributed:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
@@ -186,13 +188,13 @@ def main():
         # render this rank's bands (world == 1: the whole frame, one band set)
         if time_kernel is not None:
             time_kernel[0].record(stream)
-        if world > 1:
+        if distributed:
             ds.render_bands_device(opts, local_buf, BAND_H, rank, world, stream=stream, stats=False)
         else:
             ds.render_device(opts, fb, stream=stream, stats=False)
         if time_kernel is not None:
             time_kernel[1].record(stream)
-        if world > 1:
+        if distributed:
             gather_bands(local_buf, gathered if rank == 0 else None, rows * W * 3)
             if rank == 0:
                 unshard_bands_device(gathered, fb, W, H, BAND_H, world, stream=stream)
@@ -207,7 +209,7 @@ def main():
     for _ in range(max(0, args.warmup)):
         step()
     rays_local = st.numPrimaryRays + st.numShadowRays
-    if world > 1:
+    if distributed:
         t = torch.tensor([rays_local, st.numPrimaryRays, st.numShadowRays], dtype=torch.int64,
                          device="cuda")
         dist.all_reduce(t)
@@ -218,21 +220,29 @@ def main():
     # timed region
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
            for _ in range(args.steps)]
-    if world > 1:
+    if distributed:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(args.steps):
         step(evs[k])
     torch.cuda.synchronize()
-    if world > 1:
+    if distributed:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    if world > 1:
+    if distributed:
         e = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
     kern_ms = sum(a.elapsed_time(b) for a, b in evs) / max(1, args.steps)
+    # outside the timed region: the gathered frame must equal one GPU's
+    # single-call frame bit for bit (same samples, same arithmetic per pixel)
+    frame_check = None
+    if distributed and rank == 0:
+        ref = torch.zeros_like(fb)
+        ds.render_device(opts, ref, stream=stream, stats=False)
+        torch.cuda.synchronize()
+        frame_check = {"bit_identical_to_single_call_frame": bool(torch.equal(ref, fb))}
 
     value = rays_frame * args.steps / elapsed / 1e6
     # algorithmic bytes of one launch on this rank, SURVEY.md 8(d): per ray
@@ -294,6 +304,8 @@ def main():
             },
             "cpu_baseline": None,
         }
+        if frame_check is not None:
+            out["frame_check"] = frame_check
         if world == 1 and not args.no_cpu:
             # the reference's brute-force mesh loop is infeasible past ~200k
             # triangles (~1e11 triangle tests per 4K row): same-BVH only there
@@ -303,7 +315,7 @@ def main():
             # GPU/CPU ratio is also judged against a fair CPU implementation
             out["cpu_baseline_same_bvh"] = cpu_baseline(scene, W, H, args.cpu_seconds, bvh=True)
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if distributed:
         dist.barrier()
         dist.destroy_process_group()
 
