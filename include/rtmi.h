@@ -160,6 +160,11 @@ typedef struct rt_options {
  * durations measured on its first launch. Scheduling only: the image and
  * Stats are the same either way. */
 #define RT_FLAG_NO_REORDER 0x4u
+/* float32 kernel: search the mesh BVH for every ray. By default camera rays
+ * (>= 16 samples per pixel) and shadow rays to distant lights of a scene with
+ * one mesh object search the faces binned for their pixel / light-grid cell
+ * instead. The image and Stats are the same either way. */
+#define RT_FLAG_NO_BINNING 0x8u
 
 /* Stats (src/renderer/stats.nim:4-13) plus ray counts for Mray/s. */
 typedef struct rt_stats {

@@ -1,0 +1,273 @@
+// rt_bins.cpp — host builders of the float32 kernel's pixel lists and light
+// grids (rt_bins.h). float64 throughout; every bound errs on the side of
+// listing a face.
+#include "rt_bins.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <limits>
+
+namespace rtmi {
+
+namespace {
+
+// glm column-major: m[c*4 + r]
+inline void xform_point(const double m[16], const double p[3], double out[3]) {
+  for (int r = 0; r < 3; ++r) out[r] = m[0 * 4 + r] * p[0] + m[1 * 4 + r] * p[1] + m[2 * 4 + r] * p[2] + m[3 * 4 + r];
+}
+inline void xform_dir(const double m[16], const double d[3], double out[3]) {
+  for (int r = 0; r < 3; ++r) out[r] = m[0 * 4 + r] * d[0] + m[1 * 4 + r] * d[1] + m[2 * 4 + r] * d[2];
+}
+inline double dot3(const double a[3], const double b[3]) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+inline void cross3(const double a[3], const double b[3], double o[3]) {
+  o[0] = a[1] * b[2] - a[2] * b[1];
+  o[1] = a[2] * b[0] - a[0] * b[2];
+  o[2] = a[0] * b[1] - a[1] * b[0];
+}
+inline double norm3(const double a[3]) { return std::sqrt(dot3(a, a)); }
+
+// Frobenius norm of the 3x3 part: an upper bound of the spectral norm.
+double frob3(const double m[16]) {
+  double s = 0.0;
+  for (int c = 0; c < 3; ++c)
+    for (int r = 0; r < 3; ++r) s += m[c * 4 + r] * m[c * 4 + r];
+  return std::sqrt(s);
+}
+
+bool invert4(const double m[16], double inv[16]) {
+  // Gauss-Jordan with partial pivoting on a row-major copy
+  double a[4][8];
+  for (int r = 0; r < 4; ++r)
+    for (int c = 0; c < 4; ++c) {
+      a[r][c] = m[c * 4 + r];
+      a[r][4 + c] = r == c ? 1.0 : 0.0;
+    }
+  for (int c = 0; c < 4; ++c) {
+    int piv = c;
+    for (int r = c + 1; r < 4; ++r)
+      if (std::fabs(a[r][c]) > std::fabs(a[piv][c])) piv = r;
+    if (a[piv][c] == 0.0) return false;
+    if (piv != c)
+      for (int k = 0; k < 8; ++k) std::swap(a[c][k], a[piv][k]);
+    const double d = a[c][c];
+    for (int k = 0; k < 8; ++k) a[c][k] /= d;
+    for (int r = 0; r < 4; ++r) {
+      if (r == c) continue;
+      const double f = a[r][c];
+      if (f != 0.0)
+        for (int k = 0; k < 8; ++k) a[r][k] -= f * a[c][k];
+    }
+  }
+  for (int r = 0; r < 4; ++r)
+    for (int c = 0; c < 4; ++c) inv[c * 4 + r] = a[r][4 + c];
+  return true;
+}
+
+// The single-sided test rejects det < 1e-6 (geom.nim:306). det is computed
+// in float32 from the object-space direction rd and nn = -(e1 x e2); a face
+// is left out of a family's bins only when det stays below 1e-6 even with a
+// float32 error of 1e-6 * |rd| * |nn| (generous: the test's own rounding is
+// ~1e-7 of that).
+inline bool never_passes(double det_upper, double rd_max, double nlen) {
+  return det_upper + 1e-6 * rd_max * nlen < 1e-6;
+}
+
+// Two-pass bucket fill: count[k] entries per bin -> off (prefix) -> ent.
+template <class Emit>
+bool fill_bins(size_t nbins, size_t ntri, Emit emit, std::vector<int32_t>& off, std::vector<int32_t>& ent,
+               const char** why) {
+  std::vector<int64_t> cnt(nbins + 1, 0);
+  for (size_t i = 0; i < ntri; ++i) emit(i, [&](size_t b, int32_t) { ++cnt[b + 1]; });
+  for (size_t b = 0; b < nbins; ++b) cnt[b + 1] += cnt[b];
+  if (cnt[nbins] + kBinPad > std::numeric_limits<int32_t>::max()) {
+    *why = "too many bin entries";
+    return false;
+  }
+  off.assign(cnt.begin(), cnt.end());
+  ent.assign((size_t)cnt[nbins] + kBinPad, 0);
+  std::vector<int64_t> pos(cnt.begin(), cnt.end() - 1);
+  for (size_t i = 0; i < ntri; ++i) emit(i, [&](size_t b, int32_t rec) { ent[(size_t)pos[b]++] = rec; });
+  // padding repeats the last record: a read-ahead never leaves the tree
+  for (int k = 0; k < kBinPad; ++k) ent[(size_t)cnt[nbins] + k] = cnt[nbins] > 0 ? ent[(size_t)cnt[nbins] - 1] : 0;
+  return true;
+}
+
+}  // namespace
+
+bool build_pixel_bins(const std::vector<BinTri>& tris, const double o2w[16], const double w2o[16],
+                      const double c2w[16], double fov_deg, int width, int height, PixelBinsHost* out,
+                      const char** why) {
+  *why = "";
+  if (width <= 0 || height <= 0) {
+    *why = "empty image";
+    return false;
+  }
+  double w2c[16];
+  if (!invert4(c2w, w2c)) {
+    *why = "singular camera";
+    return false;
+  }
+  // camera constants of the float32 kernel (rtmi.cpp fill_fast): a camera-space
+  // direction (cx, cy, -1) is the sample at px = w/2 + cx/a, py = h/2 - cy/c
+  const double f = std::tan(fov_deg * (3.14159265358979323846 / 180.0) / 2);
+  const double r = (double)width / (double)height;
+  const double cam_a = 2.0 * r * f / (double)width, cam_c = 2.0 * f / (double)height;
+  const double cw[3] = {c2w[12], c2w[13], c2w[14]};
+  double co[3];
+  xform_point(w2o, cw, co);  // camera origin in object space
+  // |rd| of a unit world direction lies in [1/|o2w|, |w2o|]
+  const double rd_max = frob3(w2o), rd_min = 1.0 / frob3(o2w);
+  const double margin = 0.05;  // pixels
+  // per face: pixel rectangle, or empty
+  std::vector<int32_t> rect(tris.size() * 4, -1);
+  for (size_t i = 0; i < tris.size(); ++i) {
+    const BinTri& t = tris[i];
+    double e1[3], e2[3], c[3], nn[3], dc[3];
+    for (int k = 0; k < 3; ++k) {
+      e1[k] = t.v[1][k] - t.v[0][k];
+      e2[k] = t.v[2][k] - t.v[0][k];
+      dc[k] = t.v[0][k] - co[k];
+    }
+    cross3(e1, e2, c);
+    for (int k = 0; k < 3; ++k) nn[k] = -c[k];
+    const double nlen = norm3(nn);
+    // every camera ray reaching the face's plane has det = |rd| (v0 - C).nn / |P - C|
+    const double s = dot3(dc, nn);
+    double maxd = 0.0;
+    for (int v = 0; v < 3; ++v) {
+      double dv[3] = {t.v[v][0] - co[0], t.v[v][1] - co[1], t.v[v][2] - co[2]};
+      maxd = std::max(maxd, norm3(dv));
+    }
+    if (s <= 0.0 && maxd > 0.0 && never_passes(rd_min * s / maxd, rd_max, nlen)) continue;  // back face
+    double xmin = INFINITY, xmax = -INFINITY, ymin = INFINITY, ymax = -INFINITY;
+    for (int v = 0; v < 3; ++v) {
+      double pw[3], pc[3];
+      xform_point(o2w, t.v[v], pw);
+      xform_point(w2c, pw, pc);
+      if (!(pc[2] < -1e-9 * (1.0 + std::fabs(pc[0]) + std::fabs(pc[1])))) {
+        *why = "a mesh vertex lies at or behind the camera plane";
+        return false;
+      }
+      const double px = 0.5 * width + (pc[0] / -pc[2]) / cam_a;
+      const double py = 0.5 * height - (pc[1] / -pc[2]) / cam_c;
+      xmin = std::min(xmin, px);
+      xmax = std::max(xmax, px);
+      ymin = std::min(ymin, py);
+      ymax = std::max(ymax, py);
+    }
+    if (!(xmax + margin >= 0.0 && ymax + margin >= 0.0 && xmin - margin < width && ymin - margin < height)) continue;
+    rect[4 * i + 0] = (int32_t)std::max(0.0, std::floor(xmin - margin));
+    rect[4 * i + 1] = (int32_t)std::min((double)width - 1, std::floor(xmax + margin));
+    rect[4 * i + 2] = (int32_t)std::max(0.0, std::floor(ymin - margin));
+    rect[4 * i + 3] = (int32_t)std::min((double)height - 1, std::floor(ymax + margin));
+  }
+  auto emit = [&](size_t i, auto&& put) {
+    if (rect[4 * i] < 0) return;
+    for (int32_t y = rect[4 * i + 2]; y <= rect[4 * i + 3]; ++y)
+      for (int32_t x = rect[4 * i + 0]; x <= rect[4 * i + 1]; ++x) put((size_t)y * (size_t)width + (size_t)x, tris[i].rec);
+  };
+  return fill_bins((size_t)width * (size_t)height, tris.size(), emit, out->off, out->ent, why);
+}
+
+bool build_light_grid(const std::vector<BinTri>& tris, const double w2o[16], const double dir[3],
+                      LightGridHost* out, const char** why) {
+  *why = "";
+  out->g = LightGrid{};
+  const double sd[3] = {-dir[0], -dir[1], -dir[2]};
+  double rd[3];
+  xform_dir(w2o, sd, rd);  // object-space shadow direction (the kernel's rd, up to float32 rounding)
+  const double rlen = norm3(rd);
+  if (!(rlen > 0.0) || !std::isfinite(rlen)) {
+    *why = "degenerate light direction";
+    return false;
+  }
+  const double u[3] = {rd[0] / rlen, rd[1] / rlen, rd[2] / rlen};
+  // basis orthogonal to the shadow direction
+  const int ax = std::fabs(u[0]) <= std::fabs(u[1]) && std::fabs(u[0]) <= std::fabs(u[2]) ? 0
+                 : std::fabs(u[1]) <= std::fabs(u[2])                                 ? 1
+                                                                                      : 2;
+  double a[3] = {0, 0, 0};
+  a[ax] = 1.0;
+  double e1[3], e2[3];
+  cross3(a, u, e1);
+  const double l1 = norm3(e1);
+  for (double& x : e1) x /= l1;
+  cross3(u, e1, e2);
+  double scale = 1.0;
+  for (const BinTri& t : tris)
+    for (int v = 0; v < 3; ++v)
+      for (int k = 0; k < 3; ++k) scale = std::max(scale, std::fabs(t.v[v][k]));
+  const double delta = 1e-5 * scale;
+  std::vector<double> box(tris.size() * 4, NAN);
+  double umin = INFINITY, umax = -INFINITY, vmin = INFINITY, vmax = -INFINITY;
+  size_t kept = 0;
+  for (size_t i = 0; i < tris.size(); ++i) {
+    const BinTri& t = tris[i];
+    double f1[3], f2[3], c[3], nn[3];
+    for (int k = 0; k < 3; ++k) {
+      f1[k] = t.v[1][k] - t.v[0][k];
+      f2[k] = t.v[2][k] - t.v[0][k];
+    }
+    cross3(f1, f2, c);
+    for (int k = 0; k < 3; ++k) nn[k] = -c[k];
+    if (never_passes(dot3(rd, nn), rlen, norm3(nn))) continue;  // faces away from the light
+    double bu0 = INFINITY, bu1 = -INFINITY, bv0 = INFINITY, bv1 = -INFINITY;
+    for (int v = 0; v < 3; ++v) {
+      const double pu = dot3(t.v[v], e1), pv = dot3(t.v[v], e2);
+      bu0 = std::min(bu0, pu);
+      bu1 = std::max(bu1, pu);
+      bv0 = std::min(bv0, pv);
+      bv1 = std::max(bv1, pv);
+    }
+    box[4 * i + 0] = bu0 - delta;
+    box[4 * i + 1] = bu1 + delta;
+    box[4 * i + 2] = bv0 - delta;
+    box[4 * i + 3] = bv1 + delta;
+    umin = std::min(umin, box[4 * i + 0]);
+    umax = std::max(umax, box[4 * i + 1]);
+    vmin = std::min(vmin, box[4 * i + 2]);
+    vmax = std::max(vmax, box[4 * i + 3]);
+    ++kept;
+  }
+  LightGrid& g = out->g;
+  for (int k = 0; k < 3; ++k) {
+    g.e1[k] = (float)e1[k];
+    g.e2[k] = (float)e2[k];
+  }
+  g.rmax = (float)(100.0 * scale);
+  if (kept == 0) {  // nothing faces the light: every lane misses (an empty 1x1 grid)
+    g.u0 = g.v0 = 0.0f;
+    g.inv_h = 1.0f;
+    g.gu = g.gv = 1;
+    out->off.assign(2, 0);
+    out->ent.assign(kBinPad, tris.empty() ? 0 : tris[0].rec);
+    return true;
+  }
+  // about 16 cells per listed face, square cells, at most 4096 per side
+  const double du = std::max(umax - umin, 1e-30), dv = std::max(vmax - vmin, 1e-30);
+  double h = std::sqrt(du * dv / (16.0 * (double)kept));
+  h = std::max(h, std::max(du, dv) / 4096.0);
+  const int gu = std::max(1, std::min(4096, (int)std::ceil(du / h)));
+  const int gv = std::max(1, std::min(4096, (int)std::ceil(dv / h)));
+  // the float32 origin / cell size the kernel uses, so host and device agree on
+  // cell edges up to float32 rounding (covered by delta)
+  g.u0 = (float)umin;
+  g.v0 = (float)vmin;
+  g.inv_h = (float)(1.0 / h);
+  g.gu = gu;
+  g.gv = gv;
+  const double ih = (double)g.inv_h;
+  auto emit = [&](size_t i, auto&& put) {
+    if (std::isnan(box[4 * i])) return;
+    const int c0 = std::max(0, (int)std::floor((box[4 * i + 0] - (double)g.u0) * ih));
+    const int c1 = std::min(gu - 1, (int)std::floor((box[4 * i + 1] - (double)g.u0) * ih));
+    const int r0 = std::max(0, (int)std::floor((box[4 * i + 2] - (double)g.v0) * ih));
+    const int r1 = std::min(gv - 1, (int)std::floor((box[4 * i + 3] - (double)g.v0) * ih));
+    for (int r = r0; r <= r1; ++r)
+      for (int c = c0; c <= c1; ++c) put((size_t)r * (size_t)gu + (size_t)c, tris[i].rec);
+  };
+  return fill_bins((size_t)gu * (size_t)gv, tris.size(), emit, out->off, out->ent, why);
+}
+
+}  // namespace rtmi

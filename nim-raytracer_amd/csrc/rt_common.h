@@ -177,6 +177,23 @@ struct alignas(16) FMesh {
   int32_t normal_base;
 };
 
+// Light grid of one distant light for the float32 kernel (rt_bins.h): the
+// mesh's faces binned by their projection along the object-space shadow
+// direction. gu == 0: no grid for this light.
+struct alignas(16) LightGrid {
+  float e1[3];      // orthonormal basis of the plane orthogonal to the shadow direction
+  float u0;
+  float e2[3];
+  float v0;
+  float inv_h;      // cells per unit
+  float rmax;       // |ro|_inf above this: the lane takes the BVH (float32 error bound)
+  int32_t gu, gv;   // cells along e1 / e2
+  int32_t off_base; // this grid's cell offsets start at FastParams.grid_off[off_base]
+  int32_t ent_base; // added to its offsets: entries in FastParams.grid_ent
+  int32_t pad[2];
+};
+static_assert(sizeof(LightGrid) == 64, "LightGrid must be 64 bytes");
+
 struct alignas(16) FLight {
   int32_t type;
   float ci[3];   // color * intensity
@@ -191,6 +208,11 @@ struct FastParams {
   const FLight* lights;
   const BvhNode* tree;              // nodes (child refs = byte offsets into tree) then TriFast records
   const float* normals;
+  const int32_t* pix_off;          // pixel lists of the mesh (rt_bins.h): y * width + x -> [off, off+1)
+  const int32_t* pix_ent;          //   ... of TriFast byte offsets; nullptr: BVH for camera rays
+  const LightGrid* grids;          // per light, or nullptr: BVH for shadow rays
+  const int32_t* grid_off;
+  const int32_t* grid_ent;
   float* fb;
   unsigned long long* partials;
   unsigned int* queue;             // kQueueShards heads (atomicAdd), zeroed at launch

@@ -250,20 +250,15 @@ __device__ __forceinline__ SlabRay slab_ray(F3 o, F3 d) {
   return r;
 }
 
+// The search state (key, tc) is the caller's (trace()): lanes with tc < 0
+// take no part (never entered, retired, or done by a bin search).
 template <bool COUNT>
-__device__ __forceinline__ void traverse(KP p, int root, F3 o, F3 d, SlabRay sr, bool active, bool early,
-                                         float stop, float& tbest, int& best_id, Stats32& ws) {
-  if (bal(active) == 0ull) return;
+__device__ __forceinline__ void traverse(KP p, int root, F3 o, F3 d, SlabRay sr, bool early, float stop,
+                                         unsigned long long& key, float& tc, Stats32& ws) {
+  if (bal(tc >= 0.0f) == 0ull) return;
   RT_STAMP(t_enter);
   const F3 ni = sr.ni, oi = sr.oi;
   const int lane = (int)__lane_id();
-  float tc = active ? tbest : -1.0f;
-  // Retire only on a FOUND hit: accepted t are < the initial limit tbest, so
-  // clamp stop to the float just below it (tbest > 0; for tbest == 0 the
-  // bit pattern wraps to NaN, fminf keeps stop, and nothing is acceptable).
-  stop = fminf(stop, __uint_as_float(__float_as_uint(tbest) - 1u));
-  const unsigned long long key0 = active ? tkey(tbest, 0u) : 0ull;
-  unsigned long long key = key0;
   int stack = 0;
   int sp = 0;
   int node = root;
@@ -343,13 +338,33 @@ __device__ __forceinline__ void traverse(KP p, int root, F3 o, F3 d, SlabRay sr,
              ((unsigned long long)(unsigned int)__builtin_amdgcn_readlane(mhi, sp) << 32);
     }
   }
-  if (key != key0) {
-    tbest = __uint_as_float((unsigned int)(key >> 32));
-    best_id = (int)(unsigned int)key;
-  }
 #ifdef RTMI_STAMPS
   { RT_STAMP(t_exit); RT_ACC(5, t_enter, t_exit); }
 #endif
+}
+
+// The faces listed at ent[b, e) (a pixel list or a light-grid cell, rt_bins.h)
+// against every lane's ray, with the traversal's key / early-exit rules.
+// ent is padded, so the four-record read-ahead stays inside the array.
+template <bool COUNT>
+__device__ __forceinline__ void list_search(KP p, const int32_t* ent, int b, int e, F3 o, F3 d, bool early,
+                                            float stop, unsigned long long& key, float& tc, Stats32& ws) {
+  if constexpr (COUNT) {
+    ws.v[STAT_TRI_FETCH] += (unsigned int)(e - b);
+    ws.v[STAT_LANE_TRIS] += pc(bal(tc >= 0.0f)) * (unsigned int)(e - b);
+  }
+  for (int k = b; k < e; k += 4) {
+    const RT_CONST int32_t* q = cp(ent) + k;
+    const int r0 = q[0], r1 = q[1], r2 = q[2], r3 = q[3];
+    tri_test(*rec<TriFast>(p, r0), o, d, key, tc);
+    if (k + 1 < e) tri_test(*rec<TriFast>(p, r1), o, d, key, tc);
+    if (k + 2 < e) tri_test(*rec<TriFast>(p, r2), o, d, key, tc);
+    if (k + 3 < e) tri_test(*rec<TriFast>(p, r3), o, d, key, tc);
+    if (early) {
+      tc = tc <= stop ? -1.0f : tc;
+      if (bal(tc >= 0.0f) == 0ull) break;
+    }
+  }
 }
 
 // t of analytic object i in world space, -inf on a miss (Sphere / Plane /
@@ -374,8 +389,10 @@ __device__ __forceinline__ float analytic_t(KP p, const FObj& ob, int i, F3 o, F
 // comparison is decided and the lane retires: exact, not an approximation.
 // Applied when the scene has exactly one mesh object (p->shadow_mesh); stop =
 // min t >= 0 of the analytic objects after the mesh.
+// pix: the camera ray's pixel index (y * width + x; -1 for other rays),
+// light: the shadow ray's light (-1 for other rays); they select the bins.
 template <bool COUNT, unsigned F>
-__device__ __forceinline__ Hit trace(KP p, F3 o, F3 d, float tmax, bool active, bool shadow,
+__device__ __forceinline__ Hit trace(KP p, F3 o, F3 d, float tmax, bool active, bool shadow, int pix, int light,
                                      Stats32& ws) {
   RT_STAMP(t_trace0);
   Hit h{-1, -1, tmax};
@@ -412,9 +429,10 @@ __device__ __forceinline__ Hit trace(KP p, F3 o, F3 d, float tmax, bool active, 
 #endif
       // shadow early exit (above): stop is only computed when some lane of
       // the wave enters the mesh
-      float stop = -1.0f;
       if (ob.root >= 0 && bal(part) != 0ull) {
-        if (early && i == p->shadow_mesh) {
+        const bool ex = early && i == p->shadow_mesh;
+        float stop = -1.0f;
+        if (ex) {
           RT_STAMP(t_st0);
           stop = finf();
           for (int j = i + 1; j < p->nobj; ++j) {
@@ -425,7 +443,55 @@ __device__ __forceinline__ Hit trace(KP p, F3 o, F3 d, float tmax, bool active, 
           { RT_STAMP(t_st1); RT_ACC(7, t_st0, t_st1); }
 #endif
         }
-        traverse<COUNT>(p, ob.root, ro, rd, sr, part, early && i == p->shadow_mesh, stop, tb, best, ws);
+        // search state of the lanes that enter: the best (t, face) key and
+        // the culling limit; a lane retires (early exit) on a FOUND hit with
+        // t <= stop, so stop is clamped to the float just below the initial
+        // limit (tb > 0; for tb == 0 the bit pattern wraps to NaN, fminf
+        // keeps stop, and nothing is acceptable)
+        float tc = part ? tb : -1.0f;
+        stop = fminf(stop, __uint_as_float(__float_as_uint(tb) - 1u));
+        const unsigned long long key0 = part ? tkey(tb, 0u) : 0ull;
+        unsigned long long key = key0;
+        // Coherent families search the faces binned for them (rt_bins.h)
+        // instead of the BVH: camera rays by pixel (pix: this lane's pixel
+        // index, -1 for other rays), shadow rays to a distant light by
+        // light-grid cell. Up to 4 distinct bins per wave; lanes left over
+        // (or off the grid's float32-safe range) take the BVH.
+        int bin = -1;                        // this lane's bin, -1: none
+        const int32_t* boff = nullptr;
+        const int32_t* bent = nullptr;
+        bool nohit = false;                  // off every listed face
+        if ((F & F_MESH) && !shadow && p->pix_off && pix >= 0) {
+          bin = pix;
+          boff = p->pix_off;
+          bent = p->pix_ent;
+        } else if ((F & F_MESH) && shadow && p->grids && light >= 0 && p->grids[light].gu > 0) {
+          const RT_CONST LightGrid& G = cp(p->grids)[light];
+          const float gu = __builtin_fmaf(ro.x, G.e1[0], __builtin_fmaf(ro.y, G.e1[1], ro.z * G.e1[2]));
+          const float gv = __builtin_fmaf(ro.x, G.e2[0], __builtin_fmaf(ro.y, G.e2[1], ro.z * G.e2[2]));
+          const float fu = (gu - G.u0) * G.inv_h, fv = (gv - G.v0) * G.inv_h;
+          const bool safe = fmaxf(fmaxf(fabsf(ro.x), fabsf(ro.y)), fabsf(ro.z)) <= G.rmax;
+          const bool on = fu >= 0.0f && fu < (float)G.gu && fv >= 0.0f && fv < (float)G.gv;
+          bin = safe && on ? G.off_base + (int)fv * G.gu + (int)fu : -1;
+          nohit = safe && !on;
+          boff = p->grid_off;
+          bent = p->grid_ent + G.ent_base;
+        }
+        if (boff) {
+          unsigned long long todo = bal(part && bin >= 0);
+          for (int it = 0; it < 4 && todo != 0ull; ++it) {
+            const int kb = __builtin_amdgcn_readlane(bin, (int)__builtin_ctzll(todo));
+            todo &= ~bal(bin == kb);
+            list_search<COUNT>(p, bent, cp(boff)[kb], cp(boff)[kb + 1], ro, rd, ex, stop, key, tc, ws);
+          }
+          // done: binned lanes (their bin was searched) and lanes off the grid
+          tc = (lane_in(todo) || !(bin >= 0 || nohit)) ? tc : -1.0f;
+        }
+        traverse<COUNT>(p, ob.root, ro, rd, sr, ex, stop, key, tc, ws);
+        if (key != key0) {
+          tb = __uint_as_float((unsigned int)(key >> 32));
+          best = (int)(unsigned int)key;
+        }
       }
       t = !in ? -finf() : (best >= 0 ? tb : finf());
       tri = best;
@@ -522,15 +588,17 @@ __device__ __forceinline__ F3 lds_get3(LdsF* ls, int slot) {
 //  * renderer.nim:104-124: reflection > 0 and depth <= maxRayDepth traces
 //    r = i - 2 (n.i) n from hitW + r*bias; the level's local light is
 //    weighted (1 - reflection), the reflected colour reflection.
+// pix: the sample's pixel index (y * width + x) for the camera ray's bins.
 template <bool COUNT, unsigned F>
-__device__ __forceinline__ void shade_path(KP p, F3 o, F3 d, bool active, LdsF* ls, Acc& acc, Stats32& ws) {
+__device__ __forceinline__ void shade_path(KP p, F3 o, F3 d, bool active, int pix, LdsF* ls, Acc& acc,
+                                           Stats32& ws) {
   bool act = active;
   int depth = 1;
   float w = 1.0f;
   for (int lev = 0; lev < ((F & F_REFLECT) ? kMaxShadeLevels : 1); ++lev) {
     p = params();
     if (bal(act) == 0ull) break;
-    const Hit hit = trace<COUNT, F>(p, o, d, finf(), act, false, ws);
+    const Hit hit = trace<COUNT, F>(p, o, d, finf(), act, false, lev == 0 ? pix : -1, -1, ws);
     if (act && hit.obj < 0) acc_add3(acc, w * p->bg[0], w * p->bg[1], w * p->bg[2]);
     const bool lit = act && hit.obj >= 0;
     const F3 hw = f3(__builtin_fmaf(d.x, hit.t, o.x), __builtin_fmaf(d.y, hit.t, o.y), __builtin_fmaf(d.z, hit.t, o.z));
@@ -541,14 +609,23 @@ __device__ __forceinline__ void shade_path(KP p, F3 o, F3 d, bool active, LdsF* 
     while (pending) {  // one pass per distinct object hit by the wave
       const int lead = (int)__builtin_ctzll(pending);
       const int oi = __builtin_amdgcn_readlane(hit.obj, lead);
-      const bool mine = lit && hit.obj == oi;
+      // `mine` compares against an opaque copy: knowing hit.obj == oi inside
+      // the branch, the compiler would otherwise address the object's
+      // uniform records through the per-lane hit.obj (vector loads on the
+      // sample's critical path instead of scalar loads)
+      int oi_cmp = oi;
+      asm volatile("" : "+s"(oi_cmp));
+      const bool mine = lit && hit.obj == oi_cmp;
       pending &= ~bal(mine);
       const FObj ob = cp(p->objs)[oi];
       const RT_CONST FObjX& ox = cp(p->objx)[oi];
+      const F3 oalb = f3(ox.albedo_pi[0], ox.albedo_pi[1], ox.albedo_pi[2]);
+      const float orefl = ox.refl;
+      const int nbase = ox.normal_base;
       if (mine) {
         F3 n;
         if ((F & F_MESH) && ob.type == GEOM_MESH) {
-          const float* fn = p->normals + 3 * (size_t)(ox.normal_base + hit.tri);
+          const float* fn = p->normals + 3 * (size_t)(nbase + hit.tri);
           n = f3(fn[0], fn[1], fn[2]);
         } else {
           F3 ho, unused;
@@ -563,8 +640,8 @@ __device__ __forceinline__ void shade_path(KP p, F3 o, F3 d, bool active, LdsF* 
         } else {
           N = n;
         }
-        alb = f3(ox.albedo_pi[0], ox.albedo_pi[1], ox.albedo_pi[2]);
-        refl = ox.refl;
+        alb = oalb;
+        refl = orefl;
       }
     }
     const bool reflect = (F & F_REFLECT) && lit && refl > 0.0f && depth <= p->max_depth;
@@ -601,7 +678,7 @@ __device__ __forceinline__ void shade_path(KP p, F3 o, F3 d, bool active, LdsF* 
         dist = finf();
       }
       ws.v[STAT_SHADOW] += pc(bal(lit));
-      const Hit sh = trace<COUNT, F>(p, so, sd, dist, lit, true, ws);
+      const Hit sh = trace<COUNT, F>(p, so, sd, dist, lit, true, -1, li, ws);
       if (lit && sh.obj < 0) {  // shadeDiffuse (shader.nim:12-17)
         const float ndl = fmaxf(dot3(N, sd), 0.0f) * k;
         acc_add3(acc, albw.x * L.ci[0] * ndl, albw.y * L.ci[1] * ndl, albw.z * L.ci[2] * ndl);
@@ -797,7 +874,7 @@ __global__ __launch_bounds__(256) RTMI_OCC void k_render_fast(const FastParams p
       const F3 o = f3(p->cam[0], p->cam[1], p->cam[2]);
       ws.v[STAT_PRIMARY] += pc(bal(sv));
       RT_STAMP(t_s0);
-      shade_path<COUNT, F>(p, o, d, sv, ls, pacc, ws);
+      shade_path<COUNT, F>(p, o, d, sv, sv ? gp.y * p->width + gp.x : -1, ls, pacc, ws);
 #if RTMI_STAMPS == 1
       { RT_STAMP(t_s1); RT_ACC(7, t_s0, t_s1); }
 #endif

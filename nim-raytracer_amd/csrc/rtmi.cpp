@@ -23,6 +23,7 @@
 #include <vector>
 
 #include "../../include/rtmi.h"
+#include "rt_bins.h"
 #include "rt_bvh.h"
 #include "rt_common.h"
 
@@ -164,6 +165,23 @@ struct rt_scene {
     }
   };
   std::vector<std::unique_ptr<Order>> orders;  // most recently used first, at most 8
+  // bins of the float32 kernel (rt_bins.h), for the scene's only mesh object
+  std::vector<BinTri> bin_tris;    // its faces (object space) + TriFast byte offsets
+  double mesh_o2w[16], mesh_w2o[16];
+  bool binnable = false;
+  DevBuf<LightGrid> grids;         // per light (gu == 0: none)
+  DevBuf<int32_t> grid_off, grid_ent;
+  bool has_grids = false;
+  struct PixelBins {               // camera-ray lists of one image size
+    int w = 0, h = 0;
+    bool ok = false;
+    DevBuf<int32_t> off, ent;
+    ~PixelBins() {
+      off.release();
+      ent.release();
+    }
+  };
+  std::vector<std::unique_ptr<PixelBins>> pixel_bins;  // most recently used first, at most 4
   DevBuf<float> fb_scratch;
   int max_waves = 0;
   int64_t num_triangles = 0, num_nodes = 0;
@@ -179,6 +197,10 @@ struct rt_scene {
     f64_tables.release();
     acc.release();
     fb_scratch.release();
+    grids.release();
+    grid_off.release();
+    grid_ent.release();
+    pixel_bins.clear();
     if (done) (void)hipEventDestroy(done);
     if (stream) (void)hipStreamDestroy(stream);
   }
@@ -713,6 +735,51 @@ extern "C" int rt_scene_create(const rt_scene_desc* d, rt_scene** out_scene) {
     if (!fn.empty())
       HIP_TRY(hipMemcpy(s->f32.tree.p, fn.data(), fn.size() * sizeof(BvhNode), hipMemcpyHostToDevice));
   }
+  if (s->shadow_mesh >= 0) {  // bins of the only mesh object (rt_bins.h)
+    const rt_object_desc& ob = d->objects[s->shadow_mesh];
+    const int m = ob.mesh;
+    const rt_mesh_desc& md = d->meshes[m];
+    int64_t base = 0;
+    for (int k = 0; k < m; ++k) base += d->meshes[k].num_faces;
+    const std::vector<int32_t>& order = bvhs[(size_t)m].order;
+    s->bin_tris.resize(order.size());
+    parallel_for((int64_t)order.size(), [&](int64_t b, int64_t e) {
+      for (int64_t i = b; i < e; ++i) {
+        BinTri& t = s->bin_tris[(size_t)i];
+        const int32_t* fi = &md.faces[3 * (size_t)order[(size_t)i]];
+        for (int v = 0; v < 3; ++v)
+          for (int k = 0; k < 3; ++k) t.v[v][k] = md.vertices[3 * (size_t)fi[v] + k];
+        t.rec = (int32_t)((nnodes + base + i) * (int64_t)sizeof(TriFast));
+      }
+    });
+    std::memcpy(s->mesh_o2w, ob.object_to_world, sizeof s->mesh_o2w);
+    std::memcpy(s->mesh_w2o, ob.world_to_object, sizeof s->mesh_w2o);
+    s->binnable = !s->bin_tris.empty();
+    // light grids of the distant lights
+    std::vector<LightGrid> gh((size_t)std::max(1, d->num_lights), LightGrid{});
+    std::vector<int32_t> goff, gent;
+    bool any = false;
+    for (int li = 0; s->binnable && li < d->num_lights; ++li) {
+      if (d->lights[li].type == RT_POINT_LIGHT) continue;
+      LightGridHost lg;
+      const char* why = "";
+      if (!build_light_grid(s->bin_tris, s->mesh_w2o, d->lights[li].dir, &lg, &why)) continue;
+      if ((int64_t)goff.size() + (int64_t)lg.off.size() > INT32_MAX ||
+          (int64_t)gent.size() + (int64_t)lg.ent.size() > INT32_MAX)
+        break;
+      lg.g.off_base = (int32_t)goff.size();
+      lg.g.ent_base = (int32_t)gent.size();
+      goff.insert(goff.end(), lg.off.begin(), lg.off.end());
+      gent.insert(gent.end(), lg.ent.begin(), lg.ent.end());
+      gh[(size_t)li] = lg.g;
+      any = true;
+    }
+    if (any) {
+      if ((rc = s->grids.upload(gh)) || (rc = s->grid_off.upload(goff)) || (rc = s->grid_ent.upload(gent))) return rc;
+      s->has_grids = true;
+    }
+    mark("light grids");
+  }
   s->max_waves = s->num_cus * 8 * 4;  // 8 blocks of 4 waves per CU at most
   if ((rc = s->partials.alloc((size_t)s->max_waves * kStatSlots))) return rc;
   if ((rc = s->acc.alloc(kStatSlots))) return rc;
@@ -955,6 +1022,28 @@ OrderUse group_order(rt_scene* s, const rt_options* o, const Mapping& mp, const 
   return u;
 }
 
+// Camera-ray lists for one image size (rt_bins.h), built on first use and
+// cached; nullptr when the camera set-up does not allow them (the kernel then
+// traverses the BVH).
+const rt_scene::PixelBins* pixel_bins(rt_scene* s, int w, int h) {
+  size_t i = 0;
+  while (i < s->pixel_bins.size() && !(s->pixel_bins[i]->w == w && s->pixel_bins[i]->h == h)) ++i;
+  if (i == s->pixel_bins.size()) {
+    std::unique_ptr<rt_scene::PixelBins> pb(new rt_scene::PixelBins());
+    pb->w = w;
+    pb->h = h;
+    PixelBinsHost hb;
+    const char* why = "";
+    pb->ok = build_pixel_bins(s->bin_tris, s->mesh_o2w, s->mesh_w2o, s->c2w, s->fov, w, h, &hb, &why) &&
+             pb->off.upload(hb.off) == RT_OK && pb->ent.upload(hb.ent) == RT_OK;
+    s->pixel_bins.insert(s->pixel_bins.begin(), std::move(pb));
+    if (s->pixel_bins.size() > 4) s->pixel_bins.pop_back();
+    i = 0;
+  }
+  std::rotate(s->pixel_bins.begin(), s->pixel_bins.begin() + (long)i, s->pixel_bins.begin() + (long)i + 1);
+  return s->pixel_bins[0]->ok ? s->pixel_bins[0].get() : nullptr;
+}
+
 void fill_fast(rt_scene* s, const rt_options* o, const Mapping& mp, float* fb, FastParams& p, int* blocks,
                rt_scene::Order** measuring) {
   std::memset(&p, 0, sizeof p);
@@ -1018,6 +1107,20 @@ void fill_fast(rt_scene* s, const rt_options* o, const Mapping& mp, float* fb, F
   p.inv_band_h = mp.band_h > 0 ? (float)(1.0 / (double)mp.band_h) : 0.0f;
   p.tiles_x = pl.tiles_x;
   p.ngroups = pl.ngroups;
+  // binned searches (rt_bins.h): camera rays when a wave spans at most 4
+  // pixels (>= 16 samples per pixel), shadow rays to distant lights
+  if (!(o->flags & RT_FLAG_NO_BINNING)) {
+    if (s->binnable && pl.L >= 16)
+      if (const rt_scene::PixelBins* pb = pixel_bins(s, o->width, o->height)) {
+        p.pix_off = pb->off.p;
+        p.pix_ent = pb->ent.p;
+      }
+    if (s->has_grids) {
+      p.grids = s->grids.p;
+      p.grid_off = s->grid_off.p;
+      p.grid_ent = s->grid_ent.p;
+    }
+  }
   // one work item per dequeue: per-pixel cost varies ~10x (sky vs bunny +
   // shadows), so coarser chunks leave an expensive tail in every launch
   // (C3 whole frame: 4 groups per dequeue 9.79 ms, 1 9.49 ms; 2-way bands:
