@@ -410,91 +410,108 @@ __device__ __forceinline__ Hit trace(KP p, F3 o, F3 d, float tmax, bool active, 
       RT_STAMP(t_g0);
       F3 ro, rd;
       to_object<F>(p, ob, i, o, d, ro, rd);
-      // TriangleMesh.intersect (geom.nim:339-358): a ray starting inside
-      // the mesh AABB misses (entry t < 0); otherwise the closest face. The
-      // AABB and the root ride in the object record (no dependent FMesh
-      // fetch); the gate uses the traversal's slab form of the ray.
-      const SlabRay sr = slab_ray(ro, rd);
-      const float ax = __builtin_fmaf(ob.lo[0], sr.ni.x, -sr.oi.x), bx = __builtin_fmaf(ob.hi[0], sr.ni.x, -sr.oi.x);
-      const float ay = __builtin_fmaf(ob.lo[1], sr.ni.y, -sr.oi.y), by = __builtin_fmaf(ob.hi[1], sr.ni.y, -sr.oi.y);
-      const float az = __builtin_fmaf(ob.lo[2], sr.ni.z, -sr.oi.z), bz = __builtin_fmaf(ob.hi[2], sr.ni.z, -sr.oi.z);
-      const float gmin = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
-      const float gmax = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz)) * 1.00000024f;
-      const bool in = gmin <= gmax && gmin >= 0.0f;
-      const bool part = active && in;
-      float tb = h.t;
-      int best = -1;
-#if RTMI_STAMPS == 2
-      { RT_STAMP(t_g1); RT_ACC(8, t_g0, t_g1); }
-#endif
-      // shadow early exit (above): stop is only computed when some lane of
-      // the wave enters the mesh
-      if (ob.root >= 0 && bal(part) != 0ull) {
-        const bool ex = early && i == p->shadow_mesh;
-        float stop = -1.0f;
-        if (ex) {
-          RT_STAMP(t_st0);
-          stop = finf();
-          for (int j = i + 1; j < p->nobj; ++j) {
-            const float tj = analytic_t<F>(p, cp(p->objs)[j], j, o, d);
-            stop = tj >= 0.0f ? fminf(stop, tj) : stop;
+      // Coherent families search the faces binned for them (rt_bins.h)
+      // instead of the BVH: camera rays by pixel (pix: this lane's pixel
+      // index, -1 for other rays), shadow rays to a distant light by
+      // light-grid cell. A lane whose bin is empty, or that is off the grid,
+      // can hit no face; when a camera wave's one pixel has an empty list
+      // the mesh is skipped before the AABB gate (no lane can produce a hit,
+      // so the gate's verdict cannot matter).
+      int bin = -1;                        // this lane's bin, -1: none
+      const int32_t* boff = nullptr;
+      const int32_t* bent = nullptr;
+      bool nohit = false;                  // off every listed face
+      bool skip = false;                   // wave-uniform: no lane can hit the mesh
+      if ((F & F_MESH) && !shadow && p->pix_off && pix >= 0) {
+        bin = pix;
+        boff = p->pix_off;
+        bent = p->pix_ent;
+        if (p->lanes_per_px == 64) {  // one pixel per wave: its list length decides
+          const unsigned long long pm = bal(active && pix >= 0);
+          if (pm != 0ull) {
+            const int up = __builtin_amdgcn_readlane(pix, (int)__builtin_ctzll(pm));
+            skip = cp(boff)[up] == cp(boff)[up + 1];
           }
-#if RTMI_STAMPS == 2
-          { RT_STAMP(t_st1); RT_ACC(7, t_st0, t_st1); }
-#endif
-        }
-        // search state of the lanes that enter: the best (t, face) key and
-        // the culling limit; a lane retires (early exit) on a FOUND hit with
-        // t <= stop, so stop is clamped to the float just below the initial
-        // limit (tb > 0; for tb == 0 the bit pattern wraps to NaN, fminf
-        // keeps stop, and nothing is acceptable)
-        float tc = part ? tb : -1.0f;
-        stop = fminf(stop, __uint_as_float(__float_as_uint(tb) - 1u));
-        const unsigned long long key0 = part ? tkey(tb, 0u) : 0ull;
-        unsigned long long key = key0;
-        // Coherent families search the faces binned for them (rt_bins.h)
-        // instead of the BVH: camera rays by pixel (pix: this lane's pixel
-        // index, -1 for other rays), shadow rays to a distant light by
-        // light-grid cell. Up to 4 distinct bins per wave; lanes left over
-        // (or off the grid's float32-safe range) take the BVH.
-        int bin = -1;                        // this lane's bin, -1: none
-        const int32_t* boff = nullptr;
-        const int32_t* bent = nullptr;
-        bool nohit = false;                  // off every listed face
-        if ((F & F_MESH) && !shadow && p->pix_off && pix >= 0) {
-          bin = pix;
-          boff = p->pix_off;
-          bent = p->pix_ent;
-        } else if ((F & F_MESH) && shadow && p->grids && light >= 0 && p->grids[light].gu > 0) {
-          const RT_CONST LightGrid& G = cp(p->grids)[light];
-          const float gu = __builtin_fmaf(ro.x, G.e1[0], __builtin_fmaf(ro.y, G.e1[1], ro.z * G.e1[2]));
-          const float gv = __builtin_fmaf(ro.x, G.e2[0], __builtin_fmaf(ro.y, G.e2[1], ro.z * G.e2[2]));
-          const float fu = (gu - G.u0) * G.inv_h, fv = (gv - G.v0) * G.inv_h;
-          const bool safe = fmaxf(fmaxf(fabsf(ro.x), fabsf(ro.y)), fabsf(ro.z)) <= G.rmax;
-          const bool on = fu >= 0.0f && fu < (float)G.gu && fv >= 0.0f && fv < (float)G.gv;
-          bin = safe && on ? G.off_base + (int)fv * G.gu + (int)fu : -1;
-          nohit = safe && !on;
-          boff = p->grid_off;
-          bent = p->grid_ent + G.ent_base;
-        }
-        if (boff) {
-          unsigned long long todo = bal(part && bin >= 0);
-          for (int it = 0; it < 4 && todo != 0ull; ++it) {
-            const int kb = __builtin_amdgcn_readlane(bin, (int)__builtin_ctzll(todo));
-            todo &= ~bal(bin == kb);
-            list_search<COUNT>(p, bent, cp(boff)[kb], cp(boff)[kb + 1], ro, rd, ex, stop, key, tc, ws);
-          }
-          // done: binned lanes (their bin was searched) and lanes off the grid
-          tc = (lane_in(todo) || !(bin >= 0 || nohit)) ? tc : -1.0f;
-        }
-        traverse<COUNT>(p, ob.root, ro, rd, sr, ex, stop, key, tc, ws);
-        if (key != key0) {
-          tb = __uint_as_float((unsigned int)(key >> 32));
-          best = (int)(unsigned int)key;
         }
       }
-      t = !in ? -finf() : (best >= 0 ? tb : finf());
-      tri = best;
+      if (skip) {
+        t = -finf();
+      } else {
+        // TriangleMesh.intersect (geom.nim:339-358): a ray starting inside
+        // the mesh AABB misses (entry t < 0); otherwise the closest face.
+        // The AABB and the root ride in the object record (no dependent
+        // FMesh fetch); the gate uses the traversal's slab form of the ray.
+        const SlabRay sr = slab_ray(ro, rd);
+        const float ax = __builtin_fmaf(ob.lo[0], sr.ni.x, -sr.oi.x), bx = __builtin_fmaf(ob.hi[0], sr.ni.x, -sr.oi.x);
+        const float ay = __builtin_fmaf(ob.lo[1], sr.ni.y, -sr.oi.y), by = __builtin_fmaf(ob.hi[1], sr.ni.y, -sr.oi.y);
+        const float az = __builtin_fmaf(ob.lo[2], sr.ni.z, -sr.oi.z), bz = __builtin_fmaf(ob.hi[2], sr.ni.z, -sr.oi.z);
+        const float gmin = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
+        const float gmax = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz)) * 1.00000024f;
+        const bool in = gmin <= gmax && gmin >= 0.0f;
+        const bool part = active && in;
+        float tb = h.t;
+        int best = -1;
+#if RTMI_STAMPS == 2
+        { RT_STAMP(t_g1); RT_ACC(8, t_g0, t_g1); }
+#endif
+        // shadow early exit (above): stop is only computed when some lane of
+        // the wave enters the mesh
+        if (ob.root >= 0 && bal(part) != 0ull) {
+          const bool ex = early && i == p->shadow_mesh;
+          float stop = -1.0f;
+          if (ex) {
+            RT_STAMP(t_st0);
+            stop = finf();
+            for (int j = i + 1; j < p->nobj; ++j) {
+              const float tj = analytic_t<F>(p, cp(p->objs)[j], j, o, d);
+              stop = tj >= 0.0f ? fminf(stop, tj) : stop;
+            }
+#if RTMI_STAMPS == 2
+            { RT_STAMP(t_st1); RT_ACC(7, t_st0, t_st1); }
+#endif
+          }
+          // search state of the lanes that enter: the best (t, face) key and
+          // the culling limit; a lane retires (early exit) on a FOUND hit
+          // with t <= stop, so stop is clamped to the float just below the
+          // initial limit (tb > 0; for tb == 0 the bit pattern wraps to NaN,
+          // fminf keeps stop, and nothing is acceptable)
+          float tc = part ? tb : -1.0f;
+          stop = fminf(stop, __uint_as_float(__float_as_uint(tb) - 1u));
+          const unsigned long long key0 = part ? tkey(tb, 0u) : 0ull;
+          unsigned long long key = key0;
+          // shadow rays: the light-grid cell (after the gate: the cell
+          // costs more than the gate, which already sends most waves away)
+          if ((F & F_MESH) && shadow && p->grids && light >= 0 && p->grids[light].gu > 0) {
+            const RT_CONST LightGrid& G = cp(p->grids)[light];
+            const float gu = __builtin_fmaf(ro.x, G.e1[0], __builtin_fmaf(ro.y, G.e1[1], ro.z * G.e1[2]));
+            const float gv = __builtin_fmaf(ro.x, G.e2[0], __builtin_fmaf(ro.y, G.e2[1], ro.z * G.e2[2]));
+            const float fu = (gu - G.u0) * G.inv_h, fv = (gv - G.v0) * G.inv_h;
+            const bool safe = fmaxf(fmaxf(fabsf(ro.x), fabsf(ro.y)), fabsf(ro.z)) <= G.rmax;
+            const bool on = fu >= 0.0f && fu < (float)G.gu && fv >= 0.0f && fv < (float)G.gv;
+            bin = safe && on ? G.off_base + (int)fv * G.gu + (int)fu : -1;
+            nohit = safe && !on;
+            boff = p->grid_off;
+            bent = p->grid_ent + G.ent_base;
+          }
+          if (boff) {  // up to 4 distinct bins per wave; lanes left over take the BVH
+            unsigned long long todo = bal(part && bin >= 0);
+            for (int it = 0; it < 4 && todo != 0ull; ++it) {
+              const int kb = __builtin_amdgcn_readlane(bin, (int)__builtin_ctzll(todo));
+              todo &= ~bal(bin == kb);
+              list_search<COUNT>(p, bent, cp(boff)[kb], cp(boff)[kb + 1], ro, rd, ex, stop, key, tc, ws);
+            }
+            // done: binned lanes (their bin was searched) and lanes off the grid
+            tc = (lane_in(todo) || !(bin >= 0 || nohit)) ? tc : -1.0f;
+          }
+          traverse<COUNT>(p, ob.root, ro, rd, sr, ex, stop, key, tc, ws);
+          if (key != key0) {
+            tb = __uint_as_float((unsigned int)(key >> 32));
+            best = (int)(unsigned int)key;
+          }
+        }
+        t = !in ? -finf() : (best >= 0 ? tb : finf());
+        tri = best;
+      }
     }
 #if RTMI_FCMP_MASKS
     const unsigned long long um = m_ge(t, 0.0f) & m_lt(t, h.t) & actm;
