@@ -74,6 +74,24 @@ inline bool never_passes(double det_upper, double rd_max, double nlen) {
   return det_upper + 1e-6 * rd_max * nlen < 1e-6;
 }
 
+// Separating-axis test of a 2D triangle against the box [x0, x1] x [y0, y1]
+// (the box axes are the caller's bounding-rectangle loop): false only when
+// one triangle edge has all four box corners strictly outside it.
+inline bool tri_meets_box(const double* q, double x0, double y0, double x1, double y1) {
+  const double area = (q[2] - q[0]) * (q[5] - q[1]) - (q[3] - q[1]) * (q[4] - q[0]);
+  if (!(area != 0.0)) return true;  // degenerate (or NaN): keep
+  const double sg = area > 0.0 ? 1.0 : -1.0;
+  const double cx[4] = {x0, x1, x0, x1}, cy[4] = {y0, y0, y1, y1};
+  for (int k = 0; k < 3; ++k) {
+    const double ax = q[2 * k], ay = q[2 * k + 1];
+    const double bx = q[2 * ((k + 1) % 3)], by = q[2 * ((k + 1) % 3) + 1];
+    double best = -INFINITY;
+    for (int c = 0; c < 4; ++c) best = std::max(best, sg * ((bx - ax) * (cy[c] - ay) - (by - ay) * (cx[c] - ax)));
+    if (best < 0.0) return false;
+  }
+  return true;
+}
+
 // Two-pass bucket fill: count[k] entries per bin -> off (prefix) -> ent.
 template <class Emit>
 bool fill_bins(size_t nbins, size_t ntri, Emit emit, std::vector<int32_t>& off, std::vector<int32_t>& ent,
@@ -120,8 +138,9 @@ bool build_pixel_bins(const std::vector<BinTri>& tris, const double o2w[16], con
   // |rd| of a unit world direction lies in [1/|o2w|, |w2o|]
   const double rd_max = frob3(w2o), rd_min = 1.0 / frob3(o2w);
   const double margin = 0.05;  // pixels
-  // per face: pixel rectangle, or empty
+  // per face: pixel rectangle (or empty) and projected vertices
   std::vector<int32_t> rect(tris.size() * 4, -1);
+  std::vector<double> proj(tris.size() * 6, 0.0);
   for (size_t i = 0; i < tris.size(); ++i) {
     const BinTri& t = tris[i];
     double e1[3], e2[3], c[3], nn[3], dc[3];
@@ -152,6 +171,8 @@ bool build_pixel_bins(const std::vector<BinTri>& tris, const double o2w[16], con
       }
       const double px = 0.5 * width + (pc[0] / -pc[2]) / cam_a;
       const double py = 0.5 * height - (pc[1] / -pc[2]) / cam_c;
+      proj[6 * i + 2 * v] = px;
+      proj[6 * i + 2 * v + 1] = py;
       xmin = std::min(xmin, px);
       xmax = std::max(xmax, px);
       ymin = std::min(ymin, py);
@@ -165,8 +186,11 @@ bool build_pixel_bins(const std::vector<BinTri>& tris, const double o2w[16], con
   }
   auto emit = [&](size_t i, auto&& put) {
     if (rect[4 * i] < 0) return;
+    const double* q = &proj[6 * i];
     for (int32_t y = rect[4 * i + 2]; y <= rect[4 * i + 3]; ++y)
-      for (int32_t x = rect[4 * i + 0]; x <= rect[4 * i + 1]; ++x) put((size_t)y * (size_t)width + (size_t)x, tris[i].rec);
+      for (int32_t x = rect[4 * i + 0]; x <= rect[4 * i + 1]; ++x)
+        if (tri_meets_box(q, x - margin, y - margin, x + 1 + margin, y + 1 + margin))
+          put((size_t)y * (size_t)width + (size_t)x, tris[i].rec);
   };
   return fill_bins((size_t)width * (size_t)height, tris.size(), emit, out->off, out->ent, why);
 }
@@ -200,7 +224,7 @@ bool build_light_grid(const std::vector<BinTri>& tris, const double w2o[16], con
     for (int v = 0; v < 3; ++v)
       for (int k = 0; k < 3; ++k) scale = std::max(scale, std::fabs(t.v[v][k]));
   const double delta = 1e-5 * scale;
-  std::vector<double> box(tris.size() * 4, NAN);
+  std::vector<double> box(tris.size() * 4, NAN), proj(tris.size() * 6, 0.0);
   double umin = INFINITY, umax = -INFINITY, vmin = INFINITY, vmax = -INFINITY;
   size_t kept = 0;
   for (size_t i = 0; i < tris.size(); ++i) {
@@ -216,6 +240,8 @@ bool build_light_grid(const std::vector<BinTri>& tris, const double w2o[16], con
     double bu0 = INFINITY, bu1 = -INFINITY, bv0 = INFINITY, bv1 = -INFINITY;
     for (int v = 0; v < 3; ++v) {
       const double pu = dot3(t.v[v], e1), pv = dot3(t.v[v], e2);
+      proj[6 * i + 2 * v] = pu;
+      proj[6 * i + 2 * v + 1] = pv;
       bu0 = std::min(bu0, pu);
       bu1 = std::max(bu1, pu);
       bv0 = std::min(bv0, pv);
@@ -273,8 +299,13 @@ bool build_light_grid(const std::vector<BinTri>& tris, const double w2o[16], con
     const int c1 = std::min(gu - 1, (int)std::floor((box[4 * i + 1] - (double)g.u0) * ih));
     const int r0 = std::max(0, (int)std::floor((box[4 * i + 2] - (double)g.v0) * ih));
     const int r1 = std::min(gv - 1, (int)std::floor((box[4 * i + 3] - (double)g.v0) * ih));
+    const double* q = &proj[6 * i];
     for (int r = r0; r <= r1; ++r)
-      for (int c = c0; c <= c1; ++c) put((size_t)r * (size_t)gu + (size_t)c, tris[i].rec);
+      for (int c = c0; c <= c1; ++c) {
+        const double cu0 = (double)g.u0 + c / ih, cv0 = (double)g.v0 + r / ih;
+        if (tri_meets_box(q, cu0 - delta, cv0 - delta, cu0 + 1.0 / ih + delta, cv0 + 1.0 / ih + delta))
+          put((size_t)r * (size_t)gu + (size_t)c, tris[i].rec);
+      }
   };
   return fill_bins((size_t)gu * (size_t)gv, tris.size(), emit, out->off, out->ent, why);
 }
