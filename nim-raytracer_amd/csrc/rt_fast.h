@@ -51,6 +51,14 @@ __device__ __forceinline__ const RT_CONST T* cp(const T* p) {
   return (const RT_CONST T*)(p);
 }
 
+// Record i of a small scene array (objects, lights: < 2^25 records) at a
+// 32-bit byte offset: s_load with an SGPR offset, one shift instead of the
+// 64-bit address arithmetic per object / light visit.
+template <class T>
+__device__ __forceinline__ const RT_CONST T& at(const T* base, int i) {
+  return *(const RT_CONST T*)((const RT_CONST char*)base + (unsigned)i * (unsigned)sizeof(T));
+}
+
 __device__ __forceinline__ unsigned long long bal(bool p) { return __builtin_amdgcn_ballot_w64(p); }
 // Lane masks straight from a v_cmp (llvm.amdgcn.fcmp: ordered >= / <) and a
 // mask back to a per-lane predicate (llvm.amdgcn.inverse.ballot): a ballot of
@@ -119,14 +127,13 @@ struct Hit {
 template <unsigned F>
 __device__ __forceinline__ void to_object(KP p, const FObj& ob, int i, F3 o, F3 d, F3& ro,
                                           F3& rd) {
-  if (ob.xf == XF_IDENTITY) {
-    ro = o;
-    rd = d;
-  } else if (!(F & F_XF_GENERAL) || ob.xf == XF_TRANSLATE) {
+  // identity and translation alike: the identity's translation is 0 (three
+  // adds instead of a scalar compare + selects per object visit)
+  if (!(F & F_XF_GENERAL) || ob.xf != XF_GENERAL) {
     ro = f3(o.x + ob.t[0], o.y + ob.t[1], o.z + ob.t[2]);
     rd = d;
   } else {
-    const RT_CONST FObjX& x = cp(p->objx)[i];
+    const RT_CONST FObjX& x = at(p->objx, i);
     const float* m = x.w2o;  // m[c*3 + r], c = 0..3
     ro = f3(__builtin_fmaf(m[0], o.x, __builtin_fmaf(m[3], o.y, __builtin_fmaf(m[6], o.z, m[9]))),
             __builtin_fmaf(m[1], o.x, __builtin_fmaf(m[4], o.y, __builtin_fmaf(m[7], o.z, m[10]))),
@@ -373,7 +380,8 @@ template <unsigned F>
 __device__ __forceinline__ float analytic_t(KP p, const FObj& ob, int i, F3 o, F3 d) {
   F3 ro, rd;
   to_object<F>(p, ob, i, o, d, ro, rd);
-  if ((F & F_PLANE) && ob.type == GEOM_PLANE) return plane(ro, rd);
+  // without spheres and boxes in the scene every analytic object is a plane
+  if (!(F & (F_SPHERE | F_BOX)) || ob.type == GEOM_PLANE) return plane(ro, rd);
   if ((F & F_SPHERE) && ob.type == GEOM_SPHERE) return sphere(ob.r, ro, rd);
   if (F & F_BOX) return aabb(ob.lo, ob.hi, ro, f3(rcp(rd.x), rcp(rd.y), rcp(rd.z)));
   return -finf();
@@ -401,7 +409,7 @@ __device__ __forceinline__ Hit trace(KP p, F3 o, F3 d, float tmax, bool active, 
   const unsigned long long actm = bal(active);
 #endif
   for (int i = 0; i < p->nobj; ++i) {
-    const FObj ob = cp(p->objs)[i];
+    const FObj ob = at(p->objs, i);
     float t;
     int tri = -1;
     if (!(F & F_MESH) || ob.type != GEOM_MESH) {
@@ -463,7 +471,7 @@ __device__ __forceinline__ Hit trace(KP p, F3 o, F3 d, float tmax, bool active, 
             RT_STAMP(t_st0);
             stop = finf();
             for (int j = i + 1; j < p->nobj; ++j) {
-              const float tj = analytic_t<F>(p, cp(p->objs)[j], j, o, d);
+              const float tj = analytic_t<F>(p, at(p->objs, j), j, o, d);
               stop = tj >= 0.0f ? fminf(stop, tj) : stop;
             }
 #if RTMI_STAMPS == 2
@@ -634,8 +642,8 @@ __device__ __forceinline__ void shade_path(KP p, F3 o, F3 d, bool active, int pi
       asm volatile("" : "+s"(oi_cmp));
       const bool mine = lit && hit.obj == oi_cmp;
       pending &= ~bal(mine);
-      const FObj ob = cp(p->objs)[oi];
-      const RT_CONST FObjX& ox = cp(p->objx)[oi];
+      const FObj ob = at(p->objs, oi);
+      const RT_CONST FObjX& ox = at(p->objx, oi);
       const F3 oalb = f3(ox.albedo_pi[0], ox.albedo_pi[1], ox.albedo_pi[2]);
       const float orefl = ox.refl;
       const int nbase = ox.normal_base;
@@ -679,7 +687,7 @@ __device__ __forceinline__ void shade_path(KP p, F3 o, F3 d, bool active, int pi
     if ((F & F_POINT) && p->has_point_light) lds_put3(ls, LDS_HW, hw);
     for (int li = 0; li < p->nlight; ++li) {
       p = params();
-      const FLight L = cp(p->lights)[li];
+      const FLight L = at(p->lights, li);
       F3 sd;
       float dist, k = 1.0f;
       if ((F & F_POINT) && L.type == LIGHT_POINT) {  // light.nim:52-62
