@@ -448,8 +448,12 @@ __device__ __forceinline__ Hit trace(KP p, F3 o, F3 d, float tmax, bool active, 
         // TriangleMesh.intersect (geom.nim:339-358): a ray starting inside
         // the mesh AABB misses (entry t < 0); otherwise the closest face.
         // The AABB and the root ride in the object record (no dependent
-        // FMesh fetch); the gate uses the traversal's slab form of the ray.
-        const SlabRay sr = slab_ray(ro, rd);
+        // FMesh fetch); the gate uses the traversal's slab form of the ray
+        // (built here, not hoisted to the trace's entry by the compiler:
+        // camera waves over an empty pixel list never need it).
+        F3 rdl = rd;
+        asm volatile("" : "+v"(rdl.x), "+v"(rdl.y), "+v"(rdl.z));
+        const SlabRay sr = slab_ray(ro, rdl);
         const float ax = __builtin_fmaf(ob.lo[0], sr.ni.x, -sr.oi.x), bx = __builtin_fmaf(ob.hi[0], sr.ni.x, -sr.oi.x);
         const float ay = __builtin_fmaf(ob.lo[1], sr.ni.y, -sr.oi.y), by = __builtin_fmaf(ob.hi[1], sr.ni.y, -sr.oi.y);
         const float az = __builtin_fmaf(ob.lo[2], sr.ni.z, -sr.oi.z), bz = __builtin_fmaf(ob.hi[2], sr.ni.z, -sr.oi.z);
