@@ -1234,9 +1234,26 @@ int launch(rt_scene* s, const rt_options* o, const Mapping& mp, float* d_out, hi
     rt_scene::Order* measuring = nullptr;
     fill_fast(s, o, mp, d_out, p, &blocks, &measuring);
     if (p.ngroups == 0) return RT_OK;
+    // diagnostic (tools/cost_map.py): RTMI_COST_DUMP=<file> records every
+    // pixel group's duration (s_memtime cycles) of this launch into <file>
+    static const char* cost_dump = std::getenv("RTMI_COST_DUMP");
+    DevBuf<unsigned> dbg_cost;
+    if (cost_dump && !measuring && !p.cost) {
+      if (dbg_cost.alloc((size_t)p.ngroups) == RT_OK) p.cost = dbg_cost.p;
+    }
     const int e = rtmi_launch_render_f32(&p, f32_subset(s, o), blocks, f32_table_lds(o), st);
     if (e) return fail(RT_E_DEVICE, "render kernel launch failed: %s", hipGetErrorString((hipError_t)e));
     if (measuring) HIP_TRY(hipEventRecord(measuring->measured, st));
+    if (dbg_cost.p) {
+      std::vector<unsigned> c((size_t)p.ngroups);
+      HIP_TRY(hipStreamSynchronize(st));
+      HIP_TRY(hipMemcpy(c.data(), dbg_cost.p, c.size() * sizeof(unsigned), hipMemcpyDeviceToHost));
+      dbg_cost.release();
+      if (FILE* f = std::fopen(cost_dump, "wb")) {
+        std::fwrite(c.data(), sizeof(unsigned), c.size(), f);
+        std::fclose(f);
+      }
+    }
   }
   const int e = rtmi_launch_reduce_stats(s->partials.p, blocks * 4, s->acc.p, st);
   if (e) return fail(RT_E_DEVICE, "stats reduction launch failed: %s", hipGetErrorString((hipError_t)e));
