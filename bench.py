@@ -200,12 +200,18 @@ def main():
                 unshard_bands_device(gathered, fb, W, H, BAND_H, world, stream=stream)
 
     # warmup (+ the deterministic per-frame ray counts)
-    # one instrumented launch (RT_FLAG_COUNT_TRAVERSAL) for the traversal record counts
-    from rtmi.abi import RT_FLAG_COUNT_TRAVERSAL
+    # two instrumented launches (RT_FLAG_COUNT_TRAVERSAL): the per-ray BVH
+    # visit / test counts of SURVEY 8(d)'s algorithmic bytes (BVH for every
+    # ray: RT_FLAG_NO_BINNING), and the records the kernel really fetches
+    # (camera / shadow rays searching their pixel lists and light grids)
+    from rtmi.abi import RT_FLAG_COUNT_TRAVERSAL, RT_FLAG_NO_BINNING
     import dataclasses
-    copts = dataclasses.replace(opts, flags=opts.flags | RT_FLAG_COUNT_TRAVERSAL)
+    copts = dataclasses.replace(opts, flags=opts.flags | RT_FLAG_COUNT_TRAVERSAL | RT_FLAG_NO_BINNING)
     st = ds.render_bands_device(copts, local_buf, BAND_H, rank, world, stream=stream, stats=True)
     counters = ds.last_counters()
+    kopts = dataclasses.replace(opts, flags=opts.flags | RT_FLAG_COUNT_TRAVERSAL)
+    ds.render_bands_device(kopts, local_buf, BAND_H, rank, world, stream=stream, stats=False)
+    kcounters = ds.last_counters()
     for _ in range(max(0, args.warmup)):
         step()
     rays_local = st.numPrimaryRays + st.numShadowRays
@@ -252,8 +258,8 @@ def main():
                     + counters["lane_tri_tests"] * SURVEY_TRI_BYTES + rows * W * PIXEL_BYTES)
     achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
     # what the wave-coherent kernel actually requests: one record fetch serves
-    # all 64 lanes of a wave
-    fetch_bytes = (counters["wave_node_fetches"] * NODE_BYTES + counters["wave_tri_fetches"] * TRI_BYTES
+    # all 64 lanes of a wave (binned searches: + a 4-B list entry per face)
+    fetch_bytes = (kcounters["wave_node_fetches"] * NODE_BYTES + kcounters["wave_tri_fetches"] * (TRI_BYTES + 4)
                    + rows * W * PIXEL_BYTES)
     workload_key = f"{args.config.lower()}_{W}x{H}_m{m}_world{world}"
     traffic = load_traffic(workload_key)
@@ -294,13 +300,15 @@ def main():
                 "kernel": "k_render_fast<false>",
                 "kernel_ms": round(kern_ms, 4),
                 "bytes_per_launch": int(bytes_launch),
-                "definition": "SURVEY 8(d): 32 B/box + 36 B/triangle tested per ray + 12 B/pixel",
+                "definition": ("SURVEY 8(d): 32 B/box + 36 B/triangle tested per ray by a per-ray traversal of "
+                               "the scene BVH + 12 B/pixel"),
                 "record_fetch_bytes_per_launch": int(fetch_bytes),
                 "record_fetch_gbs": round(fetch_bytes / (kern_ms * 1e-3) / 1e9, 1),
                 "lane_node_visits": counters["lane_node_visits"],
                 "lane_tri_tests": counters["lane_tri_tests"],
-                "wave_node_fetches": counters["wave_node_fetches"],
-                "wave_tri_fetches": counters["wave_tri_fetches"],
+                "kernel_wave_node_fetches": kcounters["wave_node_fetches"],
+                "kernel_wave_tri_fetches": kcounters["wave_tri_fetches"],
+                "kernel_lane_tri_tests": kcounters["lane_tri_tests"],
             },
             "cpu_baseline": None,
         }
