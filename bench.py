@@ -10,7 +10,8 @@ bunny.geom 69,451 triangles + ground plane, 2 distant lights, akGrid 16x16 =
 in HBM into a device framebuffer. With N GPUs the SAME frame is cut into
 4-row bands dealt round-robin to the ranks, each rank renders its bands and
 one RCCL gather + an on-GPU un-interleave assembles the frame on rank 0
-(strong scaling; the gather is inside the timed region).
+(strong scaling; every gather is inside the timed region, frame k's
+overlapping frame k+1's render from a second band buffer).
 
 Printed (rank 0, one JSON line): value = (primary + shadow rays of all ranks)
 x K / max-over-ranks wall time, plus
@@ -160,7 +161,13 @@ def main():
     torch.cuda.set_device(local)
     # launched by torchrun (even with one rank): the band + RCCL-gather path
     distributed = world > 1 or "TORCHELASTIC_RUN_ID" in os.environ or "LOCAL_WORLD_SIZE" in os.environ
+    # stdout carries exactly one JSON line: whatever else writes to fd 1 (the
+    # RCCL banner at communicator creation) goes to stderr
+    json_out = sys.stdout
     if distributed:
+        sys.stdout.flush()
+        json_out = os.fdopen(os.dup(1), "w")
+        os.dup2(2, 1)
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
@@ -179,25 +186,41 @@ def main():
     stream = torch.cuda.current_stream()
     rows = band_rows(H, BAND_H, world)
     fb = torch.zeros(H * W * 3, dtype=torch.float32, device="cuda")
-    local_buf = torch.zeros(rows * W * 3, dtype=torch.float32, device="cuda")
+    # two band buffers: frame k's gather (RCCL, its own stream) overlaps frame
+    # k+1's render, which writes the other buffer
+    local_bufs = [torch.zeros(rows * W * 3, dtype=torch.float32, device="cuda") for _ in range(2)]
+    local_buf = local_bufs[0]
     gathered = torch.zeros(world * rows * W * 3, dtype=torch.float32, device="cuda")
 
     from rtmi.renderer import unshard_bands_device
 
+    pending = [None]  # the previous frame's gather
+    nframe = [0]
+
+    def finish_frame():
+        # complete the previous frame: its gather, then (rank 0) the
+        # un-interleave into the frame buffer, in stream order
+        if pending[0] is not None:
+            pending[0].wait()
+            pending[0] = None
+            if rank == 0:
+                unshard_bands_device(gathered, fb, W, H, BAND_H, world, stream=stream)
+
     def step(time_kernel=None):
         # render this rank's bands (world == 1: the whole frame, one band set)
+        buf = local_bufs[nframe[0] % 2]
+        nframe[0] += 1
         if time_kernel is not None:
             time_kernel[0].record(stream)
         if distributed:
-            ds.render_bands_device(opts, local_buf, BAND_H, rank, world, stream=stream, stats=False)
+            ds.render_bands_device(opts, buf, BAND_H, rank, world, stream=stream, stats=False)
         else:
             ds.render_device(opts, fb, stream=stream, stats=False)
         if time_kernel is not None:
             time_kernel[1].record(stream)
         if distributed:
-            gather_bands(local_buf, gathered if rank == 0 else None, rows * W * 3)
-            if rank == 0:
-                unshard_bands_device(gathered, fb, W, H, BAND_H, world, stream=stream)
+            finish_frame()  # frame k-1, whose gather overlapped this render
+            pending[0] = gather_bands(buf, gathered if rank == 0 else None, rows * W * 3, async_op=True)
 
     # warmup (+ the deterministic per-frame ray counts)
     # two instrumented launches (RT_FLAG_COUNT_TRAVERSAL): the per-ray BVH
@@ -214,6 +237,7 @@ def main():
     kcounters = ds.last_counters()
     for _ in range(max(0, args.warmup)):
         step()
+    finish_frame()
     rays_local = st.numPrimaryRays + st.numShadowRays
     if distributed:
         t = torch.tensor([rays_local, st.numPrimaryRays, st.numShadowRays], dtype=torch.int64,
@@ -232,6 +256,7 @@ def main():
     t0 = time.perf_counter()
     for k in range(args.steps):
         step(evs[k])
+    finish_frame()  # the last frame's gather + un-interleave, inside the timed region
     torch.cuda.synchronize()
     if distributed:
         dist.barrier()
@@ -322,7 +347,7 @@ def main():
             # the same algorithm class on the CPU (BVH), so the
             # GPU/CPU ratio is also judged against a fair CPU implementation
             out["cpu_baseline_same_bvh"] = cpu_baseline(scene, W, H, args.cpu_seconds, bvh=True)
-        print(json.dumps(out), flush=True)
+        print(json.dumps(out), file=json_out, flush=True)
     if distributed:
         dist.barrier()
         dist.destroy_process_group()

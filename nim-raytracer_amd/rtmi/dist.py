@@ -48,16 +48,18 @@ def unshard_host(gathered, height, band_h):
     return fb
 
 
-def gather_bands(local, gathered, n, group=None):
+def gather_bands(local, gathered, n, group=None, async_op=False):
     """Rank 0 receives every rank's compact band buffer (n floats each) into
-    `gathered` (world * n floats, rank order); other ranks pass None."""
+    `gathered` (world * n floats, rank order); other ranks pass None.
+    async_op=True returns the collective's work handle (wait() before
+    reading `gathered` or reusing `local`)."""
     import torch.distributed as dist
 
     world = dist.get_world_size(group)
     if dist.get_rank(group) == 0:
-        dist.gather(local, [gathered[r * n:(r + 1) * n] for r in range(world)], dst=0, group=group)
-    else:
-        dist.gather(local, None, dst=0, group=group)
+        return dist.gather(local, [gathered[r * n:(r + 1) * n] for r in range(world)], dst=0, group=group,
+                           async_op=async_op)
+    return dist.gather(local, None, dst=0, group=group, async_op=async_op)
 
 
 def render_frame_distributed(dscene, opts, band_h=4, group=None, stream=None, gather=True):
