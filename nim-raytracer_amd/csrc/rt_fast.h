@@ -689,7 +689,9 @@ __device__ __forceinline__ void shade_path(KP p, F3 o, F3 d, bool active, int pi
     const F3 so = f3(__builtin_fmaf(N.x, p->bias, hw.x), __builtin_fmaf(N.y, p->bias, hw.y),
                      __builtin_fmaf(N.z, p->bias, hw.z));
     if ((F & F_POINT) && p->has_point_light) lds_put3(ls, LDS_HW, hw);
-    for (int li = 0; li < p->nlight; ++li) {
+    // no lane shaded a hit (the sky): no shadow rays at all
+    const int nl = bal(lit) != 0ull ? p->nlight : 0;
+    for (int li = 0; li < nl; ++li) {
       p = params();
       const FLight L = at(p->lights, li);
       F3 sd;
