@@ -4,6 +4,7 @@
 #include "rt_bins.h"
 
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <cstdint>
 #include <cstdlib>
@@ -308,6 +309,155 @@ bool build_light_grid(const std::vector<BinTri>& tris, const double w2o[16], con
       }
   };
   return fill_bins((size_t)gu * (size_t)gv, tris.size(), emit, out->off, out->ent, why);
+}
+
+}  // namespace rtmi
+
+namespace rtmi {
+
+bool build_object_pixel_masks(const std::vector<ObjBox>& objs, const double c2w[16], double fov_deg, int width,
+                              int height, std::vector<unsigned long long>* masks, const char** why) {
+  *why = "";
+  if (objs.size() > 64 || width <= 0 || height <= 0) {
+    *why = "object masks hold at most 64 objects";
+    return false;
+  }
+  double w2c[16];
+  if (!invert4(c2w, w2c)) {
+    *why = "singular camera";
+    return false;
+  }
+  const double f = std::tan(fov_deg * (3.14159265358979323846 / 180.0) / 2);
+  const double r = (double)width / (double)height;
+  const double cam_a = 2.0 * r * f / (double)width, cam_c = 2.0 * f / (double)height;
+  const double margin = 0.05;  // pixels
+  unsigned long long always = 0;
+  std::vector<std::array<int, 4>> rect(objs.size(), std::array<int, 4>{-1, -1, -1, -1});
+  for (size_t i = 0; i < objs.size(); ++i) {
+    const ObjBox& b = objs[i];
+    bool proj = !b.always;
+    double xmin = INFINITY, xmax = -INFINITY, ymin = INFINITY, ymax = -INFINITY;
+    for (int c = 0; proj && c < 8; ++c) {
+      const double pw[3] = {(c & 1) ? b.hi[0] : b.lo[0], (c & 2) ? b.hi[1] : b.lo[1], (c & 4) ? b.hi[2] : b.lo[2]};
+      double pc[3];
+      xform_point(w2c, pw, pc);
+      if (!(pc[2] < -1e-9 * (1.0 + std::fabs(pc[0]) + std::fabs(pc[1])))) {
+        proj = false;  // a corner at or behind the camera plane: no bounded projection
+        break;
+      }
+      const double px = 0.5 * width + (pc[0] / -pc[2]) / cam_a;
+      const double py = 0.5 * height - (pc[1] / -pc[2]) / cam_c;
+      xmin = std::min(xmin, px);
+      xmax = std::max(xmax, px);
+      ymin = std::min(ymin, py);
+      ymax = std::max(ymax, py);
+    }
+    if (!proj) {
+      always |= 1ull << i;
+      continue;
+    }
+    if (!(xmax + margin >= 0.0 && ymax + margin >= 0.0 && xmin - margin < width && ymin - margin < height)) continue;
+    rect[i] = {(int)std::max(0.0, std::floor(xmin - margin)), (int)std::min((double)width - 1, std::floor(xmax + margin)),
+               (int)std::max(0.0, std::floor(ymin - margin)), (int)std::min((double)height - 1, std::floor(ymax + margin))};
+  }
+  masks->assign((size_t)width * (size_t)height, always);
+  for (size_t i = 0; i < objs.size(); ++i) {
+    if (rect[i][0] < 0) continue;
+    for (int y = rect[i][2]; y <= rect[i][3]; ++y)
+      for (int x = rect[i][0]; x <= rect[i][1]; ++x) (*masks)[(size_t)y * (size_t)width + (size_t)x] |= 1ull << i;
+  }
+  return true;
+}
+
+bool build_object_light_grid(const std::vector<ObjBox>& objs, const double dir[3], ObjGridHost* out,
+                             const char** why) {
+  *why = "";
+  out->g = LightGrid{};
+  out->masks.clear();
+  out->off_grid = 0;
+  if (objs.size() > 64) {
+    *why = "object masks hold at most 64 objects";
+    return false;
+  }
+  double u[3] = {-dir[0], -dir[1], -dir[2]};
+  const double ul = norm3(u);
+  if (!(ul > 0.0) || !std::isfinite(ul)) {
+    *why = "degenerate light direction";
+    return false;
+  }
+  for (double& x : u) x /= ul;
+  const int ax = std::fabs(u[0]) <= std::fabs(u[1]) && std::fabs(u[0]) <= std::fabs(u[2]) ? 0
+                 : std::fabs(u[1]) <= std::fabs(u[2])                                 ? 1
+                                                                                      : 2;
+  double a[3] = {0, 0, 0};
+  a[ax] = 1.0;
+  double e1[3], e2[3];
+  cross3(a, u, e1);
+  const double l1 = norm3(e1);
+  for (double& x : e1) x /= l1;
+  cross3(u, e1, e2);
+  double scale = 1.0;
+  for (const ObjBox& b : objs)
+    if (!b.always)
+      for (int k = 0; k < 3; ++k) scale = std::max(scale, std::max(std::fabs(b.lo[k]), std::fabs(b.hi[k])));
+  const double delta = 1e-5 * scale;
+  std::vector<std::array<double, 4>> box(objs.size());
+  double umin = INFINITY, umax = -INFINITY, vmin = INFINITY, vmax = -INFINITY;
+  for (size_t i = 0; i < objs.size(); ++i) {
+    const ObjBox& b = objs[i];
+    if (b.always) {
+      out->off_grid |= 1ull << i;
+      continue;
+    }
+    double bu0 = INFINITY, bu1 = -INFINITY, bv0 = INFINITY, bv1 = -INFINITY;
+    for (int c = 0; c < 8; ++c) {
+      const double p[3] = {(c & 1) ? b.hi[0] : b.lo[0], (c & 2) ? b.hi[1] : b.lo[1], (c & 4) ? b.hi[2] : b.lo[2]};
+      const double pu = dot3(p, e1), pv = dot3(p, e2);
+      bu0 = std::min(bu0, pu);
+      bu1 = std::max(bu1, pu);
+      bv0 = std::min(bv0, pv);
+      bv1 = std::max(bv1, pv);
+    }
+    box[i] = {bu0 - delta, bu1 + delta, bv0 - delta, bv1 + delta};
+    umin = std::min(umin, box[i][0]);
+    umax = std::max(umax, box[i][1]);
+    vmin = std::min(vmin, box[i][2]);
+    vmax = std::max(vmax, box[i][3]);
+  }
+  LightGrid& g = out->g;
+  for (int k = 0; k < 3; ++k) {
+    g.e1[k] = (float)e1[k];
+    g.e2[k] = (float)e2[k];
+  }
+  g.rmax = (float)(50.0 * scale);
+  if (!(umin <= umax)) {  // only unbounded objects: a 1x1 grid of the always-set
+    g.u0 = g.v0 = 0.0f;
+    g.inv_h = 1.0f;
+    g.gu = g.gv = 1;
+    out->masks.assign(1, out->off_grid);
+    return true;
+  }
+  const double du = std::max(umax - umin, 1e-30), dv = std::max(vmax - vmin, 1e-30);
+  const double h = std::max(du, dv) / 256.0;  // 256 cells along the longer side
+  const int gu = std::max(1, std::min(256, (int)std::ceil(du / h)));
+  const int gv = std::max(1, std::min(256, (int)std::ceil(dv / h)));
+  g.u0 = (float)umin;
+  g.v0 = (float)vmin;
+  g.inv_h = (float)(1.0 / h);
+  g.gu = gu;
+  g.gv = gv;
+  const double ih = (double)g.inv_h;
+  out->masks.assign((size_t)gu * (size_t)gv, out->off_grid);
+  for (size_t i = 0; i < objs.size(); ++i) {
+    if (objs[i].always) continue;
+    const int c0 = std::max(0, (int)std::floor((box[i][0] - (double)g.u0) * ih));
+    const int c1 = std::min(gu - 1, (int)std::floor((box[i][1] - (double)g.u0) * ih));
+    const int r0 = std::max(0, (int)std::floor((box[i][2] - (double)g.v0) * ih));
+    const int r1 = std::min(gv - 1, (int)std::floor((box[i][3] - (double)g.v0) * ih));
+    for (int rr = r0; rr <= r1; ++rr)
+      for (int cc = c0; cc <= c1; ++cc) out->masks[(size_t)rr * (size_t)gu + (size_t)cc] |= 1ull << i;
+  }
+  return true;
 }
 
 }  // namespace rtmi

@@ -55,3 +55,28 @@ bool build_light_grid(const std::vector<BinTri>& tris, const double w2o[16], con
                       LightGridHost* out, const char** why);
 
 }  // namespace rtmi
+
+namespace rtmi {
+
+// Object bins (scenes of 4..64 objects): per pixel / per light-grid cell a
+// 64-bit mask of the objects whose world bounding box can meet the bin's rays
+// (bit i = object i, so the trace visits the listed objects in scene order).
+// An object that can only be hit by rays through its bounding box in front of
+// the ray origin (spheres, boxes, meshes: geom.nim:76-96, 215-237, 339-358)
+// and is not hit contributes nothing to the closest hit or to Stats' hit count,
+// so skipping it is exact; planes (unbounded) are in every bin.
+struct ObjBox {
+  bool always;       // in every bin (planes, boxes that cannot be projected)
+  double lo[3], hi[3];  // world-space bounding box
+};
+bool build_object_pixel_masks(const std::vector<ObjBox>& objs, const double c2w[16], double fov_deg, int width,
+                              int height, std::vector<unsigned long long>* masks, const char** why);
+struct ObjGridHost {
+  LightGrid g;                           // off_base unused; rmax: float32-safe origin radius
+  std::vector<unsigned long long> masks; // gu * gv cell masks
+  unsigned long long off_grid = 0;       // mask of a safe lane outside the grid (planes)
+};
+bool build_object_light_grid(const std::vector<ObjBox>& objs, const double dir[3], ObjGridHost* out,
+                             const char** why);
+
+}  // namespace rtmi

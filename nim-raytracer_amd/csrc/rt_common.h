@@ -213,6 +213,11 @@ struct FastParams {
   const LightGrid* grids;          // per light, or nullptr: BVH for shadow rays
   const int32_t* grid_off;
   const int32_t* grid_ent;
+  // object bins (rt_bins.h, scenes of 4..64 objects): 64-bit object masks
+  const unsigned long long* obj_pix;   // per pixel (camera rays), or nullptr
+  const LightGrid* obj_grids;          // per light (gu == 0: none), masks at obj_grid_mask[off_base + cell]
+  const unsigned long long* obj_grid_mask;
+  unsigned long long obj_off_grid;     // a safe lane outside an object grid: the unbounded objects
   float* fb;
   unsigned long long* partials;
   unsigned int* queue;             // kQueueShards heads (atomicAdd), zeroed at launch

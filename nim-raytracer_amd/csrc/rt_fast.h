@@ -408,7 +408,42 @@ __device__ __forceinline__ Hit trace(KP p, F3 o, F3 d, float tmax, bool active, 
 #if RTMI_FCMP_MASKS
   const unsigned long long actm = bal(active);
 #endif
-  for (int i = 0; i < p->nobj; ++i) {
+  // Object bins (scenes of 4..64 objects, rt_bins.h): the objects the wave's
+  // bins list, in scene order; an object no bin lists cannot be hit (it
+  // would add nothing to the closest hit or the hit count). Up to 4 distinct
+  // bins per wave, otherwise every object.
+  // Compiled for scenes with spheres or boxes only: mesh + plane scenes keep
+  // the plain object loop (C3: the mask loop cost 27 % there).
+  constexpr bool kObjBins = (F & (F_SPHERE | F_BOX)) != 0;
+  const int nobj = p->nobj;
+  unsigned long long omask = nobj >= 64 ? ~0ull : ((1ull << nobj) - 1ull);
+  if (!kObjBins) {
+  } else if (!shadow && p->obj_pix && pix >= 0) {  // camera rays: the wave's pixels
+    unsigned long long todo = bal(active && pix >= 0), m = 0ull;
+    for (int it = 0; it < 4 && todo != 0ull; ++it) {
+      const int kp = __builtin_amdgcn_readlane(pix, (int)__builtin_ctzll(todo));
+      todo &= ~bal(pix == kp);
+      m |= cp(p->obj_pix)[kp];
+    }
+    omask = todo == 0ull ? m : omask;
+  } else if (shadow && p->obj_grids && light >= 0 && p->obj_grids[light].gu > 0) {  // distant light: cells
+    const RT_CONST LightGrid& G = cp(p->obj_grids)[light];
+    const float gu = __builtin_fmaf(o.x, G.e1[0], __builtin_fmaf(o.y, G.e1[1], o.z * G.e1[2]));
+    const float gv = __builtin_fmaf(o.x, G.e2[0], __builtin_fmaf(o.y, G.e2[1], o.z * G.e2[2]));
+    const float fu = (gu - G.u0) * G.inv_h, fv = (gv - G.v0) * G.inv_h;
+    const bool safe = fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fabsf(o.z)) <= G.rmax;
+    const bool on = fu >= 0.0f && fu < (float)G.gu && fv >= 0.0f && fv < (float)G.gv;
+    const int cell = on ? (int)fv * G.gu + (int)fu : -1;
+    unsigned long long m = p->obj_off_grid;
+    unsigned long long todo = bal(active && safe && on);
+    for (int it = 0; it < 4 && todo != 0ull; ++it) {
+      const int kc = __builtin_amdgcn_readlane(cell, (int)__builtin_ctzll(todo));
+      todo &= ~bal(cell == kc);
+      m |= cp(p->obj_grid_mask)[G.off_base + kc];
+    }
+    omask = (todo == 0ull && bal(active && !safe) == 0ull) ? m : omask;
+  }
+  auto visit = [&](const int i) {
     const FObj ob = at(p->objs, i);
     float t;
     int tri = -1;
@@ -538,6 +573,18 @@ __device__ __forceinline__ Hit trace(KP p, F3 o, F3 d, float tmax, bool active, 
       h.obj = i;
       h.tri = tri;
     }
+  };
+  if constexpr (kObjBins) {
+    for (int base = 0; base < nobj; base += 64) {
+      unsigned long long om = base == 0 ? omask : (nobj - base >= 64 ? ~0ull : ((1ull << (nobj - base)) - 1ull));
+      while (om != 0ull) {
+        const int i = base + (int)__builtin_ctzll(om);
+        om &= om - 1ull;
+        visit(i);
+      }
+    }
+  } else {
+    for (int i = 0; i < nobj; ++i) visit(i);
   }
 #ifdef RTMI_STAMPS
   { RT_STAMP(t_trace1); RT_ACC(6, t_trace0, t_trace1); }

@@ -174,13 +174,23 @@ struct rt_scene {
   bool has_grids = false;
   struct PixelBins {               // camera-ray lists of one image size
     int w = 0, h = 0;
-    bool ok = false;
+    bool ok = false;               // mesh face lists
+    bool obj_ok = false;           // object masks
     DevBuf<int32_t> off, ent;
+    DevBuf<unsigned long long> omask;
     ~PixelBins() {
       off.release();
       ent.release();
+      omask.release();
     }
   };
+  // object bins (rt_bins.h ObjBox), scenes of 4..64 objects
+  std::vector<ObjBox> obj_boxes;
+  bool objbins = false;
+  DevBuf<LightGrid> obj_grids;
+  DevBuf<unsigned long long> obj_grid_mask;
+  unsigned long long obj_off_grid = 0;
+  bool has_obj_grids = false;
   std::vector<std::unique_ptr<PixelBins>> pixel_bins;  // most recently used first, at most 4
   DevBuf<float> fb_scratch;
   int max_waves = 0;
@@ -200,6 +210,8 @@ struct rt_scene {
     grids.release();
     grid_off.release();
     grid_ent.release();
+    obj_grids.release();
+    obj_grid_mask.release();
     pixel_bins.clear();
     if (done) (void)hipEventDestroy(done);
     if (stream) (void)hipStreamDestroy(stream);
@@ -780,6 +792,55 @@ extern "C" int rt_scene_create(const rt_scene_desc* d, rt_scene** out_scene) {
     }
     mark("light grids");
   }
+  if (d->num_objects >= 4 && d->num_objects <= 64) {  // object bins (rt_bins.h)
+    s->obj_boxes.assign((size_t)d->num_objects, ObjBox{});
+    for (int i = 0; i < d->num_objects; ++i) {
+      const rt_object_desc& ob = d->objects[i];
+      ObjBox& b = s->obj_boxes[(size_t)i];
+      double lo[3], hi[3], o2w[16];
+      b.always = ob.type == RT_PLANE || rt_mat4_inverse(ob.world_to_object, o2w) != RT_OK;
+      if (b.always) continue;
+      for (int k = 0; k < 3; ++k) {
+        lo[k] = ob.type == RT_SPHERE ? -std::fabs(ob.radius) : ob.type == RT_BOX ? ob.box_min[k] : aabbs[(size_t)ob.mesh][k];
+        hi[k] = ob.type == RT_SPHERE ? std::fabs(ob.radius) : ob.type == RT_BOX ? ob.box_max[k] : aabbs[(size_t)ob.mesh][3 + k];
+        b.lo[k] = INFINITY;
+        b.hi[k] = -INFINITY;
+      }
+      // the world box of the object box, through the inverse of the
+      // world_to_object the kernel transforms rays with
+      for (int c = 0; c < 8; ++c) {
+        const double q[3] = {(c & 1) ? hi[0] : lo[0], (c & 2) ? hi[1] : lo[1], (c & 4) ? hi[2] : lo[2]};
+        for (int r = 0; r < 3; ++r) {
+          const double w = o2w[0 * 4 + r] * q[0] + o2w[1 * 4 + r] * q[1] + o2w[2 * 4 + r] * q[2] + o2w[3 * 4 + r];
+          b.lo[r] = std::min(b.lo[r], w);
+          b.hi[r] = std::max(b.hi[r], w);
+        }
+      }
+      for (int k = 0; k < 3; ++k)
+        if (!std::isfinite(b.lo[k]) || !std::isfinite(b.hi[k])) b.always = true;
+    }
+    s->objbins = true;
+    std::vector<LightGrid> gh((size_t)std::max(1, d->num_lights), LightGrid{});
+    std::vector<unsigned long long> gm;
+    bool any = false;
+    for (int li = 0; li < d->num_lights; ++li) {
+      if (d->lights[li].type == RT_POINT_LIGHT) continue;
+      ObjGridHost og;
+      const char* why = "";
+      if (!build_object_light_grid(s->obj_boxes, d->lights[li].dir, &og, &why)) continue;
+      if ((int64_t)gm.size() + (int64_t)og.masks.size() > INT32_MAX) break;
+      og.g.off_base = (int32_t)gm.size();
+      gm.insert(gm.end(), og.masks.begin(), og.masks.end());
+      gh[(size_t)li] = og.g;
+      s->obj_off_grid = og.off_grid;  // the same set (the unbounded objects) for every light
+      any = true;
+    }
+    if (any) {
+      if ((rc = s->obj_grids.upload(gh)) || (rc = s->obj_grid_mask.upload(gm))) return rc;
+      s->has_obj_grids = true;
+    }
+    mark("object bins");
+  }
   s->max_waves = s->num_cus * 8 * 4;  // 8 blocks of 4 waves per CU at most
   if ((rc = s->partials.alloc((size_t)s->max_waves * kStatSlots))) return rc;
   if ((rc = s->acc.alloc(kStatSlots))) return rc;
@@ -1032,16 +1093,23 @@ const rt_scene::PixelBins* pixel_bins(rt_scene* s, int w, int h) {
     std::unique_ptr<rt_scene::PixelBins> pb(new rt_scene::PixelBins());
     pb->w = w;
     pb->h = h;
-    PixelBinsHost hb;
     const char* why = "";
-    pb->ok = build_pixel_bins(s->bin_tris, s->mesh_o2w, s->mesh_w2o, s->c2w, s->fov, w, h, &hb, &why) &&
-             pb->off.upload(hb.off) == RT_OK && pb->ent.upload(hb.ent) == RT_OK;
+    if (s->binnable) {
+      PixelBinsHost hb;
+      pb->ok = build_pixel_bins(s->bin_tris, s->mesh_o2w, s->mesh_w2o, s->c2w, s->fov, w, h, &hb, &why) &&
+               pb->off.upload(hb.off) == RT_OK && pb->ent.upload(hb.ent) == RT_OK;
+    }
+    if (s->objbins) {
+      std::vector<unsigned long long> om;
+      pb->obj_ok = build_object_pixel_masks(s->obj_boxes, s->c2w, s->fov, w, h, &om, &why) &&
+                   pb->omask.upload(om) == RT_OK;
+    }
     s->pixel_bins.insert(s->pixel_bins.begin(), std::move(pb));
     if (s->pixel_bins.size() > 4) s->pixel_bins.pop_back();
     i = 0;
   }
   std::rotate(s->pixel_bins.begin(), s->pixel_bins.begin() + (long)i, s->pixel_bins.begin() + (long)i + 1);
-  return s->pixel_bins[0]->ok ? s->pixel_bins[0].get() : nullptr;
+  return s->pixel_bins[0].get();
 }
 
 void fill_fast(rt_scene* s, const rt_options* o, const Mapping& mp, float* fb, FastParams& p, int* blocks,
@@ -1110,15 +1178,23 @@ void fill_fast(rt_scene* s, const rt_options* o, const Mapping& mp, float* fb, F
   // binned searches (rt_bins.h): camera rays when a wave spans at most 4
   // pixels (>= 16 samples per pixel), shadow rays to distant lights
   if (!(o->flags & RT_FLAG_NO_BINNING)) {
-    if (s->binnable && pl.L >= 16)
-      if (const rt_scene::PixelBins* pb = pixel_bins(s, o->width, o->height)) {
+    if ((s->binnable || s->objbins) && pl.L >= 16) {
+      const rt_scene::PixelBins* pb = pixel_bins(s, o->width, o->height);
+      if (pb->ok) {
         p.pix_off = pb->off.p;
         p.pix_ent = pb->ent.p;
       }
+      if (pb->obj_ok) p.obj_pix = pb->omask.p;
+    }
     if (s->has_grids) {
       p.grids = s->grids.p;
       p.grid_off = s->grid_off.p;
       p.grid_ent = s->grid_ent.p;
+    }
+    if (s->has_obj_grids) {
+      p.obj_grids = s->obj_grids.p;
+      p.obj_grid_mask = s->obj_grid_mask.p;
+      p.obj_off_grid = s->obj_off_grid;
     }
   }
   // one work item per dequeue: per-pixel cost varies ~10x (sky vs bunny +

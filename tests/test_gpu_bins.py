@@ -76,8 +76,14 @@ CASES = {
     # reflective mesh, point light (no grid: BVH), analytic objects after the
     # mesh (the shadow early exit's stop distance)
     "mesh_mix": scenes.mesh_mix,
-    # two mesh objects: no bins (BVH for every ray)
+    # two mesh objects: no face bins (BVH for every ray), object bins
     "two_meshes": scenes.two_meshes,
+    # analytic scenes of 4..64 objects: object bins (per-pixel / per-cell
+    # object masks), incl. rotated boxes (C2), reflections, a point light
+    "boxes2": scenes.boxes2,
+    "spheres_warm": scenes.spheres_warm,
+    "spheres_reflection": scenes.spheres_reflection,
+    "spheres_pointlight1": scenes.spheres_pointlight1,
 }
 
 
