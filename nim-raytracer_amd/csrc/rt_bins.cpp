@@ -461,3 +461,45 @@ bool build_object_light_grid(const std::vector<ObjBox>& objs, const double dir[3
 }
 
 }  // namespace rtmi
+
+// Test entry points (tests/test_bins_cpu.py; not part of include/rtmi.h): the
+// builders on a plain face array, face i's record offset = 64 * i.
+namespace {
+std::vector<rtmi::BinTri> test_tris(const double* v9, int64_t nf) {
+  std::vector<rtmi::BinTri> t((size_t)std::max<int64_t>(0, nf));
+  for (int64_t i = 0; i < nf; ++i) {
+    for (int a = 0; a < 3; ++a)
+      for (int k = 0; k < 3; ++k) t[(size_t)i].v[a][k] = v9[9 * i + 3 * a + k];
+    t[(size_t)i].rec = (int32_t)(64 * i);
+  }
+  return t;
+}
+}  // namespace
+
+extern "C" int64_t rtmi_test_pixel_bins(const double* v9, int64_t nf, const double o2w[16], const double w2o[16],
+                                        const double c2w[16], double fov, int32_t w, int32_t h, int32_t* off,
+                                        int32_t* ent, int64_t ent_cap) {
+  rtmi::PixelBinsHost hb;
+  const char* why = "";
+  if (!rtmi::build_pixel_bins(test_tris(v9, nf), o2w, w2o, c2w, fov, w, h, &hb, &why)) return -1;
+  if ((int64_t)hb.ent.size() > ent_cap) return -2;
+  std::copy(hb.off.begin(), hb.off.end(), off);
+  std::copy(hb.ent.begin(), hb.ent.end(), ent);
+  return (int64_t)hb.off.back();
+}
+
+// hdr: e1[3], u0, e2[3], v0, inv_h, rmax, gu, gv (as floats)
+extern "C" int64_t rtmi_test_light_grid(const double* v9, int64_t nf, const double w2o[16], const double dir[3],
+                                        float* hdr, int32_t* off, int64_t off_cap, int32_t* ent, int64_t ent_cap) {
+  rtmi::LightGridHost lg;
+  const char* why = "";
+  if (!rtmi::build_light_grid(test_tris(v9, nf), w2o, dir, &lg, &why)) return -1;
+  if ((int64_t)lg.off.size() > off_cap || (int64_t)lg.ent.size() > ent_cap) return -2;
+  const rtmi::LightGrid& g = lg.g;
+  const float h[12] = {g.e1[0], g.e1[1], g.e1[2], g.u0, g.e2[0], g.e2[1], g.e2[2], g.v0,
+                       g.inv_h, g.rmax, (float)g.gu, (float)g.gv};
+  std::copy(h, h + 12, hdr);
+  std::copy(lg.off.begin(), lg.off.end(), off);
+  std::copy(lg.ent.begin(), lg.ent.end(), ent);
+  return (int64_t)lg.off.back();
+}
