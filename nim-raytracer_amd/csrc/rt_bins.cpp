@@ -311,6 +311,145 @@ bool build_light_grid(const std::vector<BinTri>& tris, const double w2o[16], con
   return fill_bins((size_t)gu * (size_t)gv, tris.size(), emit, out->off, out->ent, why);
 }
 
+void grid_occupancy(const LightGridHost& lg, GridOcc* out) {
+  out->g = lg.g;
+  out->sat.clear();
+  const int gu = lg.g.gu, gv = lg.g.gv;
+  if (gu <= 0 || gv <= 0 || (int64_t)lg.off.size() < (int64_t)gu * gv + 1) {
+    out->g.gu = 0;
+    return;
+  }
+  out->sat.assign((size_t)(gu + 1) * (size_t)(gv + 1), 0);
+  for (int v = 0; v < gv; ++v) {
+    int32_t row = 0;
+    for (int u = 0; u < gu; ++u) {
+      const size_t c = (size_t)v * gu + u;
+      row += lg.off[c + 1] > lg.off[c] ? 1 : 0;
+      out->sat[(size_t)(v + 1) * (gu + 1) + u + 1] = out->sat[(size_t)v * (gu + 1) + u + 1] + row;
+    }
+  }
+}
+
+bool build_shadow_skips(const std::vector<int32_t>& pix_off, const std::vector<SkipPlane>& planes,
+                        const double mesh_w2o[16], const std::vector<GridOcc>& grids, const double c2w[16],
+                        double fov_deg, int width, int height, double bias, std::vector<uint32_t>* out,
+                        const char** why) {
+  *why = "";
+  const size_t npx = (size_t)width * (size_t)height;
+  if (width <= 0 || height <= 0 || pix_off.size() != npx + 1) {
+    *why = "pixel lists of another size";
+    return false;
+  }
+  out->assign((npx + 3) / 4, 0u);
+  const int nl = std::min<int>(8, (int)grids.size());
+  unsigned have = 0;
+  for (int l = 0; l < nl; ++l) have |= grids[(size_t)l].g.gu > 0 ? 1u << l : 0u;
+  if (have == 0) return true;
+  // the kernel's camera constants (as in build_pixel_bins); a corner ray of
+  // pixel (x, y) passes through (x +- margin, y +- margin)
+  const double f = std::tan(fov_deg * (3.14159265358979323846 / 180.0) / 2);
+  const double r = (double)width / (double)height;
+  const double cam_a = 2.0 * r * f / (double)width, cam_c = 2.0 * f / (double)height;
+  const double margin = 0.05;
+  const double cw[3] = {c2w[12], c2w[13], c2w[14]};
+  struct PlaneC {
+    double oy;        // camera origin's object-space y
+    double row[3];    // object-space y of a world direction: row . d
+    double n[3];      // world normal (object_to_world * (0, 1, 0), as the kernel's N)
+    double tol;       // float32 error allowance of row . d
+  };
+  std::vector<PlaneC> pc(planes.size());
+  for (size_t k = 0; k < planes.size(); ++k) {
+    double o[3];
+    xform_point(planes[k].w2o, cw, o);
+    pc[k].oy = o[1];
+    for (int c = 0; c < 3; ++c) {
+      pc[k].row[c] = planes[k].w2o[c * 4 + 1];
+      pc[k].n[c] = planes[k].o2w[1 * 4 + c];
+    }
+    pc[k].tol = 1e-5 * frob3(planes[k].w2o);
+    if (!(std::fabs(o[1]) > 1e-9)) {
+      *why = "the camera lies on a plane";
+      return true;  // no pixel qualifies
+    }
+  }
+  for (int y = 0; y < height; ++y) {
+    for (int x = 0; x < width; ++x) {
+      const size_t pix = (size_t)y * width + x;
+      if (pix_off[pix + 1] != pix_off[pix]) continue;  // camera rays may hit the mesh
+      double dw[4][3];
+      for (int c = 0; c < 4; ++c) {
+        const double px = (c & 1) ? x + 1 + margin : x - margin, py = (c & 2) ? y + 1 + margin : y - margin;
+        const double dc[3] = {(px - 0.5 * width) * cam_a, (0.5 * height - py) * cam_c, -1.0};
+        xform_dir(c2w, dc, dw[c]);
+        const double len = norm3(dw[c]);
+        for (int k = 0; k < 3; ++k) dw[c][k] /= len;
+      }
+      unsigned bits = have;
+      for (size_t k = 0; k < planes.size() && bits; ++k) {
+        const PlaneC& P = pc[k];
+        int hit = 0, miss = 0;
+        double t[4];
+        for (int c = 0; c < 4; ++c) {
+          const double dy = dot3(P.row, dw[c]);
+          // the kernel counts a plane hit at t = -oy / dy >= 0 with |dy| > 1e-6
+          const double s = P.oy > 0.0 ? -dy : dy;  // > 0: towards the plane
+          if (s > P.tol + 1e-6) {
+            ++hit;
+            t[c] = -P.oy / dy;
+          } else if (s < -P.tol) {
+            ++miss;
+          }
+        }
+        if (miss == 4) continue;  // no ray of the pixel reaches this plane
+        if (hit != 4) {           // a horizon inside the pixel: unbounded footprint
+          bits = 0;
+          break;
+        }
+        for (int l = 0; l < nl; ++l) {
+          if (!(bits >> l & 1u)) continue;
+          const LightGrid& g = grids[(size_t)l].g;
+          const double e1[3] = {g.e1[0], g.e1[1], g.e1[2]}, e2[3] = {g.e2[0], g.e2[1], g.e2[2]};
+          double umin = INFINITY, umax = -INFINITY, vmin = INFINITY, vmax = -INFINITY, qmax = 0.0;
+          for (int c = 0; c < 4; ++c) {
+            // shadow-ray origin: hit + N * bias (renderer.nim:94-101), in mesh space
+            const double so[3] = {cw[0] + dw[c][0] * t[c] + P.n[0] * bias, cw[1] + dw[c][1] * t[c] + P.n[1] * bias,
+                                  cw[2] + dw[c][2] * t[c] + P.n[2] * bias};
+            double q[3];
+            xform_point(mesh_w2o, so, q);
+            qmax = std::max(qmax, std::max(std::fabs(q[0]), std::max(std::fabs(q[1]), std::fabs(q[2]))));
+            const double u = dot3(q, e1), v = dot3(q, e2);
+            umin = std::min(umin, u);
+            umax = std::max(umax, u);
+            vmin = std::min(vmin, v);
+            vmax = std::max(vmax, v);
+          }
+          // float32 hit points, transforms and cell coordinates: far inside
+          // 1e-4 of the magnitudes, plus one whole cell
+          const double mw = 1e-4 * (1.0 + qmax) + 1e-4 * std::fabs(bias);
+          const double ih = g.inv_h;
+          const double fu0 = (umin - mw - g.u0) * ih - 1.0, fu1 = (umax + mw - g.u0) * ih + 1.0;
+          const double fv0 = (vmin - mw - g.v0) * ih - 1.0, fv1 = (vmax + mw - g.v0) * ih + 1.0;
+          if (!(fu1 >= 0.0 && fv1 >= 0.0 && fu0 < g.gu && fv0 < g.gv)) continue;  // off the grid
+          if (!std::isfinite(fu0 + fu1 + fv0 + fv1)) {
+            bits &= ~(1u << l);
+            continue;
+          }
+          const int u0 = (int)std::max(0.0, std::floor(fu0)), u1 = (int)std::min((double)g.gu - 1, std::floor(fu1));
+          const int v0 = (int)std::max(0.0, std::floor(fv0)), v1 = (int)std::min((double)g.gv - 1, std::floor(fv1));
+          const std::vector<int32_t>& S = grids[(size_t)l].sat;
+          const size_t W1 = (size_t)g.gu + 1;
+          const int32_t n = S[(size_t)(v1 + 1) * W1 + u1 + 1] - S[(size_t)v0 * W1 + u1 + 1] -
+                            S[(size_t)(v1 + 1) * W1 + u0] + S[(size_t)v0 * W1 + u0];
+          if (n != 0) bits &= ~(1u << l);
+        }
+      }
+      (*out)[pix >> 2] |= bits << (8 * (pix & 3));
+    }
+  }
+  return true;
+}
+
 }  // namespace rtmi
 
 namespace rtmi {
@@ -502,4 +641,32 @@ extern "C" int64_t rtmi_test_light_grid(const double* v9, int64_t nf, const doub
   std::copy(lg.off.begin(), lg.off.end(), off);
   std::copy(lg.ent.begin(), lg.ent.end(), ent);
   return (int64_t)lg.off.back();
+}
+
+// Shadow skips of a one-mesh + planes scene: planes[k] = o2w[16], w2o[16];
+// dirs: nl distant-light directions. out: (w * h + 3) / 4 dwords. Returns the
+// number of pixels with any skip bit, or -1.
+extern "C" int64_t rtmi_test_shadow_skips(const double* v9, int64_t nf, const double o2w[16], const double w2o[16],
+                                          const double c2w[16], double fov, int32_t w, int32_t h, const double* planes,
+                                          int32_t nplanes, const double* dirs, int32_t nl, double bias, uint32_t* out) {
+  const std::vector<rtmi::BinTri> tris = test_tris(v9, nf);
+  rtmi::PixelBinsHost hb;
+  const char* why = "";
+  if (!rtmi::build_pixel_bins(tris, o2w, w2o, c2w, fov, w, h, &hb, &why)) return -1;
+  std::vector<rtmi::GridOcc> occ((size_t)nl);
+  for (int l = 0; l < nl; ++l) {
+    rtmi::LightGridHost lg;
+    if (rtmi::build_light_grid(tris, w2o, dirs + 3 * l, &lg, &why)) rtmi::grid_occupancy(lg, &occ[(size_t)l]);
+  }
+  std::vector<rtmi::SkipPlane> pl((size_t)nplanes);
+  for (int k = 0; k < nplanes; ++k) {
+    std::copy(planes + 32 * k, planes + 32 * k + 16, pl[(size_t)k].o2w);
+    std::copy(planes + 32 * k + 16, planes + 32 * k + 32, pl[(size_t)k].w2o);
+  }
+  std::vector<uint32_t> sk;
+  if (!rtmi::build_shadow_skips(hb.off, pl, w2o, occ, c2w, fov, w, h, bias, &sk, &why)) return -1;
+  std::copy(sk.begin(), sk.end(), out);
+  int64_t n = 0;
+  for (int64_t i = 0; i < (int64_t)w * h; ++i) n += (sk[(size_t)(i >> 2)] >> (8 * (i & 3)) & 0xffu) != 0u;
+  return n;
 }

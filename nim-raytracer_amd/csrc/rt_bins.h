@@ -54,6 +54,32 @@ struct LightGridHost {
 bool build_light_grid(const std::vector<BinTri>& tris, const double w2o[16], const double dir[3],
                       LightGridHost* out, const char** why);
 
+// Shadow skips. Per pixel, bit l (l < 8): every shadow ray to distant light
+// l that leaves a camera hit of this pixel provably meets no face of the mesh,
+// so the kernel drops the mesh from that wave's shadow trace (the mesh could
+// only have answered "miss"). Built for scenes of one mesh and planes: a pixel
+// qualifies when its camera-ray list is empty (its rays hit planes or
+// nothing), and the footprint of its rays on every plane they reach — the
+// quad of the pixel's (grown) corner rays, moved by the shadow-ray bias and
+// grown by a float32 error margin — covers only empty cells of the light's
+// grid (a cell range checked on the grid's occupancy prefix sums) or lies off
+// the grid. Pixels whose corner rays straddle a plane's horizon do not
+// qualify.
+struct GridOcc {
+  LightGrid g{};                 // g.gu == 0: no grid for this light
+  std::vector<int32_t> sat;      // (gu + 1) x (gv + 1) prefix counts of non-empty cells
+};
+void grid_occupancy(const LightGridHost& lg, GridOcc* out);
+struct SkipPlane {
+  double o2w[16], w2o[16];       // a plane object's transforms (y = 0 in object space)
+};
+// pix_off: the pixel lists' offsets (w * h + 1); out: one byte per pixel,
+// packed four to a dword (pixel 4i + k in byte k of out[i]).
+bool build_shadow_skips(const std::vector<int32_t>& pix_off, const std::vector<SkipPlane>& planes,
+                        const double mesh_w2o[16], const std::vector<GridOcc>& grids, const double c2w[16],
+                        double fov_deg, int width, int height, double bias, std::vector<uint32_t>* out,
+                        const char** why);
+
 }  // namespace rtmi
 
 namespace rtmi {

@@ -201,6 +201,11 @@ struct alignas(16) FLight {
   float pad;
 };
 
+// FastParams.pix_info: the low 24 bits hold the pixel's list length (clamped;
+// 0 = the camera rays cannot hit the mesh), bit 24 + l the shadow skip of
+// light l (l < 8). kPixCount alone: nothing known about the pixel.
+constexpr uint32_t kPixCount = 0x00FFFFFFu;
+
 struct FastParams {
   const FObj* objs;
   const FObjX* objx;
@@ -218,6 +223,8 @@ struct FastParams {
   const LightGrid* obj_grids;          // per light (gu == 0: none), masks at obj_grid_mask[off_base + cell]
   const unsigned long long* obj_grid_mask;
   unsigned long long obj_off_grid;     // a safe lane outside an object grid: the unbounded objects
+  const uint32_t* pix_info;        // per pixel: min(list length, kPixCount) | shadow skip bits << 24 (rt_bins.h),
+                                   //   set when a wave holds one pixel; or nullptr
   float* fb;
   unsigned long long* partials;
   unsigned int* queue;             // kQueueShards heads (atomicAdd), zeroed at launch

@@ -399,9 +399,69 @@ __device__ __forceinline__ float analytic_t(KP p, const FObj& ob, int i, F3 o, F
 // min t >= 0 of the analytic objects after the mesh.
 // pix: the camera ray's pixel index (y * width + x; -1 for other rays),
 // light: the shadow ray's light (-1 for other rays); they select the bins.
+// The search of the mesh's faces for the lanes that passed the AABB gate
+// (part): the shadow early exit's stop distance, the binned lists, then the
+// BVH for the lanes no bin served. Returns the best (t, face) key (key0 = the
+// entry key when nothing closer was found).
+template <bool COUNT, unsigned F>
+__device__ __forceinline__ unsigned long long mesh_search(KP p, const FObj& ob, int i, F3 o, F3 d, F3 ro, F3 rd,
+                                                          SlabRay sr, bool part, float tb, bool shadow, bool early,
+                                                          int bin, const int32_t* boff, const int32_t* bent,
+                                                          bool nohit, int light, Stats32& ws) {
+  const bool ex = early && i == p->shadow_mesh;
+  float stop = -1.0f;
+  if (ex) {
+    RT_STAMP(t_st0);
+    stop = finf();
+    for (int j = i + 1; j < p->nobj; ++j) {
+      const float tj = analytic_t<F>(p, at(p->objs, j), j, o, d);
+      stop = tj >= 0.0f ? fminf(stop, tj) : stop;
+    }
+#if RTMI_STAMPS == 2
+    { RT_STAMP(t_st1); RT_ACC(7, t_st0, t_st1); }
+#endif
+  }
+  // search state of the lanes that enter: the best (t, face) key and
+  // the culling limit; a lane retires (early exit) on a FOUND hit
+  // with t <= stop, so stop is clamped to the float just below the
+  // initial limit (tb > 0; for tb == 0 the bit pattern wraps to NaN,
+  // fminf keeps stop, and nothing is acceptable)
+  float tc = part ? tb : -1.0f;
+  stop = fminf(stop, __uint_as_float(__float_as_uint(tb) - 1u));
+  const unsigned long long key0 = part ? tkey(tb, 0u) : 0ull;
+  unsigned long long key = key0;
+  // shadow rays: the light-grid cell (after the gate: the cell
+  // costs more than the gate, which already sends most waves away)
+  if ((F & F_MESH) && shadow && p->grids && light >= 0 && p->grids[light].gu > 0) {
+    const RT_CONST LightGrid& G = cp(p->grids)[light];
+    const float gu = __builtin_fmaf(ro.x, G.e1[0], __builtin_fmaf(ro.y, G.e1[1], ro.z * G.e1[2]));
+    const float gv = __builtin_fmaf(ro.x, G.e2[0], __builtin_fmaf(ro.y, G.e2[1], ro.z * G.e2[2]));
+    const float fu = (gu - G.u0) * G.inv_h, fv = (gv - G.v0) * G.inv_h;
+    const bool safe = fmaxf(fmaxf(fabsf(ro.x), fabsf(ro.y)), fabsf(ro.z)) <= G.rmax;
+    const bool on = fu >= 0.0f && fu < (float)G.gu && fv >= 0.0f && fv < (float)G.gv;
+    bin = safe && on ? G.off_base + (int)fv * G.gu + (int)fu : -1;
+    nohit = safe && !on;
+    boff = p->grid_off;
+    bent = p->grid_ent + G.ent_base;
+  }
+  if (boff) {  // up to 4 distinct bins per wave; lanes left over take the BVH
+    unsigned long long todo = bal(part && bin >= 0);
+    for (int it = 0; it < 4 && todo != 0ull; ++it) {
+      const int kb = __builtin_amdgcn_readlane(bin, (int)__builtin_ctzll(todo));
+      todo &= ~bal(bin == kb);
+      list_search<COUNT>(p, bent, cp(boff)[kb], cp(boff)[kb + 1], ro, rd, ex, stop, key, tc, ws);
+    }
+    // done: binned lanes (their bin was searched) and lanes off the grid
+    tc = (lane_in(todo) || !(bin >= 0 || nohit)) ? tc : -1.0f;
+  }
+  traverse<COUNT>(p, ob.root, ro, rd, sr, ex, stop, key, tc, ws);
+  return key;
+}
+
+
 template <bool COUNT, unsigned F>
 __device__ __forceinline__ Hit trace(KP p, F3 o, F3 d, float tmax, bool active, bool shadow, int pix, int light,
-                                     Stats32& ws) {
+                                     Stats32& ws, bool no_mesh = false) {
   RT_STAMP(t_trace0);
   Hit h{-1, -1, tmax};
   const bool early = (F & F_MESH) && shadow && p->shadow_mesh >= 0;
@@ -457,26 +517,21 @@ __device__ __forceinline__ Hit trace(KP p, F3 o, F3 d, float tmax, bool active, 
       // instead of the BVH: camera rays by pixel (pix: this lane's pixel
       // index, -1 for other rays), shadow rays to a distant light by
       // light-grid cell. A lane whose bin is empty, or that is off the grid,
-      // can hit no face; when a camera wave's one pixel has an empty list
-      // the mesh is skipped before the AABB gate (no lane can produce a hit,
-      // so the gate's verdict cannot matter).
+      // can hit no face. When the caller knows that no lane can hit the mesh
+      // (no_mesh: a one-pixel wave whose pixel list is empty, or whose
+      // pixel's shadow skip bit for this light is set) the mesh is skipped
+      // before the AABB gate (the gate's verdict cannot matter).
       int bin = -1;                        // this lane's bin, -1: none
       const int32_t* boff = nullptr;
       const int32_t* bent = nullptr;
       bool nohit = false;                  // off every listed face
-      bool skip = false;                   // wave-uniform: no lane can hit the mesh
       if ((F & F_MESH) && !shadow && p->pix_off && pix >= 0) {
         bin = pix;
         boff = p->pix_off;
         bent = p->pix_ent;
-        if (p->lanes_per_px == 64) {  // one pixel per wave: its list length decides
-          const unsigned long long pm = bal(active && pix >= 0);
-          if (pm != 0ull) {
-            const int up = __builtin_amdgcn_readlane(pix, (int)__builtin_ctzll(pm));
-            skip = cp(boff)[up] == cp(boff)[up + 1];
-          }
-        }
       }
+      // no_mesh (wave-uniform, the caller's pixel record): no lane can hit the mesh
+      const bool skip = no_mesh;
       if (skip) {
         t = -finf();
       } else {
@@ -504,53 +559,9 @@ __device__ __forceinline__ Hit trace(KP p, F3 o, F3 d, float tmax, bool active, 
         // shadow early exit (above): stop is only computed when some lane of
         // the wave enters the mesh
         if (ob.root >= 0 && bal(part) != 0ull) {
-          const bool ex = early && i == p->shadow_mesh;
-          float stop = -1.0f;
-          if (ex) {
-            RT_STAMP(t_st0);
-            stop = finf();
-            for (int j = i + 1; j < p->nobj; ++j) {
-              const float tj = analytic_t<F>(p, at(p->objs, j), j, o, d);
-              stop = tj >= 0.0f ? fminf(stop, tj) : stop;
-            }
-#if RTMI_STAMPS == 2
-            { RT_STAMP(t_st1); RT_ACC(7, t_st0, t_st1); }
-#endif
-          }
-          // search state of the lanes that enter: the best (t, face) key and
-          // the culling limit; a lane retires (early exit) on a FOUND hit
-          // with t <= stop, so stop is clamped to the float just below the
-          // initial limit (tb > 0; for tb == 0 the bit pattern wraps to NaN,
-          // fminf keeps stop, and nothing is acceptable)
-          float tc = part ? tb : -1.0f;
-          stop = fminf(stop, __uint_as_float(__float_as_uint(tb) - 1u));
           const unsigned long long key0 = part ? tkey(tb, 0u) : 0ull;
-          unsigned long long key = key0;
-          // shadow rays: the light-grid cell (after the gate: the cell
-          // costs more than the gate, which already sends most waves away)
-          if ((F & F_MESH) && shadow && p->grids && light >= 0 && p->grids[light].gu > 0) {
-            const RT_CONST LightGrid& G = cp(p->grids)[light];
-            const float gu = __builtin_fmaf(ro.x, G.e1[0], __builtin_fmaf(ro.y, G.e1[1], ro.z * G.e1[2]));
-            const float gv = __builtin_fmaf(ro.x, G.e2[0], __builtin_fmaf(ro.y, G.e2[1], ro.z * G.e2[2]));
-            const float fu = (gu - G.u0) * G.inv_h, fv = (gv - G.v0) * G.inv_h;
-            const bool safe = fmaxf(fmaxf(fabsf(ro.x), fabsf(ro.y)), fabsf(ro.z)) <= G.rmax;
-            const bool on = fu >= 0.0f && fu < (float)G.gu && fv >= 0.0f && fv < (float)G.gv;
-            bin = safe && on ? G.off_base + (int)fv * G.gu + (int)fu : -1;
-            nohit = safe && !on;
-            boff = p->grid_off;
-            bent = p->grid_ent + G.ent_base;
-          }
-          if (boff) {  // up to 4 distinct bins per wave; lanes left over take the BVH
-            unsigned long long todo = bal(part && bin >= 0);
-            for (int it = 0; it < 4 && todo != 0ull; ++it) {
-              const int kb = __builtin_amdgcn_readlane(bin, (int)__builtin_ctzll(todo));
-              todo &= ~bal(bin == kb);
-              list_search<COUNT>(p, bent, cp(boff)[kb], cp(boff)[kb + 1], ro, rd, ex, stop, key, tc, ws);
-            }
-            // done: binned lanes (their bin was searched) and lanes off the grid
-            tc = (lane_in(todo) || !(bin >= 0 || nohit)) ? tc : -1.0f;
-          }
-          traverse<COUNT>(p, ob.root, ro, rd, sr, ex, stop, key, tc, ws);
+          const unsigned long long key = mesh_search<COUNT, F>(p, ob, i, o, d, ro, rd, sr, part, tb, shadow, early,
+                                                               bin, boff, bent, nohit, light, ws);
           if (key != key0) {
             tb = __uint_as_float((unsigned int)(key >> 32));
             best = (int)(unsigned int)key;
@@ -664,17 +675,20 @@ __device__ __forceinline__ F3 lds_get3(LdsF* ls, int slot) {
 //  * renderer.nim:104-124: reflection > 0 and depth <= maxRayDepth traces
 //    r = i - 2 (n.i) n from hitW + r*bias; the level's local light is
 //    weighted (1 - reflection), the reflected colour reflection.
-// pix: the sample's pixel index (y * width + x) for the camera ray's bins.
+// pix: the sample's pixel index (y * width + x) for the camera ray's bins;
+// pinfo: the wave's pixel record (FastParams.pix_info) when the wave holds
+// one pixel, else kPixCount (nothing known).
 template <bool COUNT, unsigned F>
-__device__ __forceinline__ void shade_path(KP p, F3 o, F3 d, bool active, int pix, LdsF* ls, Acc& acc,
-                                           Stats32& ws) {
+__device__ __forceinline__ void shade_path(KP p, F3 o, F3 d, bool active, int pix, unsigned pinfo, LdsF* ls,
+                                           Acc& acc, Stats32& ws) {
   bool act = active;
   int depth = 1;
   float w = 1.0f;
   for (int lev = 0; lev < ((F & F_REFLECT) ? kMaxShadeLevels : 1); ++lev) {
     p = params();
     if (bal(act) == 0ull) break;
-    const Hit hit = trace<COUNT, F>(p, o, d, finf(), act, false, lev == 0 ? pix : -1, -1, ws);
+    const Hit hit = trace<COUNT, F>(p, o, d, finf(), act, false, lev == 0 ? pix : -1, -1, ws,
+                                    lev == 0 && (pinfo & kPixCount) == 0u);
     if (act && hit.obj < 0) acc_add3(acc, w * p->bg[0], w * p->bg[1], w * p->bg[2]);
     const bool lit = act && hit.obj >= 0;
     const F3 hw = f3(__builtin_fmaf(d.x, hit.t, o.x), __builtin_fmaf(d.y, hit.t, o.y), __builtin_fmaf(d.z, hit.t, o.z));
@@ -738,6 +752,9 @@ __device__ __forceinline__ void shade_path(KP p, F3 o, F3 d, bool active, int pi
     if ((F & F_POINT) && p->has_point_light) lds_put3(ls, LDS_HW, hw);
     // no lane shaded a hit (the sky): no shadow rays at all
     const int nl = bal(lit) != 0ull ? p->nlight : 0;
+    // shadow skips of the wave's pixel (camera hits only): bit li set = no
+    // shadow ray to light li can meet the mesh
+    const unsigned skipw = lev == 0 ? pinfo >> 24 : 0u;
     for (int li = 0; li < nl; ++li) {
       p = params();
       const FLight L = at(p->lights, li);
@@ -756,7 +773,7 @@ __device__ __forceinline__ void shade_path(KP p, F3 o, F3 d, bool active, int pi
         dist = finf();
       }
       ws.v[STAT_SHADOW] += pc(bal(lit));
-      const Hit sh = trace<COUNT, F>(p, so, sd, dist, lit, true, -1, li, ws);
+      const Hit sh = trace<COUNT, F>(p, so, sd, dist, lit, true, -1, li, ws, li < 8 && ((skipw >> li) & 1u) != 0u);
       if (lit && sh.obj < 0) {  // shadeDiffuse (shader.nim:12-17)
         const float ndl = fmaxf(dot3(N, sd), 0.0f) * k;
         acc_add3(acc, albw.x * L.ci[0] * ndl, albw.y * L.ci[1] * ndl, albw.z * L.ci[2] * ndl);
@@ -920,6 +937,16 @@ __global__ __launch_bounds__(256) RTMI_OCC void k_render_fast(const FastParams p
     }
     Acc pacc;
     pacc.v = f3(0.0f, 0.0f, 0.0f);
+    // the pixel's record, once per work item (a one-pixel wave: every
+    // iteration shades the same pixel): list length + shadow skip bits
+    unsigned pinfo = kPixCount;
+    if ((F & F_MESH) && p->pix_info) {
+      const unsigned long long vm = bal(gp.valid);
+      if (vm != 0ull) {
+        const int up = __builtin_amdgcn_readlane(gp.y * p->width + gp.x, (int)__builtin_ctzll(vm));
+        pinfo = at(p->pix_info, up);
+      }
+    }
     for (int it = 0; it < iters; ++it) {
       p = params();
       const int s = it * L + gp.sub;  // this lane's sample index
@@ -952,7 +979,7 @@ __global__ __launch_bounds__(256) RTMI_OCC void k_render_fast(const FastParams p
       const F3 o = f3(p->cam[0], p->cam[1], p->cam[2]);
       ws.v[STAT_PRIMARY] += pc(bal(sv));
       RT_STAMP(t_s0);
-      shade_path<COUNT, F>(p, o, d, sv, sv ? gp.y * p->width + gp.x : -1, ls, pacc, ws);
+      shade_path<COUNT, F>(p, o, d, sv, sv ? gp.y * p->width + gp.x : -1, pinfo, ls, pacc, ws);
 #if RTMI_STAMPS == 1
       { RT_STAMP(t_s1); RT_ACC(7, t_s0, t_s1); }
 #endif

@@ -172,16 +172,25 @@ struct rt_scene {
   DevBuf<LightGrid> grids;         // per light (gu == 0: none)
   DevBuf<int32_t> grid_off, grid_ent;
   bool has_grids = false;
+  // shadow skips (rt_bins.h): scenes of the one mesh and planes
+  std::vector<GridOcc> grid_occ;   // per light (g.gu == 0: none)
+  std::vector<SkipPlane> skip_planes;
+  bool skippable = false;
   struct PixelBins {               // camera-ray lists of one image size
     int w = 0, h = 0;
     bool ok = false;               // mesh face lists
     bool obj_ok = false;           // object masks
     DevBuf<int32_t> off, ent;
     DevBuf<unsigned long long> omask;
+    std::vector<int32_t> host_off; // the lists' offsets (the pixel records are built from them)
+    bool info_ok = false;          // pixel records (FastParams.pix_info) built for info_bias
+    double info_bias = 0.0;
+    DevBuf<uint32_t> info;
     ~PixelBins() {
       off.release();
       ent.release();
       omask.release();
+      info.release();
     }
   };
   // object bins (rt_bins.h ObjBox), scenes of 4..64 objects
@@ -769,6 +778,7 @@ extern "C" int rt_scene_create(const rt_scene_desc* d, rt_scene** out_scene) {
     s->binnable = !s->bin_tris.empty();
     // light grids of the distant lights
     std::vector<LightGrid> gh((size_t)std::max(1, d->num_lights), LightGrid{});
+    s->grid_occ.assign((size_t)d->num_lights, GridOcc{});
     std::vector<int32_t> goff, gent;
     bool any = false;
     for (int li = 0; s->binnable && li < d->num_lights; ++li) {
@@ -784,11 +794,24 @@ extern "C" int rt_scene_create(const rt_scene_desc* d, rt_scene** out_scene) {
       goff.insert(goff.end(), lg.off.begin(), lg.off.end());
       gent.insert(gent.end(), lg.ent.begin(), lg.ent.end());
       gh[(size_t)li] = lg.g;
+      grid_occupancy(lg, &s->grid_occ[(size_t)li]);
       any = true;
     }
     if (any) {
       if ((rc = s->grids.upload(gh)) || (rc = s->grid_off.upload(goff)) || (rc = s->grid_ent.upload(gent))) return rc;
       s->has_grids = true;
+      // shadow skips: every other object a plane
+      s->skippable = true;
+      for (int i = 0; i < d->num_objects; ++i) {
+        const rt_object_desc& o = d->objects[i];
+        if (i == s->shadow_mesh) continue;
+        SkipPlane sp;
+        s->skippable = s->skippable && o.type == RT_PLANE;
+        std::memcpy(sp.o2w, o.object_to_world, sizeof sp.o2w);
+        std::memcpy(sp.w2o, o.world_to_object, sizeof sp.w2o);
+        s->skip_planes.push_back(sp);
+      }
+      if (!s->skippable) s->skip_planes.clear();
     }
     mark("light grids");
   }
@@ -1086,7 +1109,7 @@ OrderUse group_order(rt_scene* s, const rt_options* o, const Mapping& mp, const 
 // Camera-ray lists for one image size (rt_bins.h), built on first use and
 // cached; nullptr when the camera set-up does not allow them (the kernel then
 // traverses the BVH).
-const rt_scene::PixelBins* pixel_bins(rt_scene* s, int w, int h) {
+rt_scene::PixelBins* pixel_bins(rt_scene* s, int w, int h) {
   size_t i = 0;
   while (i < s->pixel_bins.size() && !(s->pixel_bins[i]->w == w && s->pixel_bins[i]->h == h)) ++i;
   if (i == s->pixel_bins.size()) {
@@ -1098,6 +1121,7 @@ const rt_scene::PixelBins* pixel_bins(rt_scene* s, int w, int h) {
       PixelBinsHost hb;
       pb->ok = build_pixel_bins(s->bin_tris, s->mesh_o2w, s->mesh_w2o, s->c2w, s->fov, w, h, &hb, &why) &&
                pb->off.upload(hb.off) == RT_OK && pb->ent.upload(hb.ent) == RT_OK;
+      if (pb->ok) pb->host_off.swap(hb.off);
     }
     if (s->objbins) {
       std::vector<unsigned long long> om;
@@ -1179,11 +1203,29 @@ void fill_fast(rt_scene* s, const rt_options* o, const Mapping& mp, float* fb, F
   // pixels (>= 16 samples per pixel), shadow rays to distant lights
   if (!(o->flags & RT_FLAG_NO_BINNING)) {
     if ((s->binnable || s->objbins) && pl.L >= 16) {
-      const rt_scene::PixelBins* pb = pixel_bins(s, o->width, o->height);
+      rt_scene::PixelBins* pb = pixel_bins(s, o->width, o->height);
       if (pb->ok) {
         p.pix_off = pb->off.p;
         p.pix_ent = pb->ent.p;
       }
+      // one-pixel waves: the pixel records (list length + shadow skips for
+      // this bias, rt_bins.h), rebuilt when the bias changes
+      if (pb->ok && pl.L == 64 && !(pb->info_ok && pb->info_bias == o->bias)) {
+        const size_t npx = (size_t)o->width * (size_t)o->height;
+        std::vector<uint32_t> sk;
+        const char* why = "";
+        if (!(s->skippable && build_shadow_skips(pb->host_off, s->skip_planes, s->mesh_w2o, s->grid_occ, s->c2w,
+                                                 s->fov, o->width, o->height, o->bias, &sk, &why)))
+          sk.assign((npx + 3) / 4, 0u);
+        std::vector<uint32_t> info(npx);
+        for (size_t i = 0; i < npx; ++i) {
+          const uint32_t n = (uint32_t)(pb->host_off[i + 1] - pb->host_off[i]);
+          info[i] = std::min<uint32_t>(n, kPixCount) | (sk[i >> 2] >> (8 * (i & 3)) & 0xffu) << 24;
+        }
+        pb->info_ok = pb->info.upload(info) == RT_OK;
+        pb->info_bias = o->bias;
+      }
+      if (pb->ok && pl.L == 64 && pb->info_ok) p.pix_info = pb->info.p;
       if (pb->obj_ok) p.obj_pix = pb->omask.p;
     }
     if (s->has_grids) {

@@ -175,3 +175,68 @@ def test_light_grid_cells_hold_every_hit_face(name):
             missing = set(hit.tolist()) - lst
             assert not missing, (name, o, sorted(missing)[:5])
     assert total_hits > 100
+
+
+def _tilted_plane():
+    m = translate(mat4(1.0), vec3(0.0, -0.4, 0.0))
+    m = rotate(m, X_AXIS, degToRad(4.0))
+    m = rotate(m, Y_AXIS, degToRad(20.0))
+    return m, inverse(m)
+
+
+@pytest.mark.parametrize("name,tilted", [("bunny", False), ("rotated_torus", True)])
+def test_shadow_skips_are_conservative(name, tilted):
+    """A pixel's skip bit for a light (rt_bins.h build_shadow_skips) promises
+    that no shadow ray to that light from a camera hit in the pixel meets a
+    face: checked for random samples (and the pixel corners) of skipped
+    pixels, against every face in float64."""
+    L = lib()
+    f = L.rtmi_test_shadow_skips
+    f.restype = C.c_int64
+    mesh = MESHES[name]()
+    v9 = _faces(mesh)
+    nf = len(v9)
+    o2w, w2o = _m(mesh.objectToWorld), _m(mesh.worldToObject)
+    sc = scenes.mesh_bunny()
+    c2w = _m(sc.cameraToWorld)
+    po2w, pw2o = _tilted_plane() if tilted else (mat4(1.0), mat4(1.0))
+    planes = np.concatenate([_m(po2w), _m(pw2o)])
+    dirs = np.ascontiguousarray(np.concatenate([np.asarray(l.dir[:3], np.float64) for l in sc.lights]))
+    W, H, fov, bias = 480, 270, 50.0, 1e-4
+    out = np.zeros((W * H + 3) // 4, np.uint32)
+    n = f(v9.ctypes.data_as(C.c_void_p), C.c_int64(nf), o2w.ctypes.data_as(C.c_void_p),
+          w2o.ctypes.data_as(C.c_void_p), c2w.ctypes.data_as(C.c_void_p), C.c_double(fov), W, H,
+          planes.ctypes.data_as(C.c_void_p), 1, dirs.ctypes.data_as(C.c_void_p), len(sc.lights), C.c_double(bias),
+          out.ctypes.data_as(C.c_void_p))
+    assert n > 0.3 * W * H  # most ground pixels skip at least one light
+    bits = (out.view(np.uint8)[:W * H]).astype(np.int64)
+    C2W, W2O, P2W, W2P = _cols(c2w), _cols(w2o), _cols(_m(po2w)), _cols(_m(pw2o))
+    N = P2W[:3, 1]
+    fo = math.tan(math.radians(fov) / 2)
+    ca, cc = 2 * (W / H) * fo / W, 2 * fo / H
+    org = C2W[:3, 3]
+    rng = np.random.default_rng(5)
+    near = 0
+    for li, light in enumerate(sc.lights):
+        rd = W2O[:3, :3] @ -np.asarray(light.dir[:3], np.float64)
+        sk = np.nonzero(bits >> li & 1)[0]
+        # skipped pixels next to unskipped ones (the shadow's border) first
+        edge = sk[(bits[np.clip(sk + 1, 0, W * H - 1)] >> li & 1) == 0]
+        pick = np.concatenate([edge[rng.permutation(len(edge))[:400]], sk[rng.integers(0, len(sk), 200)]])
+        for k, pix in enumerate(pick):
+            x, y = int(pix % W), int(pix // W)
+            sx, sy = (rng.random(), rng.random()) if k % 3 else (float(rng.integers(0, 2)), float(rng.integers(0, 2)))
+            px, py = x + min(sx, 0.999999), y + min(sy, 0.999999)
+            dc = np.array([(px - W / 2) * ca, (H / 2 - py) * cc, -1.0])
+            d = C2W[:3, :3] @ (dc / np.linalg.norm(dc))
+            oy = (W2P[:3, :3] @ org + W2P[:3, 3])[1]
+            dy = (W2P[:3, :3] @ d)[1]
+            t = -oy / dy
+            if not (t >= 0):
+                continue  # the sky: no shadow ray
+            so = org + d * t + N * bias
+            ro = W2O[:3, :3] @ so + W2O[:3, 3]
+            hit = _hits(v9, ro, rd)
+            assert len(hit) == 0, (name, li, x, y, hit[:5])
+            near += k < len(edge)
+    assert near > 100
