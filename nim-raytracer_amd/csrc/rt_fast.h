@@ -93,6 +93,11 @@ __device__ __forceinline__ KP params() {
 struct F3 {
   float x, y, z;
 };
+
+template <bool B>
+struct Bool {
+  static constexpr bool value = B;
+};
 __device__ __forceinline__ F3 f3(float x, float y, float z) { return F3{x, y, z}; }
 __device__ __forceinline__ float dot3(F3 a, F3 b) { return __builtin_fmaf(a.x, b.x, __builtin_fmaf(a.y, b.y, a.z * b.z)); }
 
@@ -755,30 +760,42 @@ __device__ __forceinline__ void shade_path(KP p, F3 o, F3 d, bool active, int pi
     // shadow skips of the wave's pixel (camera hits only): bit li set = no
     // shadow ray to light li can meet the mesh
     const unsigned skipw = lev == 0 ? pinfo >> 24 : 0u;
-    for (int li = 0; li < nl; ++li) {
-      p = params();
-      const FLight L = at(p->lights, li);
-      F3 sd;
-      float dist, k = 1.0f;
-      if ((F & F_POINT) && L.type == LIGHT_POINT) {  // light.nim:52-62
-        const F3 h = lds_get3(ls, LDS_HW);
-        const F3 lv = f3(h.x - L.v[0], h.y - L.v[1], h.z - L.v[2]);
-        const float r2 = dot3(lv, lv);
-        const float rr = rsq(r2);
-        sd = f3(-lv.x * rr, -lv.y * rr, -lv.z * rr);
-        k = rcp(12.566370614359172f * r2);
-        dist = r2 * rr;
-      } else {  // light.nim:46-50
-        sd = f3(-L.v[0], -L.v[1], -L.v[2]);
-        dist = finf();
+    // two instances of the light loop: with every light's skip bit set the
+    // shadow traces are compiled without the mesh search (C3: most waves),
+    // which the register allocation and scheduling of the loop feel even
+    // when the search is skipped at run time
+    auto light_loop = [&](auto lean) {
+      constexpr bool kLean = decltype(lean)::value;
+      for (int li = 0; li < nl; ++li) {
+        p = params();
+        const FLight L = at(p->lights, li);
+        F3 sd;
+        float dist, k = 1.0f;
+        if ((F & F_POINT) && L.type == LIGHT_POINT) {  // light.nim:52-62
+          const F3 h = lds_get3(ls, LDS_HW);
+          const F3 lv = f3(h.x - L.v[0], h.y - L.v[1], h.z - L.v[2]);
+          const float r2 = dot3(lv, lv);
+          const float rr = rsq(r2);
+          sd = f3(-lv.x * rr, -lv.y * rr, -lv.z * rr);
+          k = rcp(12.566370614359172f * r2);
+          dist = r2 * rr;
+        } else {  // light.nim:46-50
+          sd = f3(-L.v[0], -L.v[1], -L.v[2]);
+          dist = finf();
+        }
+        ws.v[STAT_SHADOW] += pc(bal(lit));
+        const Hit sh = trace<COUNT, F>(p, so, sd, dist, lit, true, -1, li, ws,
+                                       kLean || (li < 8 && ((skipw >> li) & 1u) != 0u));
+        if (lit && sh.obj < 0) {  // shadeDiffuse (shader.nim:12-17)
+          const float ndl = fmaxf(dot3(N, sd), 0.0f) * k;
+          acc_add3(acc, albw.x * L.ci[0] * ndl, albw.y * L.ci[1] * ndl, albw.z * L.ci[2] * ndl);
+        }
       }
-      ws.v[STAT_SHADOW] += pc(bal(lit));
-      const Hit sh = trace<COUNT, F>(p, so, sd, dist, lit, true, -1, li, ws, li < 8 && ((skipw >> li) & 1u) != 0u);
-      if (lit && sh.obj < 0) {  // shadeDiffuse (shader.nim:12-17)
-        const float ndl = fmaxf(dot3(N, sd), 0.0f) * k;
-        acc_add3(acc, albw.x * L.ci[0] * ndl, albw.y * L.ci[1] * ndl, albw.z * L.ci[2] * ndl);
-      }
-    }
+    };
+    if ((F & F_MESH) && nl > 0 && nl <= 8 && skipw == (1u << nl) - 1u)
+      light_loop(Bool<true>{});
+    else
+      light_loop(Bool<false>{});
     // every lane reloads (lanes that do not reflect go inactive): o and d
     // are then dead across the light loop instead of carried for them
     if ((F & F_REFLECT) && bal(reflect)) {
