@@ -683,7 +683,7 @@ __device__ __forceinline__ F3 lds_get3(LdsF* ls, int slot) {
 // pix: the sample's pixel index (y * width + x) for the camera ray's bins;
 // pinfo: the wave's pixel record (FastParams.pix_info) when the wave holds
 // one pixel, else kPixCount (nothing known).
-template <bool COUNT, unsigned F>
+template <bool COUNT, unsigned F, bool LEAN = false>
 __device__ __forceinline__ void shade_path(KP p, F3 o, F3 d, bool active, int pix, unsigned pinfo, LdsF* ls,
                                            Acc& acc, Stats32& ws) {
   bool act = active;
@@ -693,7 +693,7 @@ __device__ __forceinline__ void shade_path(KP p, F3 o, F3 d, bool active, int pi
     p = params();
     if (bal(act) == 0ull) break;
     const Hit hit = trace<COUNT, F>(p, o, d, finf(), act, false, lev == 0 ? pix : -1, -1, ws,
-                                    lev == 0 && (pinfo & kPixCount) == 0u);
+                                    lev == 0 && (LEAN || (pinfo & kPixCount) == 0u));
     if (act && hit.obj < 0) acc_add3(acc, w * p->bg[0], w * p->bg[1], w * p->bg[2]);
     const bool lit = act && hit.obj >= 0;
     const F3 hw = f3(__builtin_fmaf(d.x, hit.t, o.x), __builtin_fmaf(d.y, hit.t, o.y), __builtin_fmaf(d.z, hit.t, o.z));
@@ -792,7 +792,7 @@ __device__ __forceinline__ void shade_path(KP p, F3 o, F3 d, bool active, int pi
         }
       }
     };
-    if ((F & F_MESH) && nl > 0 && nl <= 8 && skipw == (1u << nl) - 1u)
+    if (LEAN || ((F & F_MESH) && nl > 0 && nl <= 8 && skipw == (1u << nl) - 1u))
       light_loop(Bool<true>{});
     else
       light_loop(Bool<false>{});
@@ -964,43 +964,54 @@ __global__ __launch_bounds__(256) RTMI_OCC void k_render_fast(const FastParams p
         pinfo = at(p->pix_info, up);
       }
     }
-    for (int it = 0; it < iters; ++it) {
-      p = params();
-      const int s = it * L + gp.sub;  // this lane's sample index
-      const bool sv = gp.valid && s < p->spp;
-      float px = (float)gp.x, py = (float)gp.y;
-      if (p->aa_kind == 1) {  // grid() sampling.nim:5-18: sample s = (si, sj)
-        int si;
-        const int sj = div_small(s, p->grid_m, p->sample_step, si);
-        px += __builtin_fmaf((float)si, p->sample_step, p->sample_off);
-        py += __builtin_fmaf((float)sj, p->sample_step, p->sample_off);
-      } else if ((F & F_STOCHASTIC) && p->aa_kind == 2) {  // jitteredGrid (sampling.nim:21-33): no table needed
-        double a, b;
-        jittered_entry(rng_pixel_key(p->seed, gp.x, gp.y), p->grid_m, s < p->spp ? s : 0, a, b);
-        px += (float)a;
-        py += (float)b;
-      } else if (tb) {
-        const volatile LdsF* t = tb;
-        const int ss = s < p->spp ? s : 0;
-        px += t[ss];
-        py += t[p->spp + ss];
-      }
-      // castPrimaryRay (renderer.nim:31-44), constants folded on the host
-      // ((2 x r)/w - r) f == (x - w/2) (2 r f / w): exact 0 on the centre
-      // column / row, as the reference's own formula gives there
-      const float cx = (px - p->cam_b) * p->cam_a;
-      const float cy = (p->cam_d - py) * p->cam_c;
-      const float rl = rsq(__builtin_fmaf(cx, cx, __builtin_fmaf(cy, cy, 1.0f)));
-      const F3 d = f3((cx * p->cam[3] + cy * p->cam[6] - p->cam[9]) * rl, (cx * p->cam[4] + cy * p->cam[7] - p->cam[10]) * rl,
-                      (cx * p->cam[5] + cy * p->cam[8] - p->cam[11]) * rl);
-      const F3 o = f3(p->cam[0], p->cam[1], p->cam[2]);
-      ws.v[STAT_PRIMARY] += pc(bal(sv));
-      RT_STAMP(t_s0);
-      shade_path<COUNT, F>(p, o, d, sv, sv ? gp.y * p->width + gp.x : -1, pinfo, ls, pacc, ws);
+    // a lean pixel (no camera ray can hit the mesh, every light's shadow
+    // rays skip it; no reflection) runs an instance of the sample loop
+    // compiled without any mesh search
+    auto sample_loop = [&](auto lean) {
+      for (int it = 0; it < iters; ++it) {
+        p = params();
+        const int s = it * L + gp.sub;  // this lane's sample index
+        const bool sv = gp.valid && s < p->spp;
+        float px = (float)gp.x, py = (float)gp.y;
+        if (p->aa_kind == 1) {  // grid() sampling.nim:5-18: sample s = (si, sj)
+          int si;
+          const int sj = div_small(s, p->grid_m, p->sample_step, si);
+          px += __builtin_fmaf((float)si, p->sample_step, p->sample_off);
+          py += __builtin_fmaf((float)sj, p->sample_step, p->sample_off);
+        } else if ((F & F_STOCHASTIC) && p->aa_kind == 2) {  // jitteredGrid (sampling.nim:21-33): no table needed
+          double a, b;
+          jittered_entry(rng_pixel_key(p->seed, gp.x, gp.y), p->grid_m, s < p->spp ? s : 0, a, b);
+          px += (float)a;
+          py += (float)b;
+        } else if (tb) {
+          const volatile LdsF* t = tb;
+          const int ss = s < p->spp ? s : 0;
+          px += t[ss];
+          py += t[p->spp + ss];
+        }
+        // castPrimaryRay (renderer.nim:31-44), constants folded on the host
+        // ((2 x r)/w - r) f == (x - w/2) (2 r f / w): exact 0 on the centre
+        // column / row, as the reference's own formula gives there
+        const float cx = (px - p->cam_b) * p->cam_a;
+        const float cy = (p->cam_d - py) * p->cam_c;
+        const float rl = rsq(__builtin_fmaf(cx, cx, __builtin_fmaf(cy, cy, 1.0f)));
+        const F3 d = f3((cx * p->cam[3] + cy * p->cam[6] - p->cam[9]) * rl, (cx * p->cam[4] + cy * p->cam[7] - p->cam[10]) * rl,
+                        (cx * p->cam[5] + cy * p->cam[8] - p->cam[11]) * rl);
+        const F3 o = f3(p->cam[0], p->cam[1], p->cam[2]);
+        ws.v[STAT_PRIMARY] += pc(bal(sv));
+        RT_STAMP(t_s0);
+        shade_path<COUNT, F, decltype(lean)::value>(p, o, d, sv, sv ? gp.y * p->width + gp.x : -1, pinfo, ls, pacc, ws);
 #if RTMI_STAMPS == 1
-      { RT_STAMP(t_s1); RT_ACC(7, t_s0, t_s1); }
+        { RT_STAMP(t_s1); RT_ACC(7, t_s0, t_s1); }
 #endif
-    }
+      }
+    };
+    const int nlt = p->nlight;
+    if ((F & F_MESH) && !(F & F_REFLECT) && (pinfo & kPixCount) == 0u && nlt <= 8 &&
+        ((pinfo >> 24) & ((1u << nlt) - 1u)) == (1u << nlt) - 1u)
+      sample_loop(Bool<true>{});
+    else
+      sample_loop(Bool<false>{});
     p = params();
     const int lane = lane_id_fresh();
     F3 acc = pacc.v;
