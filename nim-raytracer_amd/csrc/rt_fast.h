@@ -509,6 +509,8 @@ __device__ __forceinline__ Hit trace(KP p, F3 o, F3 d, float tmax, bool active, 
     omask = (todo == 0ull && bal(active && !safe) == 0ull) ? m : omask;
   }
   auto visit = [&](const int i) {
+    // the mesh skipped outright (no record fetch, no hit-mask work)
+    if ((F & F_MESH) && no_mesh && i == p->shadow_mesh) return;
     const FObj ob = at(p->objs, i);
     float t;
     int tri = -1;
