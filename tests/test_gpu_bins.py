@@ -143,3 +143,41 @@ def test_bins_low_spp_falls_back(gpu):
         fa, sa = _render(ds, _opts(240, 135, m, aa=aa))
         fb, sb = _render(ds, _opts(240, 135, m, RT_FLAG_NO_BINNING, aa=aa))
         assert sa == sb and torch.equal(fa, fb), m
+
+
+def _planes_scene(wall):
+    """The bunny over a tilted, rotated ground plane (general transform: the
+    shadow skips' plane footprints go through it), optionally with a back
+    wall (two planes: a pixel's rays may reach either)."""
+    from rtmi.scene import Material, Object, Scene, initPlane
+    mesh = scenes.baked_bunny()
+    mesh.objectToWorld = translate(mat4(1.0), vec3(0.0, 0.0001, -12.0))
+    mesh.worldToObject = inverse(mesh.objectToWorld)
+    g = translate(mat4(1.0), vec3(0.0, -0.4, 0.0))
+    g = rotate(g, X_AXIS, degToRad(4.0))
+    g = rotate(g, Y_AXIS, degToRad(20.0))
+    objects = [Object("bunny", mesh, Material(albedo=vec3(0.6, 0.9, 0.2))),
+               Object("ground", initPlane(objectToWorld=g), Material(albedo=vec3(0.4)))]
+    if wall:
+        w = rotate(translate(mat4(1.0), vec3(0.0, 0.0, -24.0)), X_AXIS, degToRad(90.0))
+        objects.append(Object("wall", initPlane(objectToWorld=w), Material(albedo=vec3(0.3, 0.3, 0.5))))
+    return Scene(objects=objects, lights=scenes._warm_lights(), fov=50.0,
+                 cameraToWorld=scenes._std_camera(0.0, 5.5, 1.5), bgColor=vec3(0.01, 0.03, 0.05))
+
+
+@pytest.mark.parametrize("wall", [False, True])
+def test_pixel_records_tilted_planes_and_bias(gpu, wall):
+    """Pixel records (list length + shadow skips, rebuilt per bias) and the
+    lean sample-loop instance over general-transform planes: bit-identical to
+    the BVH-only kernel at two biases and two sample counts."""
+    import torch
+    ds = DeviceScene(_planes_scene(wall))
+    for bias in (1e-4, 1e-2, 1e-4):
+        for m in (8, 16):
+            o = Options(width=320, height=180, antialias=Antialias(akGrid, m), bias=bias, precision=Precision.fp32)
+            p = Options(width=320, height=180, antialias=Antialias(akGrid, m), bias=bias, precision=Precision.fp32,
+                        flags=RT_FLAG_NO_BINNING)
+            fa, sa = _render(ds, o)
+            fb, sb = _render(ds, p)
+            assert sa == sb, (wall, bias, m)
+            assert torch.equal(fa, fb), (wall, bias, m, float((fa - fb).abs().max()))
