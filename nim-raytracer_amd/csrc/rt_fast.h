@@ -692,7 +692,7 @@ __device__ __forceinline__ void shade_path(KP p, F3 o, F3 d, bool active, int pi
   int depth = 1;
   float w = 1.0f;
   for (int lev = 0; lev < ((F & F_REFLECT) ? kMaxShadeLevels : 1); ++lev) {
-    p = params();
+    if (LEAN == 0) p = params();
     if (bal(act) == 0ull) break;
     const Hit hit = trace<COUNT, F>(p, o, d, finf(), act, false, lev == 0 ? pix : -1, -1, ws,
                                     lev == 0 && (LEAN || (pinfo & kPixCount) == 0u));
@@ -769,7 +769,7 @@ __device__ __forceinline__ void shade_path(KP p, F3 o, F3 d, bool active, int pi
     auto light_loop = [&](auto lean) {
       constexpr bool kLean = decltype(lean)::value;
       for (int li = 0; li < nl; ++li) {
-        p = params();
+        if (!kLean) p = params();
         const FLight L = at(p->lights, li);
         F3 sd;
         float dist, k = 1.0f;
@@ -971,7 +971,7 @@ __global__ __launch_bounds__(256) RTMI_OCC void k_render_fast(const FastParams p
     // compiled without any mesh search
     auto sample_loop = [&](auto lean) {
       for (int it = 0; it < iters; ++it) {
-        p = params();
+        if (!decltype(lean)::value) p = params();
         const int s = it * L + gp.sub;  // this lane's sample index
         const bool sv = gp.valid && s < p->spp;
         float px = (float)gp.x, py = (float)gp.y;
