@@ -243,6 +243,7 @@ struct FastParams {
   float inv_band_h;
   int32_t mode, y0, nrows, ncols, step, max_step, band_h, rank, world;
   int32_t lanes_per_px, log2_lanes, tile_x, tile_y, tiles_x, ngroups;
+  int32_t log2_grid_m;             // akGrid m = 2^log2_grid_m (sample s = (s & (m-1), s >> log2)), or -1
 };
 
 enum : int32_t {

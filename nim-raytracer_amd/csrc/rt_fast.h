@@ -643,7 +643,7 @@ __device__ __forceinline__ F3 analytic_normal(const FObj& ob, F3 ho) {
 // conflicts). Parking the reflected ray and the hit point here instead of in
 // VGPRs takes them out of the register peak, which sits inside the
 // shadow-ray traversal (DESIGN.md "Occupancy").
-enum : int { LDS_RO = 0, LDS_RD = 3, LDS_HW = 6, kLdsSlots = 9 };
+enum : int { LDS_RO = 0, LDS_RD = 3, LDS_HW = 6, LDS_ALB = 9, kLdsSlots = 12 };
 // An LDS-typed pointer: 32-bit addresses with the slot offsets folded into
 // the ds_* immediates (a generic float* here became a 64-bit flat address
 // per slot, hoisted and pinned in VGPRs).
@@ -662,6 +662,25 @@ struct Acc {
 __device__ __forceinline__ void acc_add3(Acc& a, float x, float y, float z) {
   a.v = f3(a.v.x + x, a.v.y + y, a.v.z + z);
 }
+// A shading level's radiance, in the reference's grouping (shade() sums the
+// lights' shadeDiffuse terms, renderer.nim:93-104, and calcPixel adds each
+// sample's colour, renderer.nim:149-157): per light E += ci * ndl (one FMA
+// per channel), then the level adds albedo/pi * weight * E — rounded the same
+// way by every instance of the sample loop (no contraction choices left to
+// the compiler), so the batched lean samples below and the one-sample loop
+// give bit-identical pixels.
+__device__ __forceinline__ void irr_add(F3& e, const float* ci, float ndl) {
+  e = f3(__builtin_fmaf(ci[0], ndl, e.x), __builtin_fmaf(ci[1], ndl, e.y), __builtin_fmaf(ci[2], ndl, e.z));
+}
+// A product the compiler may not fuse into a later add (-ffp-contract=fast
+// contracts HIP's __fmul_rn, a plain `*`, wherever the add happens to be
+// visible): the empty asm makes the product opaque, at no instruction cost.
+__device__ __forceinline__ float mul_nc(float a, float b) {
+  float r = a * b;
+  asm("" : "+v"(r));
+  return r;
+}
+__device__ __forceinline__ F3 mul3(F3 a, F3 b) { return f3(mul_nc(a.x, b.x), mul_nc(a.y, b.y), mul_nc(a.z, b.z)); }
 // volatile: the value must really leave the registers (no store-to-load
 // forwarding across the light loop)
 __device__ __forceinline__ void lds_put3(LdsF* ls, int slot, F3 v) {
@@ -696,7 +715,7 @@ __device__ __forceinline__ void shade_path(KP p, F3 o, F3 d, bool active, int pi
     if (bal(act) == 0ull) break;
     const Hit hit = trace<COUNT, F>(p, o, d, finf(), act, false, lev == 0 ? pix : -1, -1, ws,
                                     lev == 0 && (LEAN || (pinfo & kPixCount) == 0u));
-    if (act && hit.obj < 0) acc_add3(acc, w * p->bg[0], w * p->bg[1], w * p->bg[2]);
+    if (act && hit.obj < 0) acc_add3(acc, mul_nc(w, p->bg[0]), mul_nc(w, p->bg[1]), mul_nc(w, p->bg[2]));
     const bool lit = act && hit.obj >= 0;
     const F3 hw = f3(__builtin_fmaf(d.x, hit.t, o.x), __builtin_fmaf(d.y, hit.t, o.y), __builtin_fmaf(d.z, hit.t, o.z));
     F3 N = f3(0.0f, 0.0f, 0.0f);
@@ -743,7 +762,11 @@ __device__ __forceinline__ void shade_path(KP p, F3 o, F3 d, bool active, int pi
     }
     const bool reflect = (F & F_REFLECT) && lit && refl > 0.0f && depth <= p->max_depth;
     const float wl = reflect ? w * (1.0f - refl) : w;
-    const F3 albw = f3(alb.x * wl, alb.y * wl, alb.z * wl);
+    // albedo/pi * weight waits in LDS across the light loop (the loop's
+    // register peak sits inside the shadow traversal); the lights' terms
+    // are summed into E first (irr_add)
+    lds_put3(ls, LDS_ALB, f3(alb.x * wl, alb.y * wl, alb.z * wl));
+    F3 E = f3(0.0f, 0.0f, 0.0f);
     if (F & F_REFLECT) ws.v[STAT_REFL] += pc(bal(reflect));
     if ((F & F_REFLECT) && bal(reflect)) {  // park the reflected ray (renderer.nim:109-118)
       if (reflect) {
@@ -788,16 +811,17 @@ __device__ __forceinline__ void shade_path(KP p, F3 o, F3 d, bool active, int pi
         ws.v[STAT_SHADOW] += pc(bal(lit));
         const Hit sh = trace<COUNT, F>(p, so, sd, dist, lit, true, -1, li, ws,
                                        kLean || (li < 8 && ((skipw >> li) & 1u) != 0u));
-        if (lit && sh.obj < 0) {  // shadeDiffuse (shader.nim:12-17)
-          const float ndl = fmaxf(dot3(N, sd), 0.0f) * k;
-          acc_add3(acc, albw.x * L.ci[0] * ndl, albw.y * L.ci[1] * ndl, albw.z * L.ci[2] * ndl);
-        }
+        if (lit && sh.obj < 0) irr_add(E, L.ci, fmaxf(dot3(N, sd), 0.0f) * k);  // shadeDiffuse (shader.nim:12-17)
       }
     };
     if (LEAN || ((F & F_MESH) && nl > 0 && nl <= 8 && skipw == (1u << nl) - 1u))
       light_loop(Bool<true>{});
     else
       light_loop(Bool<false>{});
+    if (lit) {
+      const F3 a = mul3(lds_get3(ls, LDS_ALB), E);
+      acc_add3(acc, a.x, a.y, a.z);
+    }
     // every lane reloads (lanes that do not reflect go inactive): o and d
     // are then dead across the light loop instead of carried for them
     if ((F & F_REFLECT) && bal(reflect)) {
@@ -874,6 +898,211 @@ __device__ __forceinline__ GroupPix group_pixel(KP p, int g, int lane) {
     if ((r.x & mask) == 0 && (r.y & mask) == 0) r.valid = false;
   }
   return r;
+}
+
+// castPrimaryRay (renderer.nim:31-44) for sample s of the lane's pixel
+// (calcPixel's sample table, renderer.nim:144-159): the direction (the
+// origin is the camera's, p->cam[0..2]). Camera constants are folded on the
+// host: ((2 x r)/w - r) f == (x - w/2) (2 r f / w), exact 0 on the centre
+// column / row as the reference's own formula gives there. Every FMA is
+// explicit, so all instances of the sample loop round alike.
+template <unsigned F>
+__device__ __forceinline__ F3 camera_dir(KP p, const GroupPix& gp, int s, const LdsF* tb) {
+  float px = (float)gp.x, py = (float)gp.y;
+  if (p->aa_kind == 1) {  // grid() sampling.nim:5-18: sample s = (si, sj)
+    int si, sj;
+    if (p->log2_grid_m >= 0) {
+      si = s & (p->grid_m - 1);
+      sj = s >> p->log2_grid_m;
+    } else {
+      sj = div_small(s, p->grid_m, p->sample_step, si);
+    }
+    px += __builtin_fmaf((float)si, p->sample_step, p->sample_off);
+    py += __builtin_fmaf((float)sj, p->sample_step, p->sample_off);
+  } else if ((F & F_STOCHASTIC) && p->aa_kind == 2) {  // jitteredGrid (sampling.nim:21-33): no table needed
+    double a, b;
+    jittered_entry(rng_pixel_key(p->seed, gp.x, gp.y), p->grid_m, s, a, b);
+    px += (float)a;
+    py += (float)b;
+  } else if ((F & F_STOCHASTIC) && tb) {
+    const volatile LdsF* t = tb;
+    px += t[s];
+    py += t[p->spp + s];
+  }
+  const float cx = (px - p->cam_b) * p->cam_a;
+  const float cy = (p->cam_d - py) * p->cam_c;
+  const float rl = rsq(__builtin_fmaf(cx, cx, __builtin_fmaf(cy, cy, 1.0f)));
+  return f3(__builtin_fmaf(cx, p->cam[3], __builtin_fmaf(cy, p->cam[6], -p->cam[9])) * rl,
+            __builtin_fmaf(cx, p->cam[4], __builtin_fmaf(cy, p->cam[7], -p->cam[10])) * rl,
+            __builtin_fmaf(cx, p->cam[5], __builtin_fmaf(cy, p->cam[8], -p->cam[11])) * rl);
+}
+
+// Lean pixels, kLeanBatch samples per lane at once. A lean pixel (one-pixel
+// wave; its pixel list is empty and every light is a distant light whose
+// shadow skip bit is set, no reflection: FastParams.pix_info) never touches
+// the mesh, so its samples only visit the analytic objects. The per-sample
+// loop pays the scalar work of every object visit (record loads, type
+// dispatch, loop control, hit-count popcounts: the CU's one scalar unit,
+// shared by its 32 resident waves, is the kernel's busiest pipe) once per 64
+// rays; here each lane carries kLeanBatch samples through the same object
+// and light loops, so that work is paid once per 64 x kLeanBatch rays. Same
+// arithmetic per sample as shade_path (camera_dir, analytic_t, the
+// irradiance sum), the samples' colours added to the pixel in sample order:
+// frames bit-identical to the one-sample loop (tests: binned vs
+// RT_FLAG_NO_BINNING, which takes no pixel records).
+constexpr int kLeanBatch = 4;
+template <unsigned F>
+__device__ __forceinline__ void lean_batch(KP p, const GroupPix& gp, int it0, const LdsF* tb, Acc& acc,
+                                           Stats32& ws) {
+  // Branch-free: per-sample predicates are lane masks in SGPRs and every
+  // update is a select (v_cndmask), so the samples' code is straight-line
+  // VALU (no exec-mask save / restore per sample). A masked-off term adds an
+  // exact zero (fma(ci, 0, E) == E, acc + 0 == acc for the non-negative
+  // sums), so values equal shade_path's branchy ones bit for bit.
+  constexpr int S = kLeanBatch;
+  const F3 o = f3(p->cam[0], p->cam[1], p->cam[2]);
+  F3 d[S];
+  unsigned long long svm[S];  // valid samples
+#pragma unroll
+  for (int k = 0; k < S; ++k) {
+    const int s = (it0 + k) * 64 + gp.sub;
+    svm[k] = bal(gp.valid && s < p->spp);
+    d[k] = camera_dir<F>(p, gp, s < p->spp ? s : 0, tb);
+    ws.v[STAT_PRIMARY] += pc(svm[k]);
+  }
+  // trace (renderer.nim:47-67) of the camera rays over the analytic objects
+  // in scene order (the mesh is left out: none of the pixel's rays can hit it)
+  const int nobj = p->nobj, mesh = p->shadow_mesh;
+  float th[S];
+  int hob[S];
+#pragma unroll
+  for (int k = 0; k < S; ++k) {
+    th[k] = finf();
+    hob[k] = -1;
+  }
+  for (int i = 0; i < nobj; ++i) {
+    if (i == mesh) continue;
+    const FObj ob = at(p->objs, i);
+#pragma unroll
+    for (int k = 0; k < S; ++k) {
+      const float t = analytic_t<F>(p, ob, i, o, d[k]);
+      const unsigned long long um = m_ge(t, 0.0f) & m_lt(t, th[k]) & svm[k];
+      ws.v[STAT_HITS] += pc(um);
+      th[k] = lane_in(um) ? t : th[k];
+      hob[k] = lane_in(um) ? i : hob[k];
+    }
+  }
+  // shade (renderer.nim:71-127): normals per distinct object hit, the shadow
+  // origins hitW + N * bias. A hit has t < inf (it beat the initial limit).
+  unsigned long long litm[S], pend[S];
+  F3 N[S], so[S];
+#pragma unroll
+  for (int k = 0; k < S; ++k) {
+    litm[k] = m_lt(th[k], finf()) & svm[k];
+    pend[k] = litm[k];
+    N[k] = f3(0.0f, 0.0f, 0.0f);
+    so[k] = f3(__builtin_fmaf(d[k].x, th[k], o.x), __builtin_fmaf(d[k].y, th[k], o.y),
+               __builtin_fmaf(d[k].z, th[k], o.z));  // the hit point until N is known
+  }
+  for (;;) {
+    int oi = -1;
+#pragma unroll
+    for (int k = S - 1; k >= 0; --k)
+      if (pend[k]) oi = __builtin_amdgcn_readlane(hob[k], (int)__builtin_ctzll(pend[k]));
+    if (oi < 0) break;
+    int oi_cmp = oi;
+    asm volatile("" : "+s"(oi_cmp));
+    const FObj ob = at(p->objs, oi);
+    const RT_CONST FObjX& ox = at(p->objx, oi);
+#pragma unroll
+    for (int k = 0; k < S; ++k) {
+      const unsigned long long mine = bal(hob[k] == oi_cmp) & pend[k];
+      pend[k] &= ~mine;
+      F3 ho, unused;
+      to_object<F>(p, ob, oi, so[k], f3(0.0f, 0.0f, 0.0f), ho, unused);
+      F3 n = analytic_normal<F>(ob, ho);
+      if ((F & F_XF_GENERAL) && ob.xf == XF_GENERAL) {  // object_to_world * n, not re-normalised
+        const float* m = ox.o2w;
+        n = f3(__builtin_fmaf(m[0], n.x, __builtin_fmaf(m[3], n.y, m[6] * n.z)),
+               __builtin_fmaf(m[1], n.x, __builtin_fmaf(m[4], n.y, m[7] * n.z)),
+               __builtin_fmaf(m[2], n.x, __builtin_fmaf(m[5], n.y, m[8] * n.z)));
+      }
+      const bool mi = lane_in(mine);
+      N[k] = f3(mi ? n.x : N[k].x, mi ? n.y : N[k].y, mi ? n.z : N[k].z);
+    }
+  }
+  const float bias = p->bias;
+#pragma unroll
+  for (int k = 0; k < S; ++k)
+    so[k] = f3(__builtin_fmaf(N[k].x, bias, so[k].x), __builtin_fmaf(N[k].y, bias, so[k].y),
+               __builtin_fmaf(N[k].z, bias, so[k].z));
+  // one shadow ray per light and lit sample (distant lights only: a point
+  // light has no skip bit, so its pixels are never lean)
+  F3 E[S];
+  unsigned long long anylit = 0ull;
+#pragma unroll
+  for (int k = 0; k < S; ++k) {
+    E[k] = f3(0.0f, 0.0f, 0.0f);
+    anylit |= litm[k];
+  }
+  const int nl = anylit ? p->nlight : 0;
+  for (int li = 0; li < nl; ++li) {
+    const FLight L = at(p->lights, li);
+    const F3 sd = f3(-L.v[0], -L.v[1], -L.v[2]);
+    float ts[S];
+#pragma unroll
+    for (int k = 0; k < S; ++k) {
+      ws.v[STAT_SHADOW] += pc(litm[k]);
+      ts[k] = finf();
+    }
+    for (int i = 0; i < nobj; ++i) {
+      if (i == mesh) continue;
+      const FObj ob = at(p->objs, i);
+#pragma unroll
+      for (int k = 0; k < S; ++k) {
+        const float t = analytic_t<F>(p, ob, i, so[k], sd);
+        const unsigned long long um = m_ge(t, 0.0f) & m_lt(t, ts[k]) & litm[k];
+        ws.v[STAT_HITS] += pc(um);
+        ts[k] = lane_in(um) ? t : ts[k];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < S; ++k) {  // unoccluded: shadeDiffuse (shader.nim:12-17)
+      const bool vis = lane_in(litm[k] & ~m_lt(ts[k], finf()));
+      irr_add(E[k], L.ci, vis ? fmaxf(dot3(N[k], sd), 0.0f) : 0.0f);
+    }
+  }
+  // albedo / pi per distinct object hit, then the samples' colours in order
+  // (the sky: the background, renderer.nim:74-75)
+#pragma unroll
+  for (int k = 0; k < S; ++k) pend[k] = litm[k];
+  for (;;) {
+    int oi = -1;
+#pragma unroll
+    for (int k = S - 1; k >= 0; --k)
+      if (pend[k]) oi = __builtin_amdgcn_readlane(hob[k], (int)__builtin_ctzll(pend[k]));
+    if (oi < 0) break;
+    int oi_cmp = oi;
+    asm volatile("" : "+s"(oi_cmp));
+    const RT_CONST FObjX& ox = at(p->objx, oi);
+    const F3 alb = f3(ox.albedo_pi[0], ox.albedo_pi[1], ox.albedo_pi[2]);
+#pragma unroll
+    for (int k = 0; k < S; ++k) {
+      const unsigned long long mine = bal(hob[k] == oi_cmp) & pend[k];
+      pend[k] &= ~mine;
+      const F3 a = mul3(alb, E[k]);
+      const bool mi = lane_in(mine);
+      E[k] = f3(mi ? a.x : E[k].x, mi ? a.y : E[k].y, mi ? a.z : E[k].z);
+    }
+  }
+  const F3 bg = f3(p->bg[0], p->bg[1], p->bg[2]);
+#pragma unroll
+  for (int k = 0; k < S; ++k) {
+    const bool lt = lane_in(litm[k]), sky = lane_in(svm[k] & ~litm[k]);
+    const F3 c = f3(lt ? E[k].x : (sky ? bg.x : 0.0f), lt ? E[k].y : (sky ? bg.y : 0.0f),
+                    lt ? E[k].z : (sky ? bg.z : 0.0f));
+    acc_add3(acc, c.x, c.y, c.z);
+  }
 }
 
 template <bool COUNT, unsigned F>
@@ -966,39 +1195,14 @@ __global__ __launch_bounds__(256) RTMI_OCC void k_render_fast(const FastParams p
         pinfo = at(p->pix_info, up);
       }
     }
-    // a lean pixel (no camera ray can hit the mesh, every light's shadow
-    // rays skip it; no reflection) runs an instance of the sample loop
-    // compiled without any mesh search
-    auto sample_loop = [&](auto lean) {
-      for (int it = 0; it < iters; ++it) {
+    // the per-sample loop; its LEAN instance is compiled without any mesh
+    // search (below)
+    auto sample_loop = [&](auto lean, int it_begin) {
+      for (int it = it_begin; it < iters; ++it) {
         if (!decltype(lean)::value) p = params();
         const int s = it * L + gp.sub;  // this lane's sample index
         const bool sv = gp.valid && s < p->spp;
-        float px = (float)gp.x, py = (float)gp.y;
-        if (p->aa_kind == 1) {  // grid() sampling.nim:5-18: sample s = (si, sj)
-          int si;
-          const int sj = div_small(s, p->grid_m, p->sample_step, si);
-          px += __builtin_fmaf((float)si, p->sample_step, p->sample_off);
-          py += __builtin_fmaf((float)sj, p->sample_step, p->sample_off);
-        } else if ((F & F_STOCHASTIC) && p->aa_kind == 2) {  // jitteredGrid (sampling.nim:21-33): no table needed
-          double a, b;
-          jittered_entry(rng_pixel_key(p->seed, gp.x, gp.y), p->grid_m, s < p->spp ? s : 0, a, b);
-          px += (float)a;
-          py += (float)b;
-        } else if (tb) {
-          const volatile LdsF* t = tb;
-          const int ss = s < p->spp ? s : 0;
-          px += t[ss];
-          py += t[p->spp + ss];
-        }
-        // castPrimaryRay (renderer.nim:31-44), constants folded on the host
-        // ((2 x r)/w - r) f == (x - w/2) (2 r f / w): exact 0 on the centre
-        // column / row, as the reference's own formula gives there
-        const float cx = (px - p->cam_b) * p->cam_a;
-        const float cy = (p->cam_d - py) * p->cam_c;
-        const float rl = rsq(__builtin_fmaf(cx, cx, __builtin_fmaf(cy, cy, 1.0f)));
-        const F3 d = f3((cx * p->cam[3] + cy * p->cam[6] - p->cam[9]) * rl, (cx * p->cam[4] + cy * p->cam[7] - p->cam[10]) * rl,
-                        (cx * p->cam[5] + cy * p->cam[8] - p->cam[11]) * rl);
+        const F3 d = camera_dir<F>(p, gp, s < p->spp ? s : 0, tb);
         const F3 o = f3(p->cam[0], p->cam[1], p->cam[2]);
         ws.v[STAT_PRIMARY] += pc(bal(sv));
         RT_STAMP(t_s0);
@@ -1010,10 +1214,20 @@ __global__ __launch_bounds__(256) RTMI_OCC void k_render_fast(const FastParams p
     };
     const int nlt = p->nlight;
     if ((F & F_MESH) && !(F & F_REFLECT) && (pinfo & kPixCount) == 0u && nlt <= 8 &&
-        ((pinfo >> 24) & ((1u << nlt) - 1u)) == (1u << nlt) - 1u)
-      sample_loop(Bool<true>{});
-    else
-      sample_loop(Bool<false>{});
+        !((F & F_POINT) && p->has_point_light) &&
+        ((pinfo >> 24) & ((1u << nlt) - 1u)) == (1u << nlt) - 1u) {
+      // a lean pixel (no camera ray can hit the mesh, every light's shadow
+      // rays skip it; no reflection): batches of samples per lane, then
+      // the remaining iterations one at a time — both compiled without any
+      // mesh search
+      int it = 0;
+#ifndef RTMI_NO_LEAN_BATCH
+      for (; it + kLeanBatch <= iters; it += kLeanBatch) lean_batch<F>(p, gp, it, tb, pacc, ws);
+#endif
+      if (it < iters) sample_loop(Bool<true>{}, it);
+    } else {
+      sample_loop(Bool<false>{}, 0);
+    }
     p = params();
     const int lane = lane_id_fresh();
     F3 acc = pacc.v;

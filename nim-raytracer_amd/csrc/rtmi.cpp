@@ -1168,6 +1168,9 @@ void fill_fast(rt_scene* s, const rt_options* o, const Mapping& mp, float* fb, F
   p.inv_len = (float)(1.0 / (double)spp);
   p.sample_step = (float)(1.0 / (double)m);
   p.sample_off = (float)(1.0 / (double)m * 0.5);
+  p.log2_grid_m = -1;
+  for (int k = 0; k <= 12; ++k)
+    if (m == (1 << k)) p.log2_grid_m = k;
   p.nobj = s->nobj;
   p.nlight = s->nlight;
   p.has_point_light = s->has_point_light;
