@@ -165,6 +165,12 @@ typedef struct rt_options {
  * one mesh object search the faces binned for their pixel / light-grid cell
  * instead. The image and Stats are the same either way. */
 #define RT_FLAG_NO_BINNING 0x8u
+/* float32 kernel: render every pixel group with the one general kernel. By
+ * default a launch whose pixel records mark pixels lean (no camera ray can hit
+ * the scene's mesh and every light is a distant light whose shadow rays
+ * provably miss it) renders those pixels with a second, lean-only kernel from
+ * a per-launch list. Scheduling only: the image and Stats are the same. */
+#define RT_FLAG_NO_SPLIT 0x10u
 
 /* Stats (src/renderer/stats.nim:4-13) plus ray counts for Mray/s. */
 typedef struct rt_stats {

@@ -244,6 +244,10 @@ struct FastParams {
   int32_t mode, y0, nrows, ncols, step, max_step, band_h, rank, world;
   int32_t lanes_per_px, log2_lanes, tile_x, tile_y, tiles_x, ngroups;
   int32_t log2_grid_m;             // akGrid m = 2^log2_grid_m (sample s = (s & (m-1), s >> log2)), or -1
+  int32_t iters;                   // sample iterations per work item: ceil(spp / lanes_per_px)
+  uint32_t tx_magic;               // g / tiles_x == (g * tx_magic) >> tx_shift for 0 <= g < 2^31
+  int32_t tx_shift;
+  int32_t stat_flush;              // work items between flushes of the 32-bit wave Stats counters
 };
 
 enum : int32_t {
@@ -267,6 +271,8 @@ extern "C" {
 int rtmi_launch_render_f32(const rtmi::FastParams* p, unsigned subset, int blocks, size_t shmem, void* stream);
 int rtmi_launch_render_f64(const rtmi::RenderParams<double>* p, int blocks, void* stream);
 int rtmi_render_f32_blocks_per_cu(int count, unsigned subset, size_t shmem);
+int rtmi_launch_lean_f32(const rtmi::FastParams* p, unsigned subset, int blocks, size_t shmem, void* stream);
+int rtmi_lean_f32_blocks_per_cu(unsigned subset, size_t shmem);
 int rtmi_launch_ppm_encode(const float* fb, long long n, int bits, int srgb, void* out, void* stream);
 int rtmi_launch_rgba_encode(const float* fb, long long npix, unsigned int alpha, void* out, void* stream);
 // Sets this thread's rt_last_error() text; returns code (rtmi.cpp).

@@ -834,6 +834,10 @@ __device__ __forceinline__ void shade_path(KP p, F3 o, F3 d, bool active, int pi
   }
 }
 
+#ifndef RTMI_QUEUE_AHEAD
+#define RTMI_QUEUE_AHEAD 1
+#endif
+
 // Occupancy target: the kernel is latency-bound (serial node-fetch chains),
 // so resident waves matter more than a few spills in the outer loops.
 // 8 waves/SIMD (<= 64 VGPRs) for every feature subset except meshes combined
@@ -878,7 +882,8 @@ __device__ __forceinline__ GroupPix group_pixel(KP p, int g, int lane) {
   r.sub = lane & (p->lanes_per_px - 1);
   const int pix = lane >> p->log2_lanes;
   const int tpx = pix & (p->tile_x - 1), tpy = pix >> p->log2_tile_x;
-  const int gy = g / p->tiles_x, gx = g - gy * p->tiles_x;  // wave-uniform (scalar)
+  const int gy = (int)(((unsigned long long)(unsigned)g * p->tx_magic) >> p->tx_shift);  // g / tiles_x (scalar)
+  const int gx = g - gy * p->tiles_x;
   const int j = gx * p->tile_x + tpx;
   const int k = gy * p->tile_y + tpy;
   r.x = j * p->step;
@@ -906,8 +911,55 @@ __device__ __forceinline__ GroupPix group_pixel(KP p, int g, int lane) {
 // host: ((2 x r)/w - r) f == (x - w/2) (2 r f / w), exact 0 on the centre
 // column / row as the reference's own formula gives there. Every FMA is
 // explicit, so all instances of the sample loop round alike.
+__device__ __forceinline__ F3 camera_ray_dir(KP p, float px, float py) {
+  const float cx = (px - p->cam_b) * p->cam_a;
+  const float cy = (p->cam_d - py) * p->cam_c;
+  const float rl = rsq(__builtin_fmaf(cx, cx, __builtin_fmaf(cy, cy, 1.0f)));
+  return f3(__builtin_fmaf(cx, p->cam[3], __builtin_fmaf(cy, p->cam[6], -p->cam[9])) * rl,
+            __builtin_fmaf(cx, p->cam[4], __builtin_fmaf(cy, p->cam[7], -p->cam[10])) * rl,
+            __builtin_fmaf(cx, p->cam[5], __builtin_fmaf(cy, p->cam[8], -p->cam[11])) * rl);
+}
+
+// Sum of a per-lane count over the wave (DPP row sums, then the rows).
+__device__ __forceinline__ unsigned wave_sum(unsigned v) {
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x111, 0xf, 0xf, false);  // row_shr:1
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x112, 0xf, 0xf, false);  // row_shr:2
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x114, 0xf, 0xf, false);  // row_shr:4
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x118, 0xf, 0xf, false);  // row_shr:8 -> lane 15 of each row: its row's sum
+  return (unsigned)__builtin_amdgcn_readlane((int)v, 15) + (unsigned)__builtin_amdgcn_readlane((int)v, 31) +
+         (unsigned)__builtin_amdgcn_readlane((int)v, 47) + (unsigned)__builtin_amdgcn_readlane((int)v, 63);
+}
+
+// Sum of a float over the wave, in lane 63's order-independent-of-data
+// sequence (DPP row_shr scans, then row_bcast:15 / :31), returned uniform.
+template <int CTRL, int ROWS>
+__device__ __forceinline__ float dpp_add(float v) {
+  return v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, ROWS, 0xf, false));
+}
+__device__ __forceinline__ float wave_total(float v) {
+  v = dpp_add<0x111, 0xf>(v);  // row_shr:1
+  v = dpp_add<0x112, 0xf>(v);  // row_shr:2
+  v = dpp_add<0x114, 0xf>(v);  // row_shr:4
+  v = dpp_add<0x118, 0xf>(v);  // row_shr:8: lane 15 of each row holds its row's sum
+  v = dpp_add<0x142, 0xa>(v);  // row_bcast:15 into rows 1 and 3
+  v = dpp_add<0x143, 0xc>(v);  // row_bcast:31 into rows 2 and 3: lane 63 holds the total
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+
+// The wave's 32-bit Stats counters into its 64-bit LDS totals (lane k adds
+// slot k), then cleared.
+__device__ __forceinline__ void flush_stats(Stats32& ws, unsigned long long* tot, int lane) {
+  unsigned int v = 0u;
+#pragma unroll
+  for (int k = 0; k < kStatSlots; ++k) v = lane == k ? ws.v[k] : v;
+  if (lane < kStatSlots) tot[lane] += v;
+#pragma unroll
+  for (int k = 0; k < kStatSlots; ++k) ws.v[k] = 0u;
+}
+
 template <unsigned F>
-__device__ __forceinline__ F3 camera_dir(KP p, const GroupPix& gp, int s, const LdsF* tb) {
+__device__ __forceinline__ void camera_pos(KP p, const GroupPix& gp, int s, const LdsF* tb, float& px_out,
+                                           float& py_out) {
   float px = (float)gp.x, py = (float)gp.y;
   if (p->aa_kind == 1) {  // grid() sampling.nim:5-18: sample s = (si, sj)
     int si, sj;
@@ -929,12 +981,14 @@ __device__ __forceinline__ F3 camera_dir(KP p, const GroupPix& gp, int s, const 
     px += t[s];
     py += t[p->spp + s];
   }
-  const float cx = (px - p->cam_b) * p->cam_a;
-  const float cy = (p->cam_d - py) * p->cam_c;
-  const float rl = rsq(__builtin_fmaf(cx, cx, __builtin_fmaf(cy, cy, 1.0f)));
-  return f3(__builtin_fmaf(cx, p->cam[3], __builtin_fmaf(cy, p->cam[6], -p->cam[9])) * rl,
-            __builtin_fmaf(cx, p->cam[4], __builtin_fmaf(cy, p->cam[7], -p->cam[10])) * rl,
-            __builtin_fmaf(cx, p->cam[5], __builtin_fmaf(cy, p->cam[8], -p->cam[11])) * rl);
+  px_out = px;
+  py_out = py;
+}
+template <unsigned F>
+__device__ __forceinline__ F3 camera_dir(KP p, const GroupPix& gp, int s, const LdsF* tb) {
+  float px, py;
+  camera_pos<F>(p, gp, s, tb, px, py);
+  return camera_ray_dir(p, px, py);
 }
 
 // Lean pixels, kLeanBatch samples per lane at once. A lean pixel (one-pixel
@@ -951,7 +1005,7 @@ __device__ __forceinline__ F3 camera_dir(KP p, const GroupPix& gp, int s, const 
 // frames bit-identical to the one-sample loop (tests: binned vs
 // RT_FLAG_NO_BINNING, which takes no pixel records).
 constexpr int kLeanBatch = 4;
-template <unsigned F>
+template <unsigned F, int S = kLeanBatch>
 __device__ __forceinline__ void lean_batch(KP p, const GroupPix& gp, int it0, const LdsF* tb, Acc& acc,
                                            Stats32& ws) {
   // Branch-free: per-sample predicates are lane masks in SGPRs and every
@@ -959,37 +1013,63 @@ __device__ __forceinline__ void lean_batch(KP p, const GroupPix& gp, int it0, co
   // VALU (no exec-mask save / restore per sample). A masked-off term adds an
   // exact zero (fma(ci, 0, E) == E, acc + 0 == acc for the non-negative
   // sums), so values equal shade_path's branchy ones bit for bit.
-  constexpr int S = kLeanBatch;
+#ifdef RTMI_DIAG_NOSAMPLES
+  return;  // diagnostic build only: the work-item overhead without the samples
+#endif
   const F3 o = f3(p->cam[0], p->cam[1], p->cam[2]);
-  F3 d[S];
-  unsigned long long svm[S];  // valid samples
+  // sample positions: akGrid with m a power of two (C2-C5) as
+  // s = (s & (m-1), s >> log2 m), the sampler decided once for the batch
+  float px[S], py[S];
+  bool sv[S];
+  if (p->aa_kind == 1 && p->log2_grid_m >= 0) {
+    const int mm = p->grid_m - 1, lg = p->log2_grid_m;
+    const float st = p->sample_step, of = p->sample_off;
 #pragma unroll
-  for (int k = 0; k < S; ++k) {
-    const int s = (it0 + k) * 64 + gp.sub;
-    svm[k] = bal(gp.valid && s < p->spp);
-    d[k] = camera_dir<F>(p, gp, s < p->spp ? s : 0, tb);
-    ws.v[STAT_PRIMARY] += pc(svm[k]);
+    for (int k = 0; k < S; ++k) {
+      const int s = (it0 + k) * 64 + gp.sub;
+      sv[k] = gp.valid && s < p->spp;
+      px[k] = (float)gp.x + __builtin_fmaf((float)(s & mm), st, of);
+      py[k] = (float)gp.y + __builtin_fmaf((float)(s >> lg), st, of);
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < S; ++k) {
+      const int s = (it0 + k) * 64 + gp.sub;
+      sv[k] = gp.valid && s < p->spp;
+      camera_pos<F>(p, gp, s < p->spp ? s : 0, tb, px[k], py[k]);
+    }
   }
+  F3 d[S];
+  unsigned nprim = 0u;
   // trace (renderer.nim:47-67) of the camera rays over the analytic objects
-  // in scene order (the mesh is left out: none of the pixel's rays can hit it)
-  const int nobj = p->nobj, mesh = p->shadow_mesh;
+  // in scene order (the mesh is left out: none of the pixel's rays can hit
+  // it). A hit is t >= 0 below the running minimum th; invalid samples start
+  // at th = -1, which no t >= 0 is below (so th alone says: -1 invalid,
+  // +inf sky, else a hit). Per-lane hit counts (VALU) instead of a mask
+  // popcount per sample and object (SALU).
   float th[S];
   int hob[S];
 #pragma unroll
   for (int k = 0; k < S; ++k) {
-    th[k] = finf();
+    d[k] = camera_ray_dir(p, px[k], py[k]);
+    nprim += pc(bal(sv[k]));
+    th[k] = sv[k] ? finf() : -1.0f;
     hob[k] = -1;
   }
+  ws.v[STAT_PRIMARY] += nprim;
+  const int nobj = p->nobj, mesh = p->shadow_mesh;
+  unsigned hitl = 0u;
   for (int i = 0; i < nobj; ++i) {
     if (i == mesh) continue;
     const FObj ob = at(p->objs, i);
 #pragma unroll
     for (int k = 0; k < S; ++k) {
       const float t = analytic_t<F>(p, ob, i, o, d[k]);
-      const unsigned long long um = m_ge(t, 0.0f) & m_lt(t, th[k]) & svm[k];
-      ws.v[STAT_HITS] += pc(um);
-      th[k] = lane_in(um) ? t : th[k];
-      hob[k] = lane_in(um) ? i : hob[k];
+      const float tp = t >= 0.0f ? t : finf();
+      const bool c = tp < th[k];
+      th[k] = c ? tp : th[k];
+      hob[k] = c ? i : hob[k];
+      hitl += c ? 1u : 0u;
     }
   }
   // shade (renderer.nim:71-127): normals per distinct object hit, the shadow
@@ -998,7 +1078,7 @@ __device__ __forceinline__ void lean_batch(KP p, const GroupPix& gp, int it0, co
   F3 N[S], so[S];
 #pragma unroll
   for (int k = 0; k < S; ++k) {
-    litm[k] = m_lt(th[k], finf()) & svm[k];
+    litm[k] = m_lt(th[k], finf()) & m_ge(th[k], 0.0f);
     pend[k] = litm[k];
     N[k] = f3(0.0f, 0.0f, 0.0f);
     so[k] = f3(__builtin_fmaf(d[k].x, th[k], o.x), __builtin_fmaf(d[k].y, th[k], o.y),
@@ -1046,32 +1126,35 @@ __device__ __forceinline__ void lean_batch(KP p, const GroupPix& gp, int it0, co
     anylit |= litm[k];
   }
   const int nl = anylit ? p->nlight : 0;
+  unsigned nlit = 0u;
+#pragma unroll
+  for (int k = 0; k < S; ++k) nlit += pc(litm[k]);
+  ws.v[STAT_SHADOW] += (unsigned)nl * nlit;
   for (int li = 0; li < nl; ++li) {
     const FLight L = at(p->lights, li);
     const F3 sd = f3(-L.v[0], -L.v[1], -L.v[2]);
-    float ts[S];
+    float ts[S];  // unlit samples start at 0 (take no part)
 #pragma unroll
-    for (int k = 0; k < S; ++k) {
-      ws.v[STAT_SHADOW] += pc(litm[k]);
-      ts[k] = finf();
-    }
+    for (int k = 0; k < S; ++k) ts[k] = lane_in(litm[k]) ? finf() : 0.0f;
     for (int i = 0; i < nobj; ++i) {
       if (i == mesh) continue;
       const FObj ob = at(p->objs, i);
 #pragma unroll
       for (int k = 0; k < S; ++k) {
         const float t = analytic_t<F>(p, ob, i, so[k], sd);
-        const unsigned long long um = m_ge(t, 0.0f) & m_lt(t, ts[k]) & litm[k];
-        ws.v[STAT_HITS] += pc(um);
-        ts[k] = lane_in(um) ? t : ts[k];
+        const float tp = t >= 0.0f ? t : finf();
+        const bool c = tp < ts[k];
+        ts[k] = c ? tp : ts[k];
+        hitl += c ? 1u : 0u;
       }
     }
 #pragma unroll
     for (int k = 0; k < S; ++k) {  // unoccluded: shadeDiffuse (shader.nim:12-17)
-      const bool vis = lane_in(litm[k] & ~m_lt(ts[k], finf()));
+      const bool vis = lane_in(litm[k]) && !(ts[k] < finf());
       irr_add(E[k], L.ci, vis ? fmaxf(dot3(N[k], sd), 0.0f) : 0.0f);
     }
   }
+  ws.v[STAT_HITS] += wave_sum(hitl);
   // albedo / pi per distinct object hit, then the samples' colours in order
   // (the sky: the background, renderer.nim:74-75)
 #pragma unroll
@@ -1098,10 +1181,81 @@ __device__ __forceinline__ void lean_batch(KP p, const GroupPix& gp, int it0, co
   const F3 bg = f3(p->bg[0], p->bg[1], p->bg[2]);
 #pragma unroll
   for (int k = 0; k < S; ++k) {
-    const bool lt = lane_in(litm[k]), sky = lane_in(svm[k] & ~litm[k]);
+    const bool lt = lane_in(litm[k]), sky = th[k] == finf();
     const F3 c = f3(lt ? E[k].x : (sky ? bg.x : 0.0f), lt ? E[k].y : (sky ? bg.y : 0.0f),
                     lt ? E[k].z : (sky ? bg.z : 0.0f));
     acc_add3(acc, c.x, c.y, c.z);
+  }
+}
+
+// multiJittered / correlatedMultiJittered (sampling.nim:39-113): the wave
+// builds each of its pixels' (m, m) tables in LDS — canonical entries spread
+// over the pixel's lanes, then the x shuffle with one lane per column and
+// the y shuffle with one lane per row (each lane only touches its own column
+// / row, so the sequential reference order holds per lane; rt_sampling.h
+// draw indices). nullptr for the other samplers.
+template <unsigned F>
+__device__ __forceinline__ LdsF* sample_table(KP p, const GroupPix& gp, float* sample_lds, int wib, int L) {
+  LdsF* tb = nullptr;
+  if ((F & F_STOCHASTIC) && p->aa_kind >= 3) {
+    const int m = p->grid_m, spp = p->spp;
+    const uint64_t key = rng_pixel_key(p->seed, gp.x, gp.y);
+    tb = (LdsF*)sample_lds + ((size_t)(wib * (64 / L) + (lane_id_fresh() >> p->log2_lanes)) * 2 * spp);
+    volatile LdsF* t = tb;
+    for (int e = gp.sub; e < spp; e += L) {
+      double a, b;
+      canonical_entry(key, m, e, a, b);
+      t[e] = (float)a;
+      t[spp + e] = (float)b;
+    }
+    const uint64_t bx = 2 * (uint64_t)spp;
+    const uint64_t by = bx + (p->aa_kind == 3 ? (uint64_t)spp : (uint64_t)m);
+    if (gp.sub < m) {
+      const int i = gp.sub;  // column i: the x shuffle
+      for (int j = 0; j < m; ++j) {
+        const int k = rng_pick(rng_draw(key, p->aa_kind == 3 ? bx + (uint64_t)j * m + i : bx + (uint64_t)j), j, m);
+        const float a = t[j * m + i], b = t[k * m + i];
+        t[j * m + i] = b;
+        t[k * m + i] = a;
+      }
+      const int j = gp.sub;  // row j: the y shuffle
+      for (int ii = 0; ii < m; ++ii) {
+        const int k = rng_pick(rng_draw(key, p->aa_kind == 3 ? by + (uint64_t)ii * m + j : by + (uint64_t)ii), ii, m);
+        const float a = t[spp + j * m + ii], b = t[spp + j * m + k];
+        t[spp + j * m + ii] = b;
+        t[spp + j * m + k] = a;
+      }
+    }
+  }
+  return tb;
+}
+
+// The end of a work item: the pixel sums over the pixel's lanes, divided by
+// the sample count (renderer.nim:159) and stored (renderer.nim:204-209: one
+// pixel, or the step x step block of a progressive pass).
+__device__ __forceinline__ void finish_item(KP p, const GroupPix& gp, F3 acc, int L) {
+  if (L == 64) {  // one pixel per wave: DPP row scans + row broadcasts, total in lane 63
+    acc = f3(wave_total(acc.x), wave_total(acc.y), wave_total(acc.z));
+  } else {
+    for (int off = 1; off < L; off <<= 1) {
+      acc.x += __shfl_xor(acc.x, off);
+      acc.y += __shfl_xor(acc.y, off);
+      acc.z += __shfl_xor(acc.z, off);
+    }
+  }
+  if (gp.valid && gp.sub == 0) {
+    if (p->aa_kind != 0) acc = f3(acc.x * p->inv_len, acc.y * p->inv_len, acc.z * p->inv_len);
+    if (p->mode == 0 && p->step > 1) {
+      const int xe = min(gp.x + p->step, p->width), ye = min(gp.y + p->step, p->height);
+      for (int yy = gp.y; yy < ye; ++yy)
+        for (int xx = gp.x; xx < xe; ++xx) {
+          float* q = p->fb + ((size_t)yy * p->width + xx) * 3;
+          q[0] = acc.x; q[1] = acc.y; q[2] = acc.z;
+        }
+    } else {
+      float* q = p->fb + ((size_t)gp.out_row * p->width + gp.x) * 3;
+      q[0] = acc.x; q[1] = acc.y; q[2] = acc.z;
+    }
   }
 }
 
@@ -1135,13 +1289,19 @@ __global__ __launch_bounds__(256) RTMI_OCC void k_render_fast(const FastParams p
   int qj = 0;
   if (__lane_id() == 0) qj = (int)atomicAdd(head, 1u);
   qj = __builtin_amdgcn_readfirstlane(qj);
-  int qj_next = 0;
+  // reservations RTMI_QUEUE_AHEAD items ahead (lane 0 holds them): the
+  // atomic's round trip overlaps that many items
+  int qj_next = 0, qj_next2 = 0;
   if (__lane_id() == 0) qj_next = (int)atomicAdd(head, 1u);
+#if RTMI_QUEUE_AHEAD >= 2
+  if (__lane_id() == 0) qj_next2 = (int)atomicAdd(head, 1u);
+#endif
   int g = qj * p->shards + shard;
+  int nflush = 0;
   while (g < p->ngroups) {
     p = params();
     const int L = p->lanes_per_px;
-    const int iters = (p->spp + L - 1) / L;
+    const int iters = p->iters;
     const int gg = p->order ? cp(p->order)[g] : g;
     const unsigned t_item = (unsigned)__builtin_amdgcn_s_memtime();
     RT_STAMP(t_it0);
@@ -1152,37 +1312,7 @@ __global__ __launch_bounds__(256) RTMI_OCC void k_render_fast(const FastParams p
     // lane per column and the y shuffle with one lane per row (each lane
     // only touches its own column / row, so the sequential reference order
     // holds per lane; rt_sampling.h draw indices)
-    LdsF* tb = nullptr;
-    if ((F & F_STOCHASTIC) && p->aa_kind >= 3) {
-      const int m = p->grid_m, spp = p->spp;
-      const uint64_t key = rng_pixel_key(p->seed, gp.x, gp.y);
-      tb = (LdsF*)sample_lds + ((size_t)(wib * (64 / L) + (lane_id_fresh() >> p->log2_lanes)) * 2 * spp);
-      volatile LdsF* t = tb;
-      for (int e = gp.sub; e < spp; e += L) {
-        double a, b;
-        canonical_entry(key, m, e, a, b);
-        t[e] = (float)a;
-        t[spp + e] = (float)b;
-      }
-      const uint64_t bx = 2 * (uint64_t)spp;
-      const uint64_t by = bx + (p->aa_kind == 3 ? (uint64_t)spp : (uint64_t)m);
-      if (gp.sub < m) {
-        const int i = gp.sub;  // column i: the x shuffle
-        for (int j = 0; j < m; ++j) {
-          const int k = rng_pick(rng_draw(key, p->aa_kind == 3 ? bx + (uint64_t)j * m + i : bx + (uint64_t)j), j, m);
-          const float a = t[j * m + i], b = t[k * m + i];
-          t[j * m + i] = b;
-          t[k * m + i] = a;
-        }
-        const int j = gp.sub;  // row j: the y shuffle
-        for (int ii = 0; ii < m; ++ii) {
-          const int k = rng_pick(rng_draw(key, p->aa_kind == 3 ? by + (uint64_t)ii * m + j : by + (uint64_t)ii), ii, m);
-          const float a = t[spp + j * m + ii], b = t[spp + j * m + k];
-          t[spp + j * m + ii] = b;
-          t[spp + j * m + k] = a;
-        }
-      }
-    }
+    LdsF* tb = sample_table<F>(p, gp, sample_lds, wib, L);
     Acc pacc;
     pacc.v = f3(0.0f, 0.0f, 0.0f);
     // the pixel's record, once per work item (a one-pixel wave: every
@@ -1230,45 +1360,83 @@ __global__ __launch_bounds__(256) RTMI_OCC void k_render_fast(const FastParams p
     }
     p = params();
     const int lane = lane_id_fresh();
-    F3 acc = pacc.v;
-    for (int off = 1; off < L; off <<= 1) {
-      acc.x += __shfl_xor(acc.x, off);
-      acc.y += __shfl_xor(acc.y, off);
-      acc.z += __shfl_xor(acc.z, off);
-    }
-    if (gp.valid && gp.sub == 0) {
-      if (p->aa_kind != 0) acc = f3(acc.x * p->inv_len, acc.y * p->inv_len, acc.z * p->inv_len);
-      if (p->mode == 0 && p->step > 1) {
-        const int xe = min(gp.x + p->step, p->width), ye = min(gp.y + p->step, p->height);
-        for (int yy = gp.y; yy < ye; ++yy)
-          for (int xx = gp.x; xx < xe; ++xx) {
-            float* q = p->fb + ((size_t)yy * p->width + xx) * 3;
-            q[0] = acc.x; q[1] = acc.y; q[2] = acc.z;
-          }
-      } else {
-        float* q = p->fb + ((size_t)gp.out_row * p->width + gp.x) * 3;
-        q[0] = acc.x; q[1] = acc.y; q[2] = acc.z;
-      }
-    }
+    finish_item(p, gp, pacc.v, L);
     if (p->cost && lane == 0) p->cost[gg] = (unsigned)__builtin_amdgcn_s_memtime() - t_item;
 #if RTMI_STAMPS == 1
     { RT_STAMP(t_it1); RT_ACC(8, t_it0, t_it1); }
 #endif
-    // 32-bit wave counters -> the wave's 64-bit LDS totals
-    if (lane < kStatSlots) {
-      unsigned int v = 0u;
-#pragma unroll
-      for (int k = 0; k < kStatSlots; ++k) v = lane == k ? ws.v[k] : v;
-      lds_tot[wib][lane] += v;
+    // 32-bit wave counters -> the wave's 64-bit LDS totals, every
+    // p->stat_flush items (before any counter can wrap) and at the end
+    if (++nflush >= p->stat_flush) {
+      flush_stats(ws, lds_tot[wib], lane);
+      nflush = 0;
     }
-#pragma unroll
-    for (int k = 0; k < kStatSlots; ++k) ws.v[k] = 0u;
     qj = __builtin_amdgcn_readfirstlane(qj_next);
+#if RTMI_QUEUE_AHEAD >= 2
+    qj_next = qj_next2;
+    if (lane == 0) qj_next2 = (int)atomicAdd(head, 1u);
+#else
     if (lane == 0) qj_next = (int)atomicAdd(head, 1u);
+#endif
     g = qj * p->shards + shard;
   }
   p = params();
   const int lane = (int)__lane_id();
+  flush_stats(ws, lds_tot[wib], lane);
+  const int wave = (int)(blockIdx.x * (blockDim.x >> 6) + threadIdx.x / 64u);
+  if (lane < kStatSlots) p->partials[(size_t)wave * kStatSlots + lane] = lds_tot[wib][lane];
+}
+
+// The lean-pixel kernel (two-class launches, rtmi.cpp split_lists): the
+// work items are the launch's lean pixel groups (p->order lists them,
+// p->ngroups counts them), every one rendered by lean_batch. The kernel
+// holds nothing but that path, so unlike k_render_fast (whose register
+// allocation is set by the mesh searches: kernel arguments re-read per use,
+// spilled SGPRs) its item loop keeps the arguments in SGPRs; per work item
+// it costs a dequeue, a list read and the pixel sum. Frames are
+// bit-identical to k_render_fast's lean path (same lean_batch, same sums).
+template <unsigned F>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k_render_lean(
+    const FastParams params_by_value) {
+  (void)params_by_value;
+  const KP p = params();
+  extern __shared__ float sample_lds[];
+  __shared__ unsigned long long lds_tot[4][kStatSlots];
+  const int wib = (int)(threadIdx.x >> 6);
+  const int lane = (int)__lane_id();
+  if (lane < kStatSlots) lds_tot[wib][lane] = 0ull;
+  Stats32 ws;
+#pragma unroll
+  for (int k = 0; k < kStatSlots; ++k) ws.v[k] = 0u;
+  const int shard = (int)(blockIdx.x % (unsigned int)p->shards);
+  unsigned int* head = p->queue + shard * kQueueStride;
+  int qj = 0;
+  if (lane == 0) qj = (int)atomicAdd(head, 1u);
+  qj = __builtin_amdgcn_readfirstlane(qj);
+  int qj_next = 0;
+  if (lane == 0) qj_next = (int)atomicAdd(head, 1u);
+  int g = qj * p->shards + shard;
+  int nflush = 0;
+  const int iters = p->iters;
+  while (g < p->ngroups) {
+    const int gg = cp(p->order)[g];
+    const GroupPix gp = group_pixel(p, gg, lane);
+    const LdsF* tb = sample_table<F>(p, gp, sample_lds, wib, 64);
+    Acc acc;
+    acc.v = f3(0.0f, 0.0f, 0.0f);
+    int it = 0;
+    for (; it + kLeanBatch <= iters; it += kLeanBatch) lean_batch<F, kLeanBatch>(p, gp, it, tb, acc, ws);
+    for (; it < iters; ++it) lean_batch<F, 1>(p, gp, it, tb, acc, ws);
+    finish_item(p, gp, acc.v, 64);
+    if (++nflush >= p->stat_flush) {
+      flush_stats(ws, lds_tot[wib], lane);
+      nflush = 0;
+    }
+    qj = __builtin_amdgcn_readfirstlane(qj_next);
+    if (lane == 0) qj_next = (int)atomicAdd(head, 1u);
+    g = qj * p->shards + shard;
+  }
+  flush_stats(ws, lds_tot[wib], lane);
   const int wave = (int)(blockIdx.x * (blockDim.x >> 6) + threadIdx.x / 64u);
   if (lane < kStatSlots) p->partials[(size_t)wave * kStatSlots + lane] = lds_tot[wib][lane];
 }

@@ -59,7 +59,9 @@ template __global__ void fast::k_render_fast<true, fast::F_ALL>(const FastParams
 // feature-subset specialisations: rt_kernels_f32_part.hip, 16 objects
 #define RTMI_PART_DECL(k)                                                                             \
   extern "C" int rtmi_launch_render_f32_part##k(unsigned, const rtmi::FastParams*, int, size_t, void*); \
-  extern "C" int rtmi_render_f32_part_blocks_per_cu##k(unsigned, size_t);
+  extern "C" int rtmi_render_f32_part_blocks_per_cu##k(unsigned, size_t);                              \
+  extern "C" int rtmi_launch_lean_f32_part##k(unsigned, const rtmi::FastParams*, int, size_t, void*);   \
+  extern "C" int rtmi_lean_f32_part_blocks_per_cu##k(unsigned, size_t);
 RTMI_PART_DECL(0) RTMI_PART_DECL(1) RTMI_PART_DECL(2) RTMI_PART_DECL(3)
 RTMI_PART_DECL(4) RTMI_PART_DECL(5) RTMI_PART_DECL(6) RTMI_PART_DECL(7)
 RTMI_PART_DECL(8) RTMI_PART_DECL(9) RTMI_PART_DECL(10) RTMI_PART_DECL(11)
@@ -74,7 +76,26 @@ int (*const kLaunch[16])(unsigned, const rtmi::FastParams*, int, size_t, void*) 
 int (*const kOccupancy[16])(unsigned, size_t) = {
     RTMI_O(0), RTMI_O(1), RTMI_O(2),  RTMI_O(3),  RTMI_O(4),  RTMI_O(5),  RTMI_O(6),  RTMI_O(7),
     RTMI_O(8), RTMI_O(9), RTMI_O(10), RTMI_O(11), RTMI_O(12), RTMI_O(13), RTMI_O(14), RTMI_O(15)};
+#define RTMI_LL(k) rtmi_launch_lean_f32_part##k
+#define RTMI_LO(k) rtmi_lean_f32_part_blocks_per_cu##k
+int (*const kLaunchLean[16])(unsigned, const rtmi::FastParams*, int, size_t, void*) = {
+    RTMI_LL(0), RTMI_LL(1), RTMI_LL(2),  RTMI_LL(3),  RTMI_LL(4),  RTMI_LL(5),  RTMI_LL(6),  RTMI_LL(7),
+    RTMI_LL(8), RTMI_LL(9), RTMI_LL(10), RTMI_LL(11), RTMI_LL(12), RTMI_LL(13), RTMI_LL(14), RTMI_LL(15)};
+int (*const kOccupancyLean[16])(unsigned, size_t) = {
+    RTMI_LO(0), RTMI_LO(1), RTMI_LO(2),  RTMI_LO(3),  RTMI_LO(4),  RTMI_LO(5),  RTMI_LO(6),  RTMI_LO(7),
+    RTMI_LO(8), RTMI_LO(9), RTMI_LO(10), RTMI_LO(11), RTMI_LO(12), RTMI_LO(13), RTMI_LO(14), RTMI_LO(15)};
 }  // namespace
+
+// The lean-pixel kernel of a feature subset (two-class launches).
+extern "C" int rtmi_launch_lean_f32(const rtmi::FastParams* p, unsigned subset, int blocks, size_t shmem,
+                                    void* stream) {
+  return kLaunchLean[(subset >> 3) & 15u](subset & 127u, p, blocks, shmem, stream);
+}
+
+// Resident blocks per CU of the lean-pixel kernel; 0: no lean kernel for the subset.
+extern "C" int rtmi_lean_f32_blocks_per_cu(unsigned subset, size_t shmem) {
+  return kOccupancyLean[(subset >> 3) & 15u](subset & 127u, shmem);
+}
 
 extern "C" int rtmi_launch_render_f32(const rtmi::FastParams* p, unsigned subset, int blocks, size_t shmem,
                                       void* stream) {

@@ -138,6 +138,11 @@ struct rt_scene {
   int num_cus = 256;
   hipStream_t stream = nullptr;
   hipEvent_t done = nullptr;
+  // two-class launches: the lean kernel runs on `aux`, forked from and
+  // joined back into the caller's stream, so its waves take the general
+  // kernel's slots as that kernel's waves drain (no tail between the two)
+  hipStream_t aux = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
   int32_t nobj = 0, nlight = 0, nmesh = 0;
   int32_t shadow_mesh = -1;  // the only mesh object, or -1 (FastParams.shadow_mesh)
   int32_t has_point_light = 0;
@@ -165,6 +170,16 @@ struct rt_scene {
     }
   };
   std::vector<std::unique_ptr<Order>> orders;  // most recently used first, at most 8
+  struct Split {                   // one launch mapping's lean / general pixel group lists
+    std::array<int64_t, 13> key;
+    DevBuf<int32_t> lean, heavy;
+    int n_lean = 0, n_heavy = 0;
+    ~Split() {
+      lean.release();
+      heavy.release();
+    }
+  };
+  std::vector<std::unique_ptr<Split>> splits;  // most recently used first, at most 8
   // bins of the float32 kernel (rt_bins.h), for the scene's only mesh object
   std::vector<BinTri> bin_tris;    // its faces (object space) + TriFast byte offsets
   double mesh_o2w[16], mesh_w2o[16];
@@ -186,6 +201,7 @@ struct rt_scene {
     bool info_ok = false;          // pixel records (FastParams.pix_info) built for info_bias
     double info_bias = 0.0;
     DevBuf<uint32_t> info;
+    std::vector<uint32_t> host_info;  // the records (two-class launches list lean pixels from them)
     ~PixelBins() {
       off.release();
       ent.release();
@@ -222,7 +238,11 @@ struct rt_scene {
     obj_grids.release();
     obj_grid_mask.release();
     pixel_bins.clear();
+    splits.clear();
     if (done) (void)hipEventDestroy(done);
+    if (fork) (void)hipEventDestroy(fork);
+    if (join) (void)hipEventDestroy(join);
+    if (aux) (void)hipStreamDestroy(aux);
     if (stream) (void)hipStreamDestroy(stream);
   }
 };
@@ -685,6 +705,9 @@ extern "C" int rt_scene_create(const rt_scene_desc* d, rt_scene** out_scene) {
   std::memcpy(s->bg, d->bg_color, sizeof s->bg);
   HIP_TRY(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
   HIP_TRY(hipEventCreateWithFlags(&s->done, hipEventDisableTiming));
+  HIP_TRY(hipStreamCreateWithFlags(&s->aux, hipStreamNonBlocking));
+  HIP_TRY(hipEventCreateWithFlags(&s->fork, hipEventDisableTiming));
+  HIP_TRY(hipEventCreateWithFlags(&s->join, hipEventDisableTiming));
   {
     std::vector<DevObject<float>> o;
     std::vector<DevLight<float>> l;
@@ -865,9 +888,10 @@ extern "C" int rt_scene_create(const rt_scene_desc* d, rt_scene** out_scene) {
     mark("object bins");
   }
   s->max_waves = s->num_cus * 8 * 4;  // 8 blocks of 4 waves per CU at most
-  if ((rc = s->partials.alloc((size_t)s->max_waves * kStatSlots))) return rc;
+  // two kernels per two-class launch: their waves' partial counters side by side
+  if ((rc = s->partials.alloc((size_t)2 * s->max_waves * kStatSlots))) return rc;
   if ((rc = s->acc.alloc(kStatSlots))) return rc;
-  if ((rc = s->queue.alloc((size_t)kQueueShards * kQueueStride))) return rc;
+  if ((rc = s->queue.alloc((size_t)2 * kQueueShards * kQueueStride))) return rc;  // general + lean kernel
   HIP_TRY(hipMemset(s->acc.p, 0, kStatSlots * sizeof(unsigned long long)));
   HIP_TRY(hipDeviceSynchronize());
   mark("nodes + buffers");
@@ -1202,6 +1226,22 @@ void fill_fast(rt_scene* s, const rt_options* o, const Mapping& mp, float* fb, F
   p.inv_band_h = mp.band_h > 0 ? (float)(1.0 / (double)mp.band_h) : 0.0f;
   p.tiles_x = pl.tiles_x;
   p.ngroups = pl.ngroups;
+  p.iters = (spp + pl.L - 1) / pl.L;
+  {  // g / tiles_x by multiply-shift: m = floor(2^(31+s) / d) + 1, s = ceil(log2 d), exact for g < 2^31
+    const uint64_t d = (uint64_t)std::max(1, pl.tiles_x);
+    int sh = 0;
+    while ((1ull << sh) < d) ++sh;
+    p.tx_shift = 31 + sh;
+    p.tx_magic = (uint32_t)((1ull << (31 + sh)) / d + 1ull);
+  }
+  {  // the 32-bit wave counters stay in registers across work items and are
+     // added to the 64-bit totals before any can wrap: per item at most
+     // 64 lanes x iters samples x levels x (1 + lights) traces x objects hits
+    const uint64_t levels = s->any_reflective ? (uint64_t)std::min(kMaxShadeLevels, std::max(1, o->max_ray_depth + 1)) : 1ull;
+    const uint64_t per_item = 64ull * (uint64_t)p.iters * levels * (1ull + (uint64_t)s->nlight) *
+                              (uint64_t)std::max(1, s->nobj);
+    p.stat_flush = (o->flags & RT_FLAG_COUNT_TRAVERSAL) ? 1 : (int32_t)std::min<uint64_t>(1u << 20, std::max<uint64_t>(1, 0xFFFFFFFFull / per_item));
+  }
   // binned searches (rt_bins.h): camera rays when a wave spans at most 4
   // pixels (>= 16 samples per pixel), shadow rays to distant lights
   if (!(o->flags & RT_FLAG_NO_BINNING)) {
@@ -1227,6 +1267,8 @@ void fill_fast(rt_scene* s, const rt_options* o, const Mapping& mp, float* fb, F
         }
         pb->info_ok = pb->info.upload(info) == RT_OK;
         pb->info_bias = o->bias;
+        pb->host_info.swap(info);
+        s->splits.clear();  // lists of the previous records
       }
       if (pb->ok && pl.L == 64 && pb->info_ok) p.pix_info = pb->info.p;
       if (pb->obj_ok) p.obj_pix = pb->omask.p;
@@ -1333,6 +1375,68 @@ void fill_params(rt_scene* s, const PrecisionData<R>& pd, const rt_options* o, c
   *blocks = (int)std::max(1LL, std::min<long long>(want, cap));
 }
 
+// Two-class launches (float32, one pixel per wave, pixel records present):
+// the launch's pixel groups split into the lean ones — no camera ray of the
+// pixel can hit the mesh and every light is a distant light whose shadow
+// rays from the pixel provably miss it (rt_bins.h pixel records), no
+// reflection — and the rest. The general kernel renders the rest from one
+// list, k_render_lean (rt_fast.h) the lean ones from the other: the lean
+// path's register allocation is then its own (C3: ~90 % of the pixels).
+// Groups outside the image / skipped by a progressive pass are in neither
+// list (they render nothing). Lists are built per launch mapping on the
+// host from the records and cached (LRU, 8). Scheduling only: the image
+// and Stats are those of the one-kernel launch.
+rt_scene::Split* split_lists(rt_scene* s, const rt_options* o, const Mapping& mp, const FastParams& p) {
+  if (o->flags & (RT_FLAG_NO_SPLIT | RT_FLAG_COUNT_TRAVERSAL)) return nullptr;
+  if (p.lanes_per_px != 64 || !p.pix_info || p.order || p.cost || s->nlight > 8) return nullptr;
+  const unsigned sub = f32_subset(s, o);
+  if (rtmi_lean_f32_blocks_per_cu(sub, f32_table_lds(o)) <= 0) return nullptr;
+  rt_scene::PixelBins* pb = s->pixel_bins.empty() ? nullptr : s->pixel_bins[0].get();
+  if (!pb || pb->w != o->width || pb->h != o->height || !pb->info_ok ||
+      pb->host_info.size() != (size_t)o->width * (size_t)o->height)
+    return nullptr;
+  int64_t bias_bits;
+  std::memcpy(&bias_bits, &o->bias, sizeof bias_bits);
+  const std::array<int64_t, 13> key = {o->width, o->height, bias_bits, mp.mode, mp.y0,   mp.nrows, mp.ncols,
+                                       mp.step,  mp.max_step, mp.band_h, mp.rank, mp.world, s->nlight};
+  size_t i = 0;
+  while (i < s->splits.size() && s->splits[i]->key != key) ++i;
+  if (i < s->splits.size()) {
+    std::rotate(s->splits.begin(), s->splits.begin() + (long)i, s->splits.begin() + (long)i + 1);
+    return s->splits[0].get();
+  }
+  const uint32_t full = (1u << s->nlight) - 1u;
+  std::vector<int32_t> lean, heavy;
+  for (int64_t g = 0; g < (int64_t)p.ngroups; ++g) {  // group_pixel (rt_fast.h) for one-pixel groups
+    const int k = (int)(g / mp.ncols), j = (int)(g % mp.ncols);
+    const int x = j * mp.step;
+    int y;
+    if (mp.mode == 0) {
+      y = mp.y0 + k * mp.step;
+    } else {
+      y = (k / mp.band_h * mp.world + mp.rank) * mp.band_h + k % mp.band_h;
+      if (y >= o->height) continue;
+    }
+    if (mp.step < mp.max_step) {
+      const int mask = mp.step * 2 - 1;
+      if ((x & mask) == 0 && (y & mask) == 0) continue;
+    }
+    const uint32_t r = pb->host_info[(size_t)y * o->width + x];
+    const bool is_lean = (r & kPixCount) == 0u && ((r >> 24) & full) == full;
+    (is_lean ? lean : heavy).push_back((int32_t)g);
+  }
+  std::unique_ptr<rt_scene::Split> e(new rt_scene::Split());
+  e->key = key;
+  e->n_lean = (int)lean.size();
+  e->n_heavy = (int)heavy.size();
+  if (lean.empty()) lean.push_back(0);  // keep both allocations non-empty
+  if (heavy.empty()) heavy.push_back(0);
+  if (e->lean.upload(lean) != RT_OK || e->heavy.upload(heavy) != RT_OK) return nullptr;
+  s->splits.insert(s->splits.begin(), std::move(e));
+  if (s->splits.size() > 8) s->splits.pop_back();
+  return s->splits[0].get();
+}
+
 int launch(rt_scene* s, const rt_options* o, const Mapping& mp, float* d_out, hipStream_t st) {
   int blocks = 1;
   if (o->precision == RT_FP64) {
@@ -1362,8 +1466,44 @@ int launch(rt_scene* s, const rt_options* o, const Mapping& mp, float* d_out, hi
     if (cost_dump && !measuring && !p.cost) {
       if (dbg_cost.alloc((size_t)p.ngroups) == RT_OK) p.cost = dbg_cost.p;
     }
-    const int e = rtmi_launch_render_f32(&p, f32_subset(s, o), blocks, f32_table_lds(o), st);
-    if (e) return fail(RT_E_DEVICE, "render kernel launch failed: %s", hipGetErrorString((hipError_t)e));
+    rt_scene::Split* sp = (cost_dump || measuring) ? nullptr : split_lists(s, o, mp, p);
+    if (sp) {  // two-class launch: the general kernel on its list, then the lean kernel on its own
+      const size_t shmem = f32_table_lds(o);
+      const unsigned sub = f32_subset(s, o);
+      FastParams ph = p, pl = p;
+      const int hb = (int)std::max(1LL, std::min<long long>(blocks, ((long long)sp->n_heavy + 3) / 4));
+      ph.order = sp->heavy.p;
+      ph.ngroups = sp->n_heavy;
+      ph.shards = std::min(kQueueShards, hb);
+      const long long lcap = (long long)rtmi_lean_f32_blocks_per_cu(sub, shmem) * s->num_cus;
+      const int lb = (int)std::max(1LL, std::min<long long>(std::min<long long>(lcap, s->max_waves / 4),
+                                                            ((long long)sp->n_lean + 3) / 4));
+      pl.order = sp->lean.p;
+      pl.ngroups = sp->n_lean;
+      pl.shards = std::min(kQueueShards, lb);
+      pl.queue = s->queue.p + (size_t)kQueueShards * kQueueStride;
+      pl.partials = s->partials.p + (size_t)hb * 4 * kStatSlots;
+      // general kernel first on the caller's stream, the lean kernel on
+      // the scene's aux stream (forked after the caller's earlier work,
+      // joined before its later work)
+      static const bool serial = std::getenv("RTMI_SPLIT_SERIAL") != nullptr;  // diagnostic: one stream
+      hipStream_t sl = serial ? st : s->aux;
+      if (!serial) {
+        HIP_TRY(hipEventRecord(s->fork, st));
+        HIP_TRY(hipStreamWaitEvent(s->aux, s->fork, 0));
+      }
+      int e = rtmi_launch_render_f32(&ph, sub, hb, shmem, st);
+      if (!e) e = rtmi_launch_lean_f32(&pl, sub, lb, shmem, sl);
+      if (e) return fail(RT_E_DEVICE, "render kernel launch failed: %s", hipGetErrorString((hipError_t)e));
+      if (!serial) {
+        HIP_TRY(hipEventRecord(s->join, s->aux));
+        HIP_TRY(hipStreamWaitEvent(st, s->join, 0));
+      }
+      blocks = hb + lb;
+    } else {
+      const int e = rtmi_launch_render_f32(&p, f32_subset(s, o), blocks, f32_table_lds(o), st);
+      if (e) return fail(RT_E_DEVICE, "render kernel launch failed: %s", hipGetErrorString((hipError_t)e));
+    }
     if (measuring) HIP_TRY(hipEventRecord(measuring->measured, st));
     if (dbg_cost.p) {
       std::vector<unsigned> c((size_t)p.ngroups);
@@ -1419,7 +1559,7 @@ int render_device(rt_scene* s, const rt_options* o, const Mapping& mp, float* d_
   HIP_TRY(hipStreamWaitEvent(st, s->done, 0));
   HIP_TRY(hipMemsetAsync(s->acc.p, 0, kStatSlots * sizeof(unsigned long long), st));
   if (o->precision == RT_FP32)
-    HIP_TRY(hipMemsetAsync(s->queue.p, 0, (size_t)kQueueShards * kQueueStride * sizeof(unsigned int), st));
+    HIP_TRY(hipMemsetAsync(s->queue.p, 0, (size_t)2 * kQueueShards * kQueueStride * sizeof(unsigned int), st));
   int rc = launch(s, o, mp, d_out, st);
   if (rc) return rc;
   HIP_TRY(hipEventRecord(s->done, st));

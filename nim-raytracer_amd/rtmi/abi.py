@@ -22,6 +22,7 @@ RT_FLAG_ANYHIT_SHADOWS = 0x1
 RT_FLAG_COUNT_TRAVERSAL = 0x2
 RT_FLAG_NO_REORDER = 0x4
 RT_FLAG_NO_BINNING = 0x8
+RT_FLAG_NO_SPLIT = 0x10
 RT_BVH_SAH = 0
 RT_OBJ_SLASH_INDICES = 0x1
 RT_BVH_PLOC = 1

@@ -11,6 +11,7 @@ sys.path.insert(0, "nim-raytracer_amd")
 import torch  # noqa: E402  (one HIP runtime for all libraries)
 
 from rtmi import abi, scenes  # noqa: E402
+from rtmi.glm import inverse, mat4, translate, vec3  # noqa: E402
 from rtmi.scene import Antialias, Options, Precision, akGrid, flatten  # noqa: E402
 
 
@@ -27,6 +28,12 @@ def variants():
     s = scenes.mesh_bunny(); s.objects = [s.objects[1]]; v["ground_only"] = (s, o)
     s = scenes.mesh_bunny(); s.objects = [s.objects[0]]; v["bunny_only"] = (s, o)
     s = scenes.mesh_bunny(); s.lights = []; v["c3_nolights"] = (s, o)
+    # every pixel lean (the bunny and its shadows off screen)
+    s = scenes.mesh_bunny(); s.objects[0].geometry.objectToWorld = translate(mat4(1.0), vec3(200.0, 0.0001, -12.0))
+    s.objects[0].geometry.worldToObject = inverse(s.objects[0].geometry.objectToWorld); v["lean_only"] = (s, o)
+    s = scenes.mesh_bunny(); s.objects[0].geometry.objectToWorld = translate(mat4(1.0), vec3(200.0, 0.0001, -12.0))
+    s.objects[0].geometry.worldToObject = inverse(s.objects[0].geometry.objectToWorld); s.lights = []
+    v["lean_nolights"] = (s, o)
     v["boxes2_c2"] = (scenes.boxes2(), Options(width=1920, height=1080, antialias=Antialias(akGrid, 8),
                                                bias=1e-4, precision=Precision.fp32))
     sel = os.environ.get("ABLATE", "")

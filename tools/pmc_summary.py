@@ -12,7 +12,11 @@ import os
 import sys
 
 
-def means(path, kernel="k_render_fast<false"):
+KERNEL = "k_render_fast<false"  # substring of the kernel names summarised
+
+
+def means(path, kernel=None):
+    kernel = kernel or KERNEL
     agg = collections.defaultdict(float)
     for r in csv.DictReader(open(path)):
         if kernel not in r["Kernel_Name"]:
