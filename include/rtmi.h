@@ -389,6 +389,11 @@ int rt_rgba_encode_device(const float *d_fb, int32_t width, int32_t height,
  * Zero unless that call set RT_FLAG_COUNT_TRAVERSAL. */
 int rt_scene_last_counters(rt_scene *scene, rt_traversal_counters *out);
 
+/* Work split of the last render call on this scene: pixel groups rendered by
+ * the lean-pixel kernel and by the general kernel (RT_FLAG_NO_SPLIT; a
+ * float64 call counts every group as general). Host-side bookkeeping, no wait. */
+int rt_scene_last_split(rt_scene *scene, int64_t *lean_groups, int64_t *general_groups);
+
 /* ---- helpers ----------------------------------------------------------- */
 
 /* glm-style inverse of a column-major 4x4 (what geom.nim's

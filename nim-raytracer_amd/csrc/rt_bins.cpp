@@ -9,6 +9,7 @@
 #include <cstdint>
 #include <cstdlib>
 #include <limits>
+#include <thread>
 
 namespace rtmi {
 
@@ -138,7 +139,7 @@ bool build_pixel_bins(const std::vector<BinTri>& tris, const double o2w[16], con
   xform_point(w2o, cw, co);  // camera origin in object space
   // |rd| of a unit world direction lies in [1/|o2w|, |w2o|]
   const double rd_max = frob3(w2o), rd_min = 1.0 / frob3(o2w);
-  const double margin = 0.05;  // pixels
+  const double margin = kPixelMargin;
   // per face: pixel rectangle (or empty) and projected vertices
   std::vector<int32_t> rect(tris.size() * 4, -1);
   std::vector<double> proj(tris.size() * 6, 0.0);
@@ -350,7 +351,7 @@ bool build_shadow_skips(const std::vector<int32_t>& pix_off, const std::vector<S
   const double f = std::tan(fov_deg * (3.14159265358979323846 / 180.0) / 2);
   const double r = (double)width / (double)height;
   const double cam_a = 2.0 * r * f / (double)width, cam_c = 2.0 * f / (double)height;
-  const double margin = 0.05;
+  const double margin = kPixelMargin;
   const double cw[3] = {c2w[12], c2w[13], c2w[14]};
   struct PlaneC {
     double oy;        // camera origin's object-space y
@@ -373,7 +374,10 @@ bool build_shadow_skips(const std::vector<int32_t>& pix_off, const std::vector<S
       return true;  // no pixel qualifies
     }
   }
-  for (int y = 0; y < height; ++y) {
+  // rows in parallel (host threads), one byte per pixel, packed below
+  std::vector<uint8_t> bytes(npx, 0);
+  auto rows = [&](int ya, int yb) {
+  for (int y = ya; y < yb; ++y) {
     for (int x = 0; x < width; ++x) {
       const size_t pix = (size_t)y * width + x;
       if (pix_off[pix + 1] != pix_off[pix]) continue;  // camera rays may hit the mesh
@@ -444,9 +448,23 @@ bool build_shadow_skips(const std::vector<int32_t>& pix_off, const std::vector<S
           if (n != 0) bits &= ~(1u << l);
         }
       }
-      (*out)[pix >> 2] |= bits << (8 * (pix & 3));
+      bytes[pix] = (uint8_t)bits;
     }
   }
+  };
+  const int nt = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  if (nt == 1 || npx < 65536) {
+    rows(0, height);
+  } else {
+    std::vector<std::thread> th;
+    const int chunk = (height + nt - 1) / nt;
+    for (int t = 0; t < nt; ++t) {
+      const int ya = t * chunk, yb = std::min(height, ya + chunk);
+      if (ya < yb) th.emplace_back(rows, ya, yb);
+    }
+    for (auto& t : th) t.join();
+  }
+  for (size_t pix = 0; pix < npx; ++pix) (*out)[pix >> 2] |= (uint32_t)bytes[pix] << (8 * (pix & 3));
   return true;
 }
 
@@ -469,7 +487,7 @@ bool build_object_pixel_masks(const std::vector<ObjBox>& objs, const double c2w[
   const double f = std::tan(fov_deg * (3.14159265358979323846 / 180.0) / 2);
   const double r = (double)width / (double)height;
   const double cam_a = 2.0 * r * f / (double)width, cam_c = 2.0 * f / (double)height;
-  const double margin = 0.05;  // pixels
+  const double margin = kPixelMargin;
   unsigned long long always = 0;
   std::vector<std::array<int, 4>> rect(objs.size(), std::array<int, 4>{-1, -1, -1, -1});
   for (size_t i = 0; i < objs.size(); ++i) {

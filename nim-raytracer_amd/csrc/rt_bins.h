@@ -25,6 +25,16 @@
 
 namespace rtmi {
 
+// Growth of a pixel's square (in pixels) in every camera-ray bin: a pixel's
+// bins (face lists, object masks, shadow skips) cover every ray through
+// [x - kPixelMargin, x + 1 + kPixelMargin] x [y - ..., y + 1 + ...]. That
+// holds for the kernels' camera rays as long as every sample offset lies in
+// [0, 1) — true for all of sampling.nim's samplers (akNone: 0, grid:
+// (i + 1/2)/m, jittered / multi-jittered / correlated: [0, 1)), checked on
+// the host (rtmi.cpp sampler_in_pixel) before any bin is handed to a kernel —
+// and the margin is far above the float32 error of the ray set-up.
+constexpr double kPixelMargin = 0.05;
+
 // One face of the binned mesh: object-space vertices (float64, as given) and
 // the byte offset of its TriFast record in FastData.tree.
 struct BinTri {

@@ -365,6 +365,9 @@ __device__ __forceinline__ void list_search(KP p, const int32_t* ent, int b, int
     ws.v[STAT_TRI_FETCH] += (unsigned int)(e - b);
     ws.v[STAT_LANE_TRIS] += pc(bal(tc >= 0.0f)) * (unsigned int)(e - b);
   }
+#ifdef RTMI_DIAG_NOLIST
+  return;  // diagnostic build only: the binned searches' share of the frame
+#endif
   for (int k = b; k < e; k += 4) {
     const RT_CONST int32_t* q = cp(ent) + k;
     const int r0 = q[0], r1 = q[1], r2 = q[2], r3 = q[3];
@@ -1316,7 +1319,11 @@ __global__ __launch_bounds__(256) RTMI_OCC void k_render_fast(const FastParams p
     Acc pacc;
     pacc.v = f3(0.0f, 0.0f, 0.0f);
     // the pixel's record, once per work item (a one-pixel wave: every
-    // iteration shades the same pixel): list length + shadow skip bits
+    // iteration shades the same pixel): list length + shadow skip bits. The
+    // record speaks for every ray through the pixel's square grown by
+    // rt_bins.h kPixelMargin, i.e. for sample offsets in [0, 1): the host
+    // hands records (and pixel lists) only to samplers with that property
+    // (rtmi.cpp sampler_in_pixel)
     unsigned pinfo = kPixCount;
     if ((F & F_MESH) && p->pix_info) {
       const unsigned long long vm = bal(gp.valid);

@@ -143,6 +143,7 @@ struct rt_scene {
   // kernel's slots as that kernel's waves drain (no tail between the two)
   hipStream_t aux = nullptr;
   hipEvent_t fork = nullptr, join = nullptr;
+  int64_t last_lean = 0, last_general = 0;  // rt_scene_last_split
   int32_t nobj = 0, nlight = 0, nmesh = 0;
   int32_t shadow_mesh = -1;  // the only mesh object, or -1 (FastParams.shadow_mesh)
   int32_t has_point_light = 0;
@@ -198,15 +199,21 @@ struct rt_scene {
     DevBuf<int32_t> off, ent;
     DevBuf<unsigned long long> omask;
     std::vector<int32_t> host_off; // the lists' offsets (the pixel records are built from them)
-    bool info_ok = false;          // pixel records (FastParams.pix_info) built for info_bias
-    double info_bias = 0.0;
-    DevBuf<uint32_t> info;
-    std::vector<uint32_t> host_info;  // the records (two-class launches list lean pixels from them)
+    // pixel records (FastParams.pix_info) per shadow bias, most recently
+    // used first (at most 4): callers alternating biases switch buffers
+    // instead of rebuilding and reallocating
+    struct Records {
+      double bias = 0.0;
+      DevBuf<uint32_t> info;
+      std::vector<uint32_t> host;  // the records (two-class launches list lean pixels from them)
+      ~Records() { info.release(); }
+    };
+    std::vector<std::unique_ptr<Records>> records;
     ~PixelBins() {
       off.release();
       ent.release();
       omask.release();
-      info.release();
+      records.clear();
     }
   };
   // object bins (rt_bins.h ObjBox), scenes of 4..64 objects
@@ -1160,6 +1167,51 @@ rt_scene::PixelBins* pixel_bins(rt_scene* s, int w, int h) {
   return s->pixel_bins[0].get();
 }
 
+// The pixel records of one image size for o->bias (built on first use,
+// cached per bias, LRU of 4); nullptr if they cannot be built.
+const rt_scene::PixelBins::Records* pixel_records(rt_scene* s, rt_scene::PixelBins* pb, const rt_options* o) {
+  auto& rs = pb->records;
+  size_t i = 0;
+  while (i < rs.size() && rs[i]->bias != o->bias) ++i;
+  if (i < rs.size()) {
+    std::rotate(rs.begin(), rs.begin() + (long)i, rs.begin() + (long)i + 1);
+    return rs[0].get();
+  }
+  const size_t npx = (size_t)o->width * (size_t)o->height;
+  std::vector<uint32_t> sk;
+  const char* why = "";
+  if (!(s->skippable && build_shadow_skips(pb->host_off, s->skip_planes, s->mesh_w2o, s->grid_occ, s->c2w, s->fov,
+                                           o->width, o->height, o->bias, &sk, &why)))
+    sk.assign((npx + 3) / 4, 0u);
+  std::unique_ptr<rt_scene::PixelBins::Records> r(new rt_scene::PixelBins::Records());
+  r->bias = o->bias;
+  r->host.resize(npx);
+  for (size_t k = 0; k < npx; ++k) {
+    const uint32_t n = (uint32_t)(pb->host_off[k + 1] - pb->host_off[k]);
+    r->host[k] = std::min<uint32_t>(n, kPixCount) | (sk[k >> 2] >> (8 * (k & 3)) & 0xffu) << 24;
+  }
+  if (r->info.upload(r->host) != RT_OK) return nullptr;
+  rs.insert(rs.begin(), std::move(r));
+  if (rs.size() > 4) rs.pop_back();
+  return rs[0].get();
+}
+
+// Every sample offset of the sampler lies in [0, 1) x [0, 1) of its pixel
+// (sampling.nim:5-113, renderer.nim:135), the premise of the camera-ray bins
+// (rt_bins.h kPixelMargin). A sampler outside this list gets no bins.
+bool sampler_in_pixel(int32_t aa_kind) {
+  switch (aa_kind) {
+    case RT_AA_NONE:                    // the pixel corner: offset 0
+    case RT_AA_GRID:                    // (i + 1/2) / m
+    case RT_AA_JITTERED:                // (i + u) / m, u in [0, 1)
+    case RT_AA_MULTI_JITTERED:          // (i + (j + u) / n) / m
+    case RT_AA_CORRELATED_MULTI_JITTERED:
+      return true;
+    default:
+      return false;
+  }
+}
+
 void fill_fast(rt_scene* s, const rt_options* o, const Mapping& mp, float* fb, FastParams& p, int* blocks,
                rt_scene::Order** measuring) {
   std::memset(&p, 0, sizeof p);
@@ -1245,32 +1297,16 @@ void fill_fast(rt_scene* s, const rt_options* o, const Mapping& mp, float* fb, F
   // binned searches (rt_bins.h): camera rays when a wave spans at most 4
   // pixels (>= 16 samples per pixel), shadow rays to distant lights
   if (!(o->flags & RT_FLAG_NO_BINNING)) {
-    if ((s->binnable || s->objbins) && pl.L >= 16) {
+    if ((s->binnable || s->objbins) && pl.L >= 16 && sampler_in_pixel(o->aa_kind)) {
       rt_scene::PixelBins* pb = pixel_bins(s, o->width, o->height);
       if (pb->ok) {
         p.pix_off = pb->off.p;
         p.pix_ent = pb->ent.p;
       }
       // one-pixel waves: the pixel records (list length + shadow skips for
-      // this bias, rt_bins.h), rebuilt when the bias changes
-      if (pb->ok && pl.L == 64 && !(pb->info_ok && pb->info_bias == o->bias)) {
-        const size_t npx = (size_t)o->width * (size_t)o->height;
-        std::vector<uint32_t> sk;
-        const char* why = "";
-        if (!(s->skippable && build_shadow_skips(pb->host_off, s->skip_planes, s->mesh_w2o, s->grid_occ, s->c2w,
-                                                 s->fov, o->width, o->height, o->bias, &sk, &why)))
-          sk.assign((npx + 3) / 4, 0u);
-        std::vector<uint32_t> info(npx);
-        for (size_t i = 0; i < npx; ++i) {
-          const uint32_t n = (uint32_t)(pb->host_off[i + 1] - pb->host_off[i]);
-          info[i] = std::min<uint32_t>(n, kPixCount) | (sk[i >> 2] >> (8 * (i & 3)) & 0xffu) << 24;
-        }
-        pb->info_ok = pb->info.upload(info) == RT_OK;
-        pb->info_bias = o->bias;
-        pb->host_info.swap(info);
-        s->splits.clear();  // lists of the previous records
-      }
-      if (pb->ok && pl.L == 64 && pb->info_ok) p.pix_info = pb->info.p;
+      // this bias, rt_bins.h), one set per bias (cached)
+      const rt_scene::PixelBins::Records* rec = (pb->ok && pl.L == 64) ? pixel_records(s, pb, o) : nullptr;
+      if (rec) p.pix_info = rec->info.p;
       if (pb->obj_ok) p.obj_pix = pb->omask.p;
     }
     if (s->has_grids) {
@@ -1392,9 +1428,10 @@ rt_scene::Split* split_lists(rt_scene* s, const rt_options* o, const Mapping& mp
   const unsigned sub = f32_subset(s, o);
   if (rtmi_lean_f32_blocks_per_cu(sub, f32_table_lds(o)) <= 0) return nullptr;
   rt_scene::PixelBins* pb = s->pixel_bins.empty() ? nullptr : s->pixel_bins[0].get();
-  if (!pb || pb->w != o->width || pb->h != o->height || !pb->info_ok ||
-      pb->host_info.size() != (size_t)o->width * (size_t)o->height)
+  if (!pb || pb->w != o->width || pb->h != o->height || pb->records.empty() || pb->records[0]->bias != o->bias ||
+      pb->records[0]->info.p != p.pix_info)
     return nullptr;
+  const std::vector<uint32_t>& host_info = pb->records[0]->host;
   int64_t bias_bits;
   std::memcpy(&bias_bits, &o->bias, sizeof bias_bits);
   const std::array<int64_t, 13> key = {o->width, o->height, bias_bits, mp.mode, mp.y0,   mp.nrows, mp.ncols,
@@ -1421,7 +1458,7 @@ rt_scene::Split* split_lists(rt_scene* s, const rt_options* o, const Mapping& mp
       const int mask = mp.step * 2 - 1;
       if ((x & mask) == 0 && (y & mask) == 0) continue;
     }
-    const uint32_t r = pb->host_info[(size_t)y * o->width + x];
+    const uint32_t r = host_info[(size_t)y * o->width + x];
     const bool is_lean = (r & kPixCount) == 0u && ((r >> 24) & full) == full;
     (is_lean ? lean : heavy).push_back((int32_t)g);
   }
@@ -1452,6 +1489,8 @@ int launch(rt_scene* s, const rt_options* o, const Mapping& mp, float* d_out, hi
       }
       p.sample_scratch = s->f64_tables.p;
     }
+    s->last_lean = 0;
+    s->last_general = p.ngroups;
     const int e = rtmi_launch_render_f64(&p, blocks, st);
     if (e) return fail(RT_E_DEVICE, "render kernel launch failed: %s", hipGetErrorString((hipError_t)e));
   } else {
@@ -1500,7 +1539,11 @@ int launch(rt_scene* s, const rt_options* o, const Mapping& mp, float* d_out, hi
         HIP_TRY(hipStreamWaitEvent(st, s->join, 0));
       }
       blocks = hb + lb;
+      s->last_lean = sp->n_lean;
+      s->last_general = sp->n_heavy;
     } else {
+      s->last_lean = 0;
+      s->last_general = p.ngroups;
       const int e = rtmi_launch_render_f32(&p, f32_subset(s, o), blocks, f32_table_lds(o), st);
       if (e) return fail(RT_E_DEVICE, "render kernel launch failed: %s", hipGetErrorString((hipError_t)e));
     }
@@ -1699,6 +1742,14 @@ extern "C" int rt_rgba_encode_device(const float* d_fb, int32_t width, int32_t h
   if (((uintptr_t)d_fb & 3) || ((uintptr_t)d_out & 3)) return fail(RT_E_INVALID, "buffers must be 4-B aligned");
   const int e = rtmi_launch_rgba_encode(d_fb, (long long)width * height, alpha, d_out, stream);
   if (e) return fail(RT_E_DEVICE, "rgba encode launch failed: %s", hipGetErrorString((hipError_t)e));
+  return RT_OK;
+}
+
+extern "C" int rt_scene_last_split(rt_scene* s, int64_t* lean_groups, int64_t* general_groups) {
+  if (!s || !lean_groups || !general_groups) return fail(RT_E_INVALID, "null argument");
+  std::lock_guard<std::mutex> lk(s->mu);
+  *lean_groups = s->last_lean;
+  *general_groups = s->last_general;
   return RT_OK;
 }
 

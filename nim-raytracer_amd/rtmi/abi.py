@@ -170,6 +170,7 @@ SIGNATURES = {
     "rt_unshard_bands_device": (C.c_int, [_P, _P, C.c_int32, C.c_int32, C.c_int32, C.c_int32, _P]),
     "rt_band_rows": (C.c_int, [C.c_int32, C.c_int32, C.c_int32, C.POINTER(C.c_int32)]),
     "rt_scene_last_counters": (C.c_int, [_P, C.POINTER(rt_traversal_counters)]),
+    "rt_scene_last_split": (C.c_int, [_P, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
     "rt_mat4_inverse": (C.c_int, [C.POINTER(C.c_double), C.POINTER(C.c_double)]),
     "rt_load_geom": (C.c_int, [C.c_char_p, C.POINTER(C.c_int64), C.POINTER(C.c_double)]),
     "rt_ppm_encode_device": (C.c_int, [_P, C.c_int32, C.c_int32, C.c_int32, C.c_int32, _P, _P]),

@@ -95,6 +95,12 @@ class DeviceScene:
                                            int(world), _stream(stream), C.byref(st) if stats else None))
         return Stats.from_c(st) if stats else None
 
+    def last_split(self):
+        """(lean, general) pixel groups of the last render call (two-class launches)."""
+        a, b = C.c_int64(), C.c_int64()
+        check(lib().rt_scene_last_split(self.h, C.byref(a), C.byref(b)))
+        return int(a.value), int(b.value)
+
     def last_counters(self):
         c = abi.rt_traversal_counters()
         check(lib().rt_scene_last_counters(self.h, C.byref(c)))

@@ -1,0 +1,152 @@
+"""Two-class launches of the float32 kernel (rtmi.cpp split_lists): lean
+pixels — no camera ray can hit the mesh, every light is a distant light whose
+shadow rays provably miss it — render in k_render_lean from a per-launch
+list, the rest in k_render_fast. Scheduling only: frames and Stats must be
+bit-identical to the one-kernel launch (RT_FLAG_NO_SPLIT) and to the
+BVH-only kernel (RT_FLAG_NO_BINNING: no pixel records, no lean path at all),
+whose parity with the oracle test_gpu_parity.py pins.
+
+Also the cases the round-1 review found uncovered: shadow skip bits in a
+kernel compiled with reflection (they may apply at the camera level only),
+stochastic samplers and progressive passes (step > 1) against the records."""
+import pytest
+
+from rtmi import Antialias, Options, Precision, akGrid, scenes
+from rtmi.abi import RT_FLAG_NO_BINNING, RT_FLAG_NO_SPLIT
+from rtmi.dist import band_rows
+from rtmi.glm import X_AXIS, degToRad, inverse, mat4, rotate, translate, vec3
+from rtmi.renderer import DeviceScene
+from rtmi.scene import akCorrelatedMultiJittered, akJittered, akMultiJittered
+
+pytestmark = pytest.mark.gpu
+
+FLAG_SETS = (0, RT_FLAG_NO_SPLIT, RT_FLAG_NO_BINNING)
+
+
+def _opts(w, h, m, flags=0, aa=akGrid, bias=1e-4, seed=0):
+    return Options(width=w, height=h, antialias=Antialias(aa, m), bias=bias, precision=Precision.fp32,
+                   flags=flags, seed=seed)
+
+
+def _frames(ds, make_opts, y0=0, y1=None, step=1, max_step=1):
+    import torch
+    out = []
+    for flags in FLAG_SETS:
+        o = make_opts(flags)
+        fb = torch.full((o.height * o.width * 3,), -7.0, dtype=torch.float32, device="cuda")
+        st = ds.render_device(o, fb, y0=y0, y1=o.height if y1 is None else y1, step=step, maxStep=max_step)
+        out.append((fb, st))
+    return out
+
+
+def _assert_same(frames, what):
+    import torch
+    (fa, sa) = frames[0]
+    for (fb, sb), flags in zip(frames[1:], FLAG_SETS[1:]):
+        assert sa == sb, (what, flags, sa, sb)
+        assert torch.equal(fa, fb), (what, flags, float((fa - fb).abs().max()))
+
+
+def _reflective_ground(wall):
+    """The bunny over a reflective ground plane (and optionally a reflective
+    back wall): pixel records exist (one mesh + planes), the kernel is
+    compiled with reflection, so skip bits must only drop the mesh from the
+    camera level's shadow rays, never from a reflected ray's."""
+    from rtmi.scene import Material, Object, Scene, initPlane
+    mesh = scenes.baked_bunny()
+    mesh.objectToWorld = translate(mat4(1.0), vec3(0.0, 0.0001, -12.0))
+    mesh.worldToObject = inverse(mesh.objectToWorld)
+    objects = [Object("bunny", mesh, Material(albedo=vec3(0.6, 0.9, 0.2))),
+               Object("ground", initPlane(objectToWorld=mat4(1.0)), Material(albedo=vec3(0.4), reflection=0.5))]
+    if wall:
+        w = rotate(translate(mat4(1.0), vec3(0.0, 0.0, -20.0)), X_AXIS, degToRad(90.0))
+        objects.append(Object("wall", initPlane(objectToWorld=w),
+                              Material(albedo=vec3(0.3, 0.3, 0.5), reflection=0.7)))
+    return Scene(objects=objects, lights=scenes._warm_lights(), fov=50.0,
+                 cameraToWorld=scenes._std_camera(0.0, 5.5, 1.5), bgColor=vec3(0.01, 0.03, 0.05))
+
+
+SCENES = {
+    "bunny": scenes.mesh_bunny,
+    "torus": lambda: scenes._mesh_scene(scenes.torus_mesh(96, 48), "t", (0.9, 0.5, 0.2)),
+    "mesh_mix": scenes.mesh_mix,         # point light: no lean pixels
+    "two_meshes": scenes.two_meshes,     # no pixel records
+}
+
+
+@pytest.mark.parametrize("name", list(SCENES))
+@pytest.mark.parametrize("m", [8, 10, 12, 16, 32])
+def test_split_matches_one_kernel(gpu, name, m):
+    """spp 64 .. 1024 incl. iteration counts that are not a multiple of the
+    lean batch (m = 10: 2 iterations, m = 12: 3)."""
+    ds = DeviceScene(SCENES[name]())
+    _assert_same(_frames(ds, lambda f: _opts(200, 120, m, f)), (name, m))
+
+
+@pytest.mark.parametrize("aa", [akJittered, akMultiJittered, akCorrelatedMultiJittered])
+@pytest.mark.parametrize("m", [8, 16])
+def test_split_stochastic_samplers(gpu, aa, m):
+    """Jittered / (correlated) multi-jittered samples stay inside their pixel
+    square, so the pixel records hold for them: same frames with and
+    without records and lean kernel."""
+    ds = DeviceScene(scenes.mesh_bunny())
+    _assert_same(_frames(ds, lambda f: _opts(160, 96, m, f, aa=aa, seed=0x5EED)), (aa, m))
+
+
+def test_split_progressive_and_row_ranges(gpu):
+    """renderLine's progressive passes (step > 1: skipped pixels, block
+    fills) and partial row ranges use their own per-launch lists."""
+    ds = DeviceScene(scenes.mesh_bunny())
+    for step, mx in ((4, 4), (2, 4), (1, 2)):
+        _assert_same(_frames(ds, lambda f: _opts(192, 108, 16, f), step=step, max_step=mx), (step, mx))
+    _assert_same(_frames(ds, lambda f: _opts(192, 108, 16, f), y0=37, y1=90), "rows 37..90")
+
+
+def test_split_bands(gpu):
+    """Multi-GPU band launches: each rank's list covers exactly its bands."""
+    import torch
+    ds = DeviceScene(scenes.mesh_bunny())
+    w, h, world = 256, 144, 3
+    rows = band_rows(h, 4, world)
+    for r in range(world):
+        res = []
+        for flags in FLAG_SETS:
+            b = torch.full((rows * w * 3,), -7.0, dtype=torch.float32, device="cuda")
+            st = ds.render_bands_device(_opts(w, h, 16, flags), b, 4, r, world)
+            res.append((b, st))
+        _assert_same(res, ("rank", r))
+
+
+@pytest.mark.parametrize("wall", [False, True])
+def test_skip_bits_with_reflection(gpu, wall):
+    """Reflective ground (and wall) under the bunny: the skip bits of the
+    camera level must not leak into reflected rays' shadow traces."""
+    ds = DeviceScene(_reflective_ground(wall))
+    for m in (8, 16):
+        _assert_same(_frames(ds, lambda f: _opts(240, 135, m, f)), (wall, m))
+
+
+def test_split_full_c3(gpu):
+    """BASELINE config C3 at full size: the two-class launch equals the
+    one-kernel launch, and both equal the BVH-only kernel; most pixels are
+    lean and really go to the lean kernel."""
+    import torch
+    ds = DeviceScene(scenes.mesh_bunny())
+    _assert_same(_frames(ds, lambda f: _opts(1920, 1080, 16, f)), "C3")
+    fb = torch.zeros(1920 * 1080 * 3, dtype=torch.float32, device="cuda")
+    ds.render_device(_opts(1920, 1080, 16), fb)
+    lean, general = ds.last_split()
+    assert lean + general == 1920 * 1080 and lean > 0.8 * 1920 * 1080, (lean, general)
+    ds.render_device(_opts(1920, 1080, 16, RT_FLAG_NO_SPLIT), fb)
+    assert ds.last_split() == (0, 1920 * 1080)
+
+
+def test_no_split_without_records(gpu):
+    """No lean kernel where no pixel can be lean: a point light (no skip
+    bit), two meshes (no pixel records), fewer than 64 samples per pixel."""
+    import torch
+    for name, m in (("mesh_mix", 16), ("two_meshes", 16), ("bunny", 4)):
+        ds = DeviceScene(SCENES[name]())
+        fb = torch.zeros(200 * 120 * 3, dtype=torch.float32, device="cuda")
+        ds.render_device(_opts(200, 120, m), fb)
+        assert ds.last_split()[0] == 0, name
