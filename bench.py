@@ -15,15 +15,22 @@ overlapping frame k+1's render from a second band buffer).
 
 Printed (rank 0, one JSON line): value = (primary + shadow rays of all ranks)
 x K / max-over-ranks wall time, plus
-  roofline     — the dominant kernel (k_render_fast<false>): SURVEY 8(d)'s
-                 algorithmic bytes (per ray 32 B per BVH box tested + 36 B per
-                 triangle tested + 12 B per pixel, counts from one instrumented
-                 launch) / its average duration, timed live with HIP events on
-                 the stream it runs on, vs the 8 TB/s HBM peak; also the bytes
-                 the wave-coherent kernel actually requests (one record fetch
-                 serves 64 lanes); `traffic` is the PMC-measured HBM bytes per
-                 launch from the committed rocprofv3 summary (profiles/), or
-                 null;
+  roofline     — the render call (the general kernel k_render_fast and, on
+                 two-class launches, the lean-pixel kernel k_render_lean), HIP
+                 events on the stream it runs on, against the 8 TB/s HBM peak.
+                 `achieved` = SURVEY 8(d)'s algorithmic bytes per ray — 32 B
+                 per BVH box and 36 B per triangle the ray is tested against,
+                 + 12 B per pixel — summed over the rays with the per-lane
+                 counts of the algorithm the kernels execute (binned face
+                 lists, pixel records, BVH only for left-over lanes; from one
+                 instrumented launch), / the call's duration. `traffic` = the
+                 PMC-measured HBM bytes per launch (profiles/, or null); the
+                 kernels are not HBM-bound (one scalar record fetch serves 64
+                 lanes, the working set lives in the caches): `issue` holds
+                 the VALU / SALU issue utilisation from the committed PMC
+                 instruction counts, the actual limiter. The per-ray BVH model
+                 of round 1 (every ray traverses the scene BVH) is kept as
+                 `survey_bvh_model_gbs` for comparison only;
   cpu_baseline — the fp64 oracle (the reference algorithm: linear objects,
                  brute-force mesh, scanline thread pool) on this host, 1 spp on
                  a bounded row subsample of the same frame (rank 0, N = 1 only).
@@ -132,15 +139,19 @@ def cpu_baseline(scene, width, height, target_s, bvh=False):
     }
 
 
-def load_traffic(workload_key):
-    """HBM bytes per k_render launch from the committed PMC summary, if any."""
+SIMDS = 1024           # MI355X: 256 CUs x 4 SIMDs (MI355X_MICROARCH.md)
+CLOCK_GHZ = 2.4        # peak engine clock
+VALU_CYCLES = 2        # a wave64 fp32 VALU instruction per SIMD (tools/micro/issue_rate.hip)
+
+
+def load_pmc(workload_key):
+    """Per-launch PMC figures of the render call from the committed summary
+    (profiles/pmc_summary.json, tools/pmc_summary.py), or None."""
     p = os.path.join(REPO, "profiles", "pmc_summary.json")
     try:
         with open(p) as f:
-            d = json.load(f)
-        e = d.get(workload_key)
-        return None if e is None else float(e["hbm_bytes_per_launch"])
-    except (OSError, ValueError, KeyError):
+            return json.load(f).get(workload_key)
+    except (OSError, ValueError):
         return None
 
 
@@ -184,6 +195,19 @@ def main():
     opts = Options(width=W, height=H, antialias=Antialias(akGrid, m), bias=1e-4,
                    precision=Precision.fp32, flags=args.flags)
     stream = torch.cuda.current_stream()
+    # the first frame of this camera and image size also builds its
+    # camera-dependent bins (pixel face lists, pixel records, lean/general
+    # lists): timed on its own, reported beside the steady-state frame
+    if not distributed:
+        fb0 = torch.zeros(H * W * 3, dtype=torch.float32, device="cuda")
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        ds.render_device(opts, fb0, stream=stream, stats=False)
+        torch.cuda.synchronize()
+        first_frame_ms = (time.perf_counter() - t0) * 1e3
+        del fb0
+    else:
+        first_frame_ms = None
     rows = band_rows(H, BAND_H, world)
     fb = torch.zeros(H * W * 3, dtype=torch.float32, device="cuda")
     # two band buffers: frame k's gather (RCCL, its own stream) overlaps frame
@@ -266,6 +290,7 @@ def main():
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
     kern_ms = sum(a.elapsed_time(b) for a, b in evs) / max(1, args.steps)
+    lean_groups, general_groups = ds.last_split()
     # outside the timed region: the gathered frame must equal one GPU's
     # single-call frame bit for bit (same samples, same arithmetic per pixel)
     frame_check = None
@@ -278,16 +303,31 @@ def main():
     value = rays_frame * args.steps / elapsed / 1e6
     # algorithmic bytes of one launch on this rank, SURVEY.md 8(d): per ray
     # 32 B x boxes tested + 36 B x triangles tested + 12/spp B, summed over
-    # the launch's rays (per-ray visit counts from the instrumented launch)
-    bytes_launch = (counters["lane_node_visits"] * 2 * SURVEY_BOX_BYTES
-                    + counters["lane_tri_tests"] * SURVEY_TRI_BYTES + rows * W * PIXEL_BYTES)
+    # the launch's rays with the per-lane counts of the executed algorithm
+    # (binned lists, pixel records, BVH for left-over lanes only)
+    bytes_launch = (kcounters["lane_node_visits"] * 2 * SURVEY_BOX_BYTES
+                    + kcounters["lane_tri_tests"] * SURVEY_TRI_BYTES + rows * W * PIXEL_BYTES)
     achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
-    # what the wave-coherent kernel actually requests: one record fetch serves
-    # all 64 lanes of a wave (binned searches: + a 4-B list entry per face)
+    # round 1's model: every ray traverses the scene BVH (what a per-ray
+    # BVH tracer would need; the kernels skip most of it)
+    bvh_model_bytes = (counters["lane_node_visits"] * 2 * SURVEY_BOX_BYTES
+                       + counters["lane_tri_tests"] * SURVEY_TRI_BYTES + rows * W * PIXEL_BYTES)
+    # what the wave-coherent kernels request: one record fetch serves all 64
+    # lanes of a wave (binned searches: + a 4-B list entry per face)
     fetch_bytes = (kcounters["wave_node_fetches"] * NODE_BYTES + kcounters["wave_tri_fetches"] * (TRI_BYTES + 4)
                    + rows * W * PIXEL_BYTES)
     workload_key = f"{args.config.lower()}_{W}x{H}_m{m}_world{world}"
-    traffic = load_traffic(workload_key)
+    pmc = load_pmc(workload_key)
+    traffic = None if pmc is None or "hbm_bytes_per_launch" not in pmc else float(pmc["hbm_bytes_per_launch"])
+    issue = None
+    if pmc is not None and "SQ_INSTS_VALU" in pmc.get("counters_mean_per_dispatch", {}):
+        c = pmc["counters_mean_per_dispatch"]
+        cyc = kern_ms * 1e-3 * CLOCK_GHZ * 1e9
+        issue = {"valu_busy": round(c["SQ_INSTS_VALU"] * VALU_CYCLES / SIMDS / cyc, 3),
+                 "salu_busy": round(c["SQ_INSTS_SALU"] / (SIMDS // 4) / cyc, 3),
+                 "note": ("PMC instruction counts per call (committed summary) over this run's call time at "
+                          f"{CLOCK_GHZ} GHz: VALU {VALU_CYCLES} cycles per wave64 instruction per SIMD, SALU one "
+                          "instruction per cycle per CU (shared by its 4 SIMDs)")}
 
     if rank == 0:
         out = {
@@ -313,6 +353,8 @@ def main():
                 "bvh_nodes": info["num_bvh_nodes"], "primary_rays_per_frame": prim_frame,
                 "shadow_rays_per_frame": shadow_frame, "parallelism": f"bands{world}",
                 "scene_setup_s": round(setup_s, 3), "scene_setup_ms_lib": round(info["build_ms"], 1),
+                "first_frame_ms": None if first_frame_ms is None else round(first_frame_ms, 1),
+                "lean_pixel_groups": lean_groups, "general_pixel_groups": general_groups,
                 "bvh_builder": {"sah": "host binned SAH", "ploc": "device PLOC"}[args.bvh],
             },
             "roofline": {
@@ -322,18 +364,24 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
-                "kernel": "k_render_fast<false>",
+                "kernel": "render call: k_render_fast<false> + k_render_lean (two-class launch)",
                 "kernel_ms": round(kern_ms, 4),
                 "bytes_per_launch": int(bytes_launch),
-                "definition": ("SURVEY 8(d): 32 B/box + 36 B/triangle tested per ray by a per-ray traversal of "
-                               "the scene BVH + 12 B/pixel"),
+                "definition": ("SURVEY 8(d) per-ray bytes (32 B/BVH box + 36 B/triangle tested, 12 B/pixel) over "
+                               "the per-lane tests the kernels execute (binned face lists, pixel records, BVH for "
+                               "left-over lanes)"),
+                "limiter": ("instruction issue (SALU + VALU), not HBM: one scalar record fetch serves 64 lanes and "
+                            "the records live in the caches (traffic << achieved)"),
+                "issue": issue,
                 "record_fetch_bytes_per_launch": int(fetch_bytes),
                 "record_fetch_gbs": round(fetch_bytes / (kern_ms * 1e-3) / 1e9, 1),
-                "lane_node_visits": counters["lane_node_visits"],
-                "lane_tri_tests": counters["lane_tri_tests"],
+                "survey_bvh_model_gbs": round(bvh_model_bytes / (kern_ms * 1e-3) / 1e9, 1),
+                "kernel_lane_node_visits": kcounters["lane_node_visits"],
+                "kernel_lane_tri_tests": kcounters["lane_tri_tests"],
                 "kernel_wave_node_fetches": kcounters["wave_node_fetches"],
                 "kernel_wave_tri_fetches": kcounters["wave_tri_fetches"],
-                "kernel_lane_tri_tests": kcounters["lane_tri_tests"],
+                "bvh_model_lane_node_visits": counters["lane_node_visits"],
+                "bvh_model_lane_tri_tests": counters["lane_tri_tests"],
             },
             "cpu_baseline": None,
         }

@@ -1,43 +1,55 @@
 """Summarise rocprofv3 --pmc CSVs (one counter set per pass) into
-profiles/pmc_summary.json, per-dispatch means for the render kernel.
+profiles/pmc_summary.json: per render call, the per-dispatch means of every
+render kernel (the general k_render_fast and, on two-class launches, the
+lean-pixel k_render_lean — one dispatch each per call) summed over the
+kernels, plus the per-kernel means.
 
 HBM bytes per launch = (2 * FETCH_SIZE + WRITE_SIZE) * 1024: FETCH_SIZE and
 WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE under-reports wide reads by 2x
 (MI355X_MICROARCH.md "HBM"), so it is doubled as that guide prescribes.
+
+    python tools/pmc_summary.py <pmc_dir> <workload_key> [note]
 """
 import collections
 import csv
 import json
 import os
+import re
 import sys
 
-
-KERNEL = "k_render_fast<false"  # substring of the kernel names summarised
+# the render call's kernels (a regex on the kernel name)
+KERNEL = r"k_render_fast<false|k_render_lean<"
 
 
 def means(path, kernel=None):
-    kernel = kernel or KERNEL
+    """{kernel name: {counter: mean per dispatch}} of the matching kernels."""
+    pat = re.compile(kernel or KERNEL)
     agg = collections.defaultdict(float)
     for r in csv.DictReader(open(path)):
-        if kernel not in r["Kernel_Name"]:
+        if not pat.search(r["Kernel_Name"]):
             continue
-        agg[(r["Dispatch_Id"], r["Counter_Name"])] += float(r["Counter_Value"])
-    per = collections.defaultdict(list)
-    for (_, c), v in agg.items():
-        per[c].append(v)
-    return {c: sum(v) / len(v) for c, v in per.items()}
+        agg[(r["Kernel_Name"], r["Dispatch_Id"], r["Counter_Name"])] += float(r["Counter_Value"])
+    per = collections.defaultdict(lambda: collections.defaultdict(list))
+    for (k, _, c), v in agg.items():
+        per[k][c].append(v)
+    return {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in per.items()}
 
 
 def main(pmc_dir, key, out="profiles/pmc_summary.json", note=""):
-    m = {}
+    per_kernel = collections.defaultdict(dict)
     for sub in sorted(os.listdir(pmc_dir)):
         f = os.path.join(pmc_dir, sub, "p_counter_collection.csv")
         if os.path.exists(f):
-            m.update(means(f))
+            for k, cs in means(f).items():
+                per_kernel[k].update(cs)
+    call = collections.defaultdict(float)
+    for cs in per_kernel.values():
+        for c, v in cs.items():
+            call[c] += v
     d = json.load(open(out)) if os.path.exists(out) else {}
-    e = {"counters_mean_per_dispatch": m, "note": note}
-    if "FETCH_SIZE" in m and "WRITE_SIZE" in m:
-        e["hbm_bytes_per_launch"] = (2 * m["FETCH_SIZE"] + m["WRITE_SIZE"]) * 1024
+    e = {"counters_mean_per_dispatch": dict(call), "per_kernel": per_kernel, "note": note}
+    if "FETCH_SIZE" in call and "WRITE_SIZE" in call:
+        e["hbm_bytes_per_launch"] = (2 * call["FETCH_SIZE"] + call["WRITE_SIZE"]) * 1024
     d[key] = e
     json.dump(d, open(out, "w"), indent=1, sort_keys=True)
     print(json.dumps(e, indent=1))
