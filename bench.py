@@ -15,8 +15,9 @@ overlapping frame k+1's render from a second band buffer).
 
 Printed (rank 0, one JSON line): value = (primary + shadow rays of all ranks)
 x K / max-over-ranks wall time, plus
-  roofline     — the render call (the general kernel k_render_fast and, on
-                 two-class launches, the lean-pixel kernel k_render_lean), HIP
+  roofline     — the render call (two-class launches: the lean-pixel kernel
+                 k_render_lean + the batched general-pixel kernel
+                 k_render_gen, or k_render_fast where those do not apply), HIP
                  events on the stream it runs on, against the 8 TB/s HBM peak.
                  `achieved` = SURVEY 8(d)'s algorithmic bytes per ray — 32 B
                  per BVH box and 36 B per triangle the ray is tested against,
@@ -291,6 +292,10 @@ def main():
         elapsed = float(e.item())
     kern_ms = sum(a.elapsed_time(b) for a, b in evs) / max(1, args.steps)
     lean_groups, general_groups = ds.last_split()
+    # outside the timed region: one more launch with Stats, for how many of
+    # the batched general pixels fell back to the one-sample loop
+    ds.render_bands_device(opts, local_bufs[0], BAND_H, rank, world, stream=stream, stats=True)
+    batched_groups, batch_fallback = ds.last_batch()
     # outside the timed region: the gathered frame must equal one GPU's
     # single-call frame bit for bit (same samples, same arithmetic per pixel)
     frame_check = None
@@ -355,6 +360,7 @@ def main():
                 "scene_setup_s": round(setup_s, 3), "scene_setup_ms_lib": round(info["build_ms"], 1),
                 "first_frame_ms": None if first_frame_ms is None else round(first_frame_ms, 1),
                 "lean_pixel_groups": lean_groups, "general_pixel_groups": general_groups,
+                "batched_general_groups": batched_groups, "batch_fallback_groups": batch_fallback,
                 "bvh_builder": {"sah": "host binned SAH", "ploc": "device PLOC"}[args.bvh],
             },
             "roofline": {
@@ -364,7 +370,9 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
-                "kernel": "render call: k_render_fast<false> + k_render_lean (two-class launch)",
+                "kernel": ("render call: " + ("k_render_lean + k_render_gen (two-class launch)" if batched_groups
+                                              else "k_render_lean + k_render_fast<false> (two-class launch)"
+                                              if lean_groups else "k_render_fast<false>")),
                 "kernel_ms": round(kern_ms, 4),
                 "bytes_per_launch": int(bytes_launch),
                 "definition": ("SURVEY 8(d) per-ray bytes (32 B/BVH box + 36 B/triangle tested, 12 B/pixel) over "

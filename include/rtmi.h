@@ -171,6 +171,17 @@ typedef struct rt_options {
  * provably miss it) renders those pixels with a second, lean-only kernel from
  * a per-launch list. Scheduling only: the image and Stats are the same. */
 #define RT_FLAG_NO_SPLIT 0x10u
+/* float32 kernel, two-class launches: render the general (not lean) pixels
+ * with the one-sample loop of the general kernel. By default, in scenes of
+ * one mesh object with distant lights only and no reflection, they render in
+ * a kernel that carries several samples per lane through each face list
+ * (falling back to the one-sample loop for a pixel whose shadow rays need
+ * the BVH). Scheduling only: the image and Stats are the same. */
+#define RT_FLAG_NO_BATCH 0x20u
+/* Test hook: the batched general kernel discards each general pixel's
+ * batches at its last one and re-renders the pixel with the one-sample loop
+ * (the path it takes when a shadow ray needs the BVH). Same image and Stats. */
+#define RT_FLAG_BATCH_FALLBACK 0x40u
 
 /* Stats (src/renderer/stats.nim:4-13) plus ray counts for Mray/s. */
 typedef struct rt_stats {
@@ -393,6 +404,12 @@ int rt_scene_last_counters(rt_scene *scene, rt_traversal_counters *out);
  * the lean-pixel kernel and by the general kernel (RT_FLAG_NO_SPLIT; a
  * float64 call counts every group as general). Host-side bookkeeping, no wait. */
 int rt_scene_last_split(rt_scene *scene, int64_t *lean_groups, int64_t *general_groups);
+/* Of the last render call's general pixel groups: how many went to the
+ * batched general kernel (0 with RT_FLAG_NO_BATCH or where it does not
+ * apply), and how many of those it re-rendered with the one-sample loop
+ * because a shadow ray needed the BVH (as of the last call that returned
+ * Stats; -1 before any). Diagnostics for tests and the benchmark. */
+int rt_scene_last_batch(rt_scene *scene, int64_t *batched_groups, int64_t *fallback_groups);
 
 /* ---- helpers ----------------------------------------------------------- */
 

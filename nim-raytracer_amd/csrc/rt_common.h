@@ -21,7 +21,7 @@ enum : int32_t { LIGHT_DISTANT = 0, LIGHT_POINT = 1 };
 // DevObject.xf: what world_to_object is (host-classified, float32 fast paths)
 enum : int32_t { XF_IDENTITY = 0, XF_TRANSLATE = 1, XF_GENERAL = 2 };
 // RenderParams.flags bits
-enum : int32_t { RT_DEV_FLAG_COUNT = 0x2 };
+enum : int32_t { RT_DEV_FLAG_COUNT = 0x2, RT_DEV_FLAG_FALLBACK = 0x40 };
 
 constexpr int kMaxBvhDepth = 60;      // stack fits one 64-lane VGPR
 constexpr int kLeafMax = 4;           // triangles per BVH leaf (arrays padded by kLeafMax-1)
@@ -252,7 +252,8 @@ struct FastParams {
 
 enum : int32_t {
   STAT_PRIMARY = 0, STAT_TESTS = 1, STAT_HITS = 2, STAT_SHADOW = 3, STAT_REFL = 4,
-  STAT_NODE_FETCH = 5, STAT_TRI_FETCH = 6, STAT_LANE_NODES = 7, STAT_LANE_TRIS = 8
+  STAT_NODE_FETCH = 5, STAT_TRI_FETCH = 6, STAT_LANE_NODES = 7, STAT_LANE_TRIS = 8,
+  STAT_GEN_FALLBACK = 9  // k_render_gen pixel groups re-rendered by the one-sample loop
 };
 // float32 kernel scene-feature subset index (rt_kernels_f32_part.hip): bit 0
 // sphere, 1 box, 2 mesh, 3 general transform, 4 point light, 5 reflection,
@@ -273,6 +274,8 @@ int rtmi_launch_render_f64(const rtmi::RenderParams<double>* p, int blocks, void
 int rtmi_render_f32_blocks_per_cu(int count, unsigned subset, size_t shmem);
 int rtmi_launch_lean_f32(const rtmi::FastParams* p, unsigned subset, int blocks, size_t shmem, void* stream);
 int rtmi_lean_f32_blocks_per_cu(unsigned subset, size_t shmem);
+int rtmi_launch_gen_f32(const rtmi::FastParams* p, unsigned subset, int blocks, size_t shmem, void* stream);
+int rtmi_gen_f32_blocks_per_cu(unsigned subset, size_t shmem);
 int rtmi_launch_ppm_encode(const float* fb, long long n, int bits, int srgb, void* out, void* stream);
 int rtmi_launch_rgba_encode(const float* fb, long long npix, unsigned int alpha, void* out, void* stream);
 // Sets this thread's rt_last_error() text; returns code (rtmi.cpp).

@@ -994,36 +994,14 @@ __device__ __forceinline__ F3 camera_dir(KP p, const GroupPix& gp, int s, const 
   return camera_ray_dir(p, px, py);
 }
 
-// Lean pixels, kLeanBatch samples per lane at once. A lean pixel (one-pixel
-// wave; its pixel list is empty and every light is a distant light whose
-// shadow skip bit is set, no reflection: FastParams.pix_info) never touches
-// the mesh, so its samples only visit the analytic objects. The per-sample
-// loop pays the scalar work of every object visit (record loads, type
-// dispatch, loop control, hit-count popcounts: the CU's one scalar unit,
-// shared by its 32 resident waves, is the kernel's busiest pipe) once per 64
-// rays; here each lane carries kLeanBatch samples through the same object
-// and light loops, so that work is paid once per 64 x kLeanBatch rays. Same
-// arithmetic per sample as shade_path (camera_dir, analytic_t, the
-// irradiance sum), the samples' colours added to the pixel in sample order:
-// frames bit-identical to the one-sample loop (tests: binned vs
-// RT_FLAG_NO_BINNING, which takes no pixel records).
-constexpr int kLeanBatch = 4;
-template <unsigned F, int S = kLeanBatch>
-__device__ __forceinline__ void lean_batch(KP p, const GroupPix& gp, int it0, const LdsF* tb, Acc& acc,
-                                           Stats32& ws) {
-  // Branch-free: per-sample predicates are lane masks in SGPRs and every
-  // update is a select (v_cndmask), so the samples' code is straight-line
-  // VALU (no exec-mask save / restore per sample). A masked-off term adds an
-  // exact zero (fma(ci, 0, E) == E, acc + 0 == acc for the non-negative
-  // sums), so values equal shade_path's branchy ones bit for bit.
-#ifdef RTMI_DIAG_NOSAMPLES
-  return;  // diagnostic build only: the work-item overhead without the samples
-#endif
-  const F3 o = f3(p->cam[0], p->cam[1], p->cam[2]);
-  // sample positions: akGrid with m a power of two (C2-C5) as
-  // s = (s & (m-1), s >> log2 m), the sampler decided once for the batch
+// Sample positions of a batch (S samples per lane: iterations it0 .. it0+S-1
+// of a one-pixel wave) and their camera-ray directions; akGrid with m a
+// power of two (C2-C5) as s = (s & (m-1), s >> log2 m), the sampler decided
+// once for the batch.
+template <unsigned F, int S>
+__device__ __forceinline__ void batch_dirs(KP p, const GroupPix& gp, int it0, const LdsF* tb, F3 (&d)[S],
+                                           bool (&sv)[S]) {
   float px[S], py[S];
-  bool sv[S];
   if (p->aa_kind == 1 && p->log2_grid_m >= 0) {
     const int mm = p->grid_m - 1, lg = p->log2_grid_m;
     const float st = p->sample_step, of = p->sample_off;
@@ -1042,7 +1020,42 @@ __device__ __forceinline__ void lean_batch(KP p, const GroupPix& gp, int it0, co
       camera_pos<F>(p, gp, s < p->spp ? s : 0, tb, px[k], py[k]);
     }
   }
+#pragma unroll
+  for (int k = 0; k < S; ++k) d[k] = camera_ray_dir(p, px[k], py[k]);
+}
+
+// Lean pixels, kLeanBatch samples per lane at once. A lean pixel (one-pixel
+// wave; its pixel list is empty and every light is a distant light whose
+// shadow skip bit is set, no reflection: FastParams.pix_info) never touches
+// the mesh, so its samples only visit the analytic objects. The per-sample
+// loop pays the scalar work of every object visit (record loads, type
+// dispatch, loop control, hit-count popcounts: the CU's one scalar unit,
+// shared by its 32 resident waves, is the kernel's busiest pipe) once per 64
+// rays; here each lane carries kLeanBatch samples through the same object
+// and light loops, so that work is paid once per 64 x kLeanBatch rays. Same
+// arithmetic per sample as shade_path (camera_dir, analytic_t, the
+// irradiance sum), the samples' colours added to the pixel in sample order:
+// frames bit-identical to the one-sample loop (tests: binned vs
+// RT_FLAG_NO_BINNING, which takes no pixel records).
+#ifndef RTMI_LEAN_BATCH
+#define RTMI_LEAN_BATCH 4
+#endif
+constexpr int kLeanBatch = RTMI_LEAN_BATCH;
+template <unsigned F, int S = kLeanBatch>
+__device__ __forceinline__ void lean_batch(KP p, const GroupPix& gp, int it0, const LdsF* tb, Acc& acc,
+                                           Stats32& ws) {
+  // Branch-free: per-sample predicates are lane masks in SGPRs and every
+  // update is a select (v_cndmask), so the samples' code is straight-line
+  // VALU (no exec-mask save / restore per sample). A masked-off term adds an
+  // exact zero (fma(ci, 0, E) == E, acc + 0 == acc for the non-negative
+  // sums), so values equal shade_path's branchy ones bit for bit.
+#ifdef RTMI_DIAG_NOSAMPLES
+  return;  // diagnostic build only: the work-item overhead without the samples
+#endif
+  const F3 o = f3(p->cam[0], p->cam[1], p->cam[2]);
   F3 d[S];
+  bool sv[S];
+  batch_dirs<F, S>(p, gp, it0, tb, d, sv);
   unsigned nprim = 0u;
   // trace (renderer.nim:47-67) of the camera rays over the analytic objects
   // in scene order (the mesh is left out: none of the pixel's rays can hit
@@ -1054,7 +1067,6 @@ __device__ __forceinline__ void lean_batch(KP p, const GroupPix& gp, int it0, co
   int hob[S];
 #pragma unroll
   for (int k = 0; k < S; ++k) {
-    d[k] = camera_ray_dir(p, px[k], py[k]);
     nprim += pc(bal(sv[k]));
     th[k] = sv[k] ? finf() : -1.0f;
     hob[k] = -1;
@@ -1189,6 +1201,352 @@ __device__ __forceinline__ void lean_batch(KP p, const GroupPix& gp, int it0, co
                     lt ? E[k].z : (sky ? bg.z : 0.0f));
     acc_add3(acc, c.x, c.y, c.z);
   }
+}
+
+// tri_test for a ray that only needs the closest t (shadow rays): the best
+// t's float bits replace the (t, face) key — a tie never changes t, so t,
+// the culling limit tc and "found" follow tri_test's exactly. A lane that
+// takes no part holds best = +0.0 (nothing is below it).
+__device__ __forceinline__ void tri_test_t(const RT_CONST TriFast& T, F3 o, F3 d, float& best, float& tc) {
+  const float tx = o.x - T.v0[0], ty = o.y - T.v0[1], tz = o.z - T.v0[2];
+  const float cx = __builtin_fmaf(ty, d.z, -tz * d.y);
+  const float cy = __builtin_fmaf(tz, d.x, -tx * d.z);
+  const float cz = __builtin_fmaf(tx, d.y, -ty * d.x);
+  const float u = __builtin_fmaf(T.e2[0], cx, __builtin_fmaf(T.e2[1], cy, T.e2[2] * cz));
+  const float v = __builtin_fmaf(T.e1n[0], cx, __builtin_fmaf(T.e1n[1], cy, T.e1n[2] * cz));
+  const float det = __builtin_fmaf(T.nn[0], d.x, __builtin_fmaf(T.nn[1], d.y, T.nn[2] * d.z));
+  const float tt = __builtin_fmaf(T.nn[0], tx, __builtin_fmaf(T.nn[1], ty, T.nn[2] * tz));
+  const float t = tt * rcp(-det);
+  const float g = fminf(fminf(fminf(u, v), det - (u + v)), det - 0.000001f);
+  const float ts = g >= 0.0f ? t : -1.0f;
+  const bool acc = __float_as_uint(ts) < __float_as_uint(best);
+  best = acc ? ts : best;
+  tc = acc ? ts : tc;
+}
+
+// The faces listed at ent[b, e) against the rays of the batch's samples
+// whose bit is set in fl (wave-uniform), each face record fetched once for
+// all of them. Camera rays (KEY): list_search's (t, face) key. Shadow rays
+// (!KEY): tri_test_t and the exact early exit (a sample's lane retires once
+// it holds a hit with t <= stop; the search ends when no lane of a listed
+// sample is left).
+template <int S, bool KEY>
+__device__ __forceinline__ void list_search_batch(KP p, const int32_t* ent, int b, int e, unsigned fl,
+                                                  const F3 (&ro)[S], const F3 (&rd)[S], const float (&stop)[S],
+                                                  unsigned long long (&key)[S], float (&best)[S], float (&tc)[S]) {
+  for (int k0 = b; k0 < e; k0 += 4) {
+    const RT_CONST int32_t* q = cp(ent) + k0;
+    const int r[4] = {q[0], q[1], q[2], q[3]};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (j > 0 && k0 + j >= e) break;
+      const RT_CONST TriFast& T = *rec<TriFast>(p, r[j]);
+#pragma unroll
+      for (int k = 0; k < S; ++k)
+        if ((fl >> k) & 1u) {
+          if constexpr (KEY) tri_test(T, ro[k], rd[k], key[k], tc[k]);
+          else tri_test_t(T, ro[k], rd[k], best[k], tc[k]);
+        }
+    }
+    if constexpr (!KEY) {
+      unsigned long long left = 0ull;
+#pragma unroll
+      for (int k = 0; k < S; ++k)
+        if ((fl >> k) & 1u) {
+          tc[k] = tc[k] <= stop[k] ? -1.0f : tc[k];
+          left |= bal(tc[k] >= 0.0f);
+        }
+      if (left == 0ull) break;
+    }
+  }
+}
+
+// The mesh's AABB gate (TriangleMesh.intersect, geom.nim:339-341) in the
+// traversal's slab form, as trace() forms it: a ray starting inside the box
+// misses.
+__device__ __forceinline__ bool mesh_gate(const FObj& ob, const SlabRay& sr) {
+  const float ax = __builtin_fmaf(ob.lo[0], sr.ni.x, -sr.oi.x), bx = __builtin_fmaf(ob.hi[0], sr.ni.x, -sr.oi.x);
+  const float ay = __builtin_fmaf(ob.lo[1], sr.ni.y, -sr.oi.y), by = __builtin_fmaf(ob.hi[1], sr.ni.y, -sr.oi.y);
+  const float az = __builtin_fmaf(ob.lo[2], sr.ni.z, -sr.oi.z), bz = __builtin_fmaf(ob.hi[2], sr.ni.z, -sr.oi.z);
+  const float gmin = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
+  const float gmax = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz)) * 1.00000024f;
+  return gmin <= gmax && gmin >= 0.0f;
+}
+
+// General pixels, S samples per lane at once (two-class launches: the
+// pixels that are not lean). Scenes of one mesh object (FastParams
+// .shadow_mesh), analytic objects and distant lights only, no reflection;
+// one-pixel waves with the pixel's record (pinfo) and its camera-ray list.
+// The same per-sample arithmetic as shade_path / trace / mesh_search —
+// camera rays search the pixel's face list, shadow rays to a light whose
+// skip bit is clear search their light-grid cells with the exact early
+// exit — with each face record, object record and loop step paid once per
+// 64 x S rays instead of per 64. No BVH here: when a shadow ray would need
+// it (a light without a grid, an origin beyond the grid's float32-safe
+// radius) the batch returns false
+// before adding anything and the caller renders the whole pixel with the
+// one-sample loop. Stats go to `wi` (committed by the caller). Frames and
+// Stats bit-identical to the one-sample loop (test_gpu_split.py against
+// RT_FLAG_NO_BATCH / NO_SPLIT / NO_BINNING).
+template <unsigned F, int S>
+__device__ __forceinline__ bool gen_batch(KP p, const GroupPix& gp, int it0, const LdsF* tb, unsigned pinfo,
+                                          LdsF* ls, Acc& acc, Stats32& wi) {
+  static_assert(3 * S <= kLdsSlots, "albedo stash: 3 LDS slots per sample");
+  // kernel arguments re-read through a laundered pointer at each stage
+  // (params()): hoisted, the many fields this path reads stay pinned in
+  // SGPRs across the whole batch and spill
+  p = params();
+  const F3 o = f3(p->cam[0], p->cam[1], p->cam[2]);
+  F3 d[S];
+  bool sv[S];
+  batch_dirs<F, S>(p, gp, it0, tb, d, sv);
+  unsigned nprim = 0u;
+  // th: -1 invalid sample, +inf sky, else the closest hit's t (lean_batch)
+  float th[S];
+  int hob[S], htri[S];
+#pragma unroll
+  for (int k = 0; k < S; ++k) {
+    nprim += pc(bal(sv[k]));
+    th[k] = sv[k] ? finf() : -1.0f;
+    hob[k] = -1;
+    htri[k] = -1;
+  }
+  const int nobj = p->nobj, mesh = p->shadow_mesh;
+  unsigned hitl = 0u;
+  // camera rays: trace (renderer.nim:47-67) over the objects in scene order
+  for (int i = 0; i < nobj; ++i) {
+    p = params();
+    const FObj ob = at(p->objs, i);
+    if (i == mesh) {
+      // an empty pixel list: no camera ray of the pixel can hit the mesh
+      // (trace's no_mesh: the gate's verdict cannot matter)
+      if ((pinfo & kPixCount) == 0u || ob.root < 0) continue;
+      F3 ro[S], rd[S];
+      unsigned long long key[S], key0[S];
+      float tc[S], unused[S];
+      unsigned long long anyp = 0ull;
+#pragma unroll
+      for (int k = 0; k < S; ++k) {
+        to_object<F>(p, ob, i, o, d[k], ro[k], rd[k]);
+        const bool part = sv[k] && mesh_gate(ob, slab_ray(ro[k], rd[k]));
+        tc[k] = part ? th[k] : -1.0f;
+        key0[k] = part ? tkey(th[k], 0u) : 0ull;
+        key[k] = key0[k];
+        unused[k] = 0.0f;
+        anyp |= bal(part);
+      }
+      if (anyp != 0ull) {  // the wave's one pixel: one list for every sample
+        const int pu = __builtin_amdgcn_readfirstlane(gp.y * p->width + gp.x);
+        list_search_batch<S, true>(p, p->pix_ent, cp(p->pix_off)[pu], cp(p->pix_off)[pu + 1], (1u << S) - 1u, ro, rd,
+                                   unused, key, unused, tc);
+      }
+#pragma unroll
+      for (int k = 0; k < S; ++k) {  // found => 0 <= t < th: the hit counts (trace's update rule)
+        const bool c = key[k] != key0[k];
+        th[k] = c ? __uint_as_float((unsigned int)(key[k] >> 32)) : th[k];
+        hob[k] = c ? i : hob[k];
+        htri[k] = c ? (int)(unsigned int)key[k] : htri[k];
+        hitl += c ? 1u : 0u;
+      }
+      continue;
+    }
+#pragma unroll
+    for (int k = 0; k < S; ++k) {
+      const float t = analytic_t<F>(p, ob, i, o, d[k]);
+      const float tp = t >= 0.0f ? t : finf();
+      const bool c = tp < th[k];
+      th[k] = c ? tp : th[k];
+      hob[k] = c ? i : hob[k];
+      hitl += c ? 1u : 0u;
+    }
+  }
+  // shade (renderer.nim:71-127): normals per distinct object hit (mesh:
+  // the face normal by face id, renderer.nim:84-88), shadow origins
+  unsigned long long litm[S], pend[S], skym[S];  // lit / sky lanes per sample
+  F3 N[S], so[S];
+#pragma unroll
+  for (int k = 0; k < S; ++k) {
+    litm[k] = m_lt(th[k], finf()) & m_ge(th[k], 0.0f);
+    skym[k] = bal(th[k] == finf());
+    pend[k] = litm[k];
+    N[k] = f3(0.0f, 0.0f, 0.0f);
+    so[k] = f3(__builtin_fmaf(d[k].x, th[k], o.x), __builtin_fmaf(d[k].y, th[k], o.y),
+               __builtin_fmaf(d[k].z, th[k], o.z));  // the hit point until N is known
+  }
+  for (;;) {
+    int oi = -1;
+#pragma unroll
+    for (int k = S - 1; k >= 0; --k)
+      if (pend[k]) oi = __builtin_amdgcn_readlane(hob[k], (int)__builtin_ctzll(pend[k]));
+    if (oi < 0) break;
+    int oi_cmp = oi;
+    asm volatile("" : "+s"(oi_cmp));
+    p = params();
+    const FObj ob = at(p->objs, oi);
+    const RT_CONST FObjX& ox = at(p->objx, oi);
+    const bool is_mesh = (F & F_MESH) && ob.type == GEOM_MESH;
+    const int nbase = ox.normal_base;
+#pragma unroll
+    for (int k = 0; k < S; ++k) {
+      const unsigned long long mine = bal(hob[k] == oi_cmp) & pend[k];
+      pend[k] &= ~mine;
+      const bool mi = lane_in(mine);
+      F3 n;
+      if (is_mesh) {
+        // every lane loads (face 0 for the others): no exec-mask branch
+        const float* fn = p->normals + 3 * (size_t)(nbase + (mi ? htri[k] : 0));
+        n = f3(fn[0], fn[1], fn[2]);
+      } else {
+        F3 ho, unused;
+        to_object<F>(p, ob, oi, so[k], f3(0.0f, 0.0f, 0.0f), ho, unused);
+        n = analytic_normal<F>(ob, ho);
+      }
+      if ((F & F_XF_GENERAL) && ob.xf == XF_GENERAL) {  // object_to_world * n, not re-normalised
+        const float* m = ox.o2w;
+        n = f3(__builtin_fmaf(m[0], n.x, __builtin_fmaf(m[3], n.y, m[6] * n.z)),
+               __builtin_fmaf(m[1], n.x, __builtin_fmaf(m[4], n.y, m[7] * n.z)),
+               __builtin_fmaf(m[2], n.x, __builtin_fmaf(m[5], n.y, m[8] * n.z)));
+      }
+      N[k] = f3(mi ? n.x : N[k].x, mi ? n.y : N[k].y, mi ? n.z : N[k].z);
+      // albedo / pi waits in LDS (slots 3k..3k+2) until the lights are summed
+      if (mi) lds_put3(ls, 3 * k, f3(ox.albedo_pi[0], ox.albedo_pi[1], ox.albedo_pi[2]));
+    }
+  }
+  const float bias = p->bias;
+#pragma unroll
+  for (int k = 0; k < S; ++k)
+    so[k] = f3(__builtin_fmaf(N[k].x, bias, so[k].x), __builtin_fmaf(N[k].y, bias, so[k].y),
+               __builtin_fmaf(N[k].z, bias, so[k].z));
+  // one shadow ray per distant light and lit sample
+  F3 E[S];
+  unsigned long long anylit = 0ull;
+  unsigned nlit = 0u;
+#pragma unroll
+  for (int k = 0; k < S; ++k) {
+    E[k] = f3(0.0f, 0.0f, 0.0f);
+    anylit |= litm[k];
+    nlit += pc(litm[k]);
+  }
+  const int nl = anylit ? p->nlight : 0;
+  const unsigned skipw = pinfo >> 24;  // bit l: no shadow ray to light l can meet the mesh
+  for (int li = 0; li < nl; ++li) {
+    p = params();
+    const FLight L = at(p->lights, li);
+    const F3 sd = f3(-L.v[0], -L.v[1], -L.v[2]);
+    float ts[S];  // unlit samples start at 0 (take no part)
+#pragma unroll
+    for (int k = 0; k < S; ++k) ts[k] = lane_in(litm[k]) ? finf() : 0.0f;
+    for (int i = 0; i < nobj; ++i) {
+      p = params();
+      const FObj ob = at(p->objs, i);
+      if (i == mesh) {
+        if ((li < 8 && ((skipw >> li) & 1u) != 0u) || ob.root < 0) continue;
+        F3 ro[S], rd[S];
+        unsigned long long pm[S], anyp = 0ull;
+#pragma unroll
+        for (int k = 0; k < S; ++k) {
+          to_object<F>(p, ob, i, so[k], sd, ro[k], rd[k]);
+          pm[k] = bal(lane_in(litm[k]) && mesh_gate(ob, slab_ray(ro[k], rd[k])));
+          anyp |= pm[k];
+        }
+        if (anyp == 0ull) continue;  // no lane enters the mesh's box
+        if (!p->grids || p->grids[li].gu <= 0) return false;  // the BVH: the caller's one-sample loop
+        // mesh_search: the exact early exit's stop distance (the analytic
+        // objects after the mesh), clamped below each lane's initial limit
+        float stop[S], tc[S], best[S];
+        unsigned long long unused[S];
+#pragma unroll
+        for (int k = 0; k < S; ++k) stop[k] = finf();
+        for (int j = i + 1; j < nobj; ++j) {
+          const FObj oj = at(p->objs, j);
+#pragma unroll
+          for (int k = 0; k < S; ++k) {
+            const float tj = analytic_t<F>(p, oj, j, so[k], sd);
+            stop[k] = tj >= 0.0f ? fminf(stop[k], tj) : stop[k];
+          }
+        }
+        // the light grid's cells (rt_bins.h); a float32-safe lane off the
+        // grid can hit no face
+        const RT_CONST LightGrid& G = cp(p->grids)[li];
+        int cell[S];
+        unsigned long long todo[S], left = 0ull, unsafe = 0ull;
+#pragma unroll
+        for (int k = 0; k < S; ++k) {
+          const bool part = lane_in(pm[k]);
+          stop[k] = fminf(stop[k], __uint_as_float(__float_as_uint(ts[k]) - 1u));
+          tc[k] = part ? ts[k] : -1.0f;
+          best[k] = part ? ts[k] : 0.0f;
+          unused[k] = 0ull;
+          const F3 r = ro[k];
+          const float gu = __builtin_fmaf(r.x, G.e1[0], __builtin_fmaf(r.y, G.e1[1], r.z * G.e1[2]));
+          const float gv = __builtin_fmaf(r.x, G.e2[0], __builtin_fmaf(r.y, G.e2[1], r.z * G.e2[2]));
+          const float fu = (gu - G.u0) * G.inv_h, fv = (gv - G.v0) * G.inv_h;
+          const bool safe = fmaxf(fmaxf(fabsf(r.x), fabsf(r.y)), fabsf(r.z)) <= G.rmax;
+          const bool on = fu >= 0.0f && fu < (float)G.gu && fv >= 0.0f && fv < (float)G.gv;
+          cell[k] = safe && on ? G.off_base + (int)fv * G.gu + (int)fu : -1;
+          todo[k] = bal(part && cell[k] >= 0);
+          unsafe |= bal(part && !safe);
+          left |= todo[k];
+        }
+        if (unsafe != 0ull) return false;
+        const int32_t* bent = p->grid_ent + G.ent_base;
+        // every distinct cell of the batch's shadow rays in turn (each round
+        // retires at least the lane the cell was taken from)
+        while (left != 0ull) {
+          int kb = -1;
+#pragma unroll
+          for (int k = S - 1; k >= 0; --k)
+            if (todo[k]) kb = __builtin_amdgcn_readlane(cell[k], (int)__builtin_ctzll(todo[k]));
+          unsigned fl = 0u;
+          left = 0ull;
+#pragma unroll
+          for (int k = 0; k < S; ++k) {
+            const unsigned long long m = bal(cell[k] == kb) & todo[k];
+            fl |= m != 0ull ? (1u << k) : 0u;
+            todo[k] &= ~m;
+            left |= todo[k];
+          }
+          list_search_batch<S, false>(p, bent, cp(p->grid_off)[kb], cp(p->grid_off)[kb + 1], fl, ro, rd, stop,
+                                      unused, best, tc);
+        }
+#pragma unroll
+        for (int k = 0; k < S; ++k) {  // found => 0 <= t < ts: the hit counts
+          const bool c = lane_in(pm[k]) && __float_as_uint(best[k]) != __float_as_uint(ts[k]);
+          ts[k] = c ? best[k] : ts[k];
+          hitl += c ? 1u : 0u;
+        }
+        continue;
+      }
+#pragma unroll
+      for (int k = 0; k < S; ++k) {
+        const float t = analytic_t<F>(p, ob, i, so[k], sd);
+        const float tp = t >= 0.0f ? t : finf();
+        const bool c = tp < ts[k];
+        ts[k] = c ? tp : ts[k];
+        hitl += c ? 1u : 0u;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < S; ++k) {  // unoccluded: shadeDiffuse (shader.nim:12-17)
+      const bool vis = lane_in(litm[k]) && !(ts[k] < finf());
+      irr_add(E[k], L.ci, vis ? fmaxf(dot3(N[k], sd), 0.0f) : 0.0f);
+    }
+  }
+  // the samples' colours in order: albedo / pi x E, the background for the sky
+  p = params();
+  const F3 bg = f3(p->bg[0], p->bg[1], p->bg[2]);
+#pragma unroll
+  for (int k = 0; k < S; ++k) {
+    const bool lt = lane_in(litm[k]), sky = lane_in(skym[k]);
+    const F3 a = mul3(lds_get3(ls, 3 * k), E[k]);
+    const F3 c = f3(lt ? a.x : (sky ? bg.x : 0.0f), lt ? a.y : (sky ? bg.y : 0.0f),
+                    lt ? a.z : (sky ? bg.z : 0.0f));
+    acc_add3(acc, c.x, c.y, c.z);
+  }
+  wi.v[STAT_PRIMARY] += nprim;
+  wi.v[STAT_SHADOW] += (unsigned)nl * nlit;
+  wi.v[STAT_HITS] += wave_sum(hitl);
+  return true;
 }
 
 // multiJittered / correlatedMultiJittered (sampling.nim:39-113): the wave
@@ -1402,8 +1760,11 @@ __global__ __launch_bounds__(256) RTMI_OCC void k_render_fast(const FastParams p
 // spilled SGPRs) its item loop keeps the arguments in SGPRs; per work item
 // it costs a dequeue, a list read and the pixel sum. Frames are
 // bit-identical to k_render_fast's lean path (same lean_batch, same sums).
+#ifndef RTMI_LEAN_WAVES
+#define RTMI_LEAN_WAVES 8
+#endif
 template <unsigned F>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k_render_lean(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RTMI_LEAN_WAVES))) void k_render_lean(
     const FastParams params_by_value) {
   (void)params_by_value;
   const KP p = params();
@@ -1443,6 +1804,96 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
     if (lane == 0) qj_next = (int)atomicAdd(head, 1u);
     g = qj * p->shards + shard;
   }
+  flush_stats(ws, lds_tot[wib], lane);
+  const int wave = (int)(blockIdx.x * (blockDim.x >> 6) + threadIdx.x / 64u);
+  if (lane < kStatSlots) p->partials[(size_t)wave * kStatSlots + lane] = lds_tot[wib][lane];
+}
+
+// The batched general-pixel kernel (two-class launches, rtmi.cpp
+// split_lists): the launch's non-lean pixel groups (p->order lists them),
+// each rendered by gen_batch from its pixel record, or — when a batch needs
+// the BVH — by k_render_fast's one-sample loop (shade_path) from scratch.
+// Used for scenes of one mesh object with distant lights only and no
+// reflection (the subsets that have k_render_lean); frames and Stats
+// bit-identical to k_render_fast.
+#ifndef RTMI_GEN_BATCH
+#define RTMI_GEN_BATCH 2
+#endif
+#ifndef RTMI_GEN_WAVES
+#define RTMI_GEN_WAVES 7
+#endif
+constexpr int kGenBatch = RTMI_GEN_BATCH;
+template <unsigned F>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RTMI_GEN_WAVES))) void k_render_gen(
+    const FastParams params_by_value) {
+  (void)params_by_value;
+  KP p = params();
+  __shared__ float lds[4][kLdsSlots][64];  // gen_batch's albedo stash / shade_path's scratch (the fallback)
+  extern __shared__ float sample_lds[];
+  __shared__ unsigned long long lds_tot[4][kStatSlots];
+  const int wib = (int)(threadIdx.x >> 6);
+  LdsF* ls = (LdsF*)&lds[wib][0][__lane_id()];
+  if (__lane_id() < (unsigned)kStatSlots) lds_tot[wib][__lane_id()] = 0ull;
+  Stats32 ws;
+#pragma unroll
+  for (int k = 0; k < kStatSlots; ++k) ws.v[k] = 0u;
+  const int shard = (int)(blockIdx.x % (unsigned int)p->shards);
+  unsigned int* head = p->queue + shard * kQueueStride;
+  int qj = 0;
+  if (__lane_id() == 0) qj = (int)atomicAdd(head, 1u);
+  qj = __builtin_amdgcn_readfirstlane(qj);
+  int qj_next = 0;
+  if (__lane_id() == 0) qj_next = (int)atomicAdd(head, 1u);
+  int g = qj * p->shards + shard;
+  int nflush = 0;
+  while (g < p->ngroups) {
+    p = params();
+    const int iters = p->iters;
+    const int gg = cp(p->order)[g];
+    const GroupPix gp = group_pixel(p, gg, lane_id_fresh());
+    const LdsF* tb = sample_table<F>(p, gp, sample_lds, wib, 64);
+    // the pixel's record (every listed group is one valid pixel)
+    const unsigned pinfo = at(p->pix_info, __builtin_amdgcn_readfirstlane(gp.y * p->width + gp.x));
+    Acc acc;
+    acc.v = f3(0.0f, 0.0f, 0.0f);
+    Stats32 wi;
+#pragma unroll
+    for (int k = 0; k < kStatSlots; ++k) wi.v[k] = 0u;
+    bool ok = true;
+    int it = 0;
+    for (; ok && it + kGenBatch <= iters; it += kGenBatch) ok = gen_batch<F, kGenBatch>(p, gp, it, tb, pinfo, ls, acc, wi);
+    for (; ok && it < iters; ++it) ok = gen_batch<F, 1>(p, gp, it, tb, pinfo, ls, acc, wi);
+    if (params()->flags & RT_DEV_FLAG_FALLBACK) ok = false;  // test hook (RT_FLAG_BATCH_FALLBACK)
+    if (ok) {
+      ws.v[STAT_PRIMARY] += wi.v[STAT_PRIMARY];
+      ws.v[STAT_SHADOW] += wi.v[STAT_SHADOW];
+      ws.v[STAT_HITS] += wi.v[STAT_HITS];
+    } else {  // some shadow ray needs the BVH: the whole pixel by the one-sample loop
+      acc.v = f3(0.0f, 0.0f, 0.0f);
+      ws.v[STAT_GEN_FALLBACK] += 1u;
+      for (int i2 = 0; i2 < iters; ++i2) {
+        p = params();
+        const int s = i2 * 64 + gp.sub;
+        const bool sv = gp.valid && s < p->spp;
+        const F3 d = camera_dir<F>(p, gp, s < p->spp ? s : 0, tb);
+        const F3 o = f3(p->cam[0], p->cam[1], p->cam[2]);
+        ws.v[STAT_PRIMARY] += pc(bal(sv));
+        shade_path<false, F, false>(p, o, d, sv, sv ? gp.y * p->width + gp.x : -1, pinfo, ls, acc, ws);
+      }
+    }
+    p = params();
+    finish_item(p, gp, acc.v, 64);
+    const int lane = lane_id_fresh();
+    if (++nflush >= p->stat_flush) {
+      flush_stats(ws, lds_tot[wib], lane);
+      nflush = 0;
+    }
+    qj = __builtin_amdgcn_readfirstlane(qj_next);
+    if (lane == 0) qj_next = (int)atomicAdd(head, 1u);
+    g = qj * p->shards + shard;
+  }
+  p = params();
+  const int lane = (int)__lane_id();
   flush_stats(ws, lds_tot[wib], lane);
   const int wave = (int)(blockIdx.x * (blockDim.x >> 6) + threadIdx.x / 64u);
   if (lane < kStatSlots) p->partials[(size_t)wave * kStatSlots + lane] = lds_tot[wib][lane];

@@ -61,7 +61,9 @@ template __global__ void fast::k_render_fast<true, fast::F_ALL>(const FastParams
   extern "C" int rtmi_launch_render_f32_part##k(unsigned, const rtmi::FastParams*, int, size_t, void*); \
   extern "C" int rtmi_render_f32_part_blocks_per_cu##k(unsigned, size_t);                              \
   extern "C" int rtmi_launch_lean_f32_part##k(unsigned, const rtmi::FastParams*, int, size_t, void*);   \
-  extern "C" int rtmi_lean_f32_part_blocks_per_cu##k(unsigned, size_t);
+  extern "C" int rtmi_lean_f32_part_blocks_per_cu##k(unsigned, size_t);                              \
+  extern "C" int rtmi_launch_gen_f32_part##k(unsigned, const rtmi::FastParams*, int, size_t, void*);    \
+  extern "C" int rtmi_gen_f32_part_blocks_per_cu##k(unsigned, size_t);
 RTMI_PART_DECL(0) RTMI_PART_DECL(1) RTMI_PART_DECL(2) RTMI_PART_DECL(3)
 RTMI_PART_DECL(4) RTMI_PART_DECL(5) RTMI_PART_DECL(6) RTMI_PART_DECL(7)
 RTMI_PART_DECL(8) RTMI_PART_DECL(9) RTMI_PART_DECL(10) RTMI_PART_DECL(11)
@@ -84,7 +86,26 @@ int (*const kLaunchLean[16])(unsigned, const rtmi::FastParams*, int, size_t, voi
 int (*const kOccupancyLean[16])(unsigned, size_t) = {
     RTMI_LO(0), RTMI_LO(1), RTMI_LO(2),  RTMI_LO(3),  RTMI_LO(4),  RTMI_LO(5),  RTMI_LO(6),  RTMI_LO(7),
     RTMI_LO(8), RTMI_LO(9), RTMI_LO(10), RTMI_LO(11), RTMI_LO(12), RTMI_LO(13), RTMI_LO(14), RTMI_LO(15)};
+#define RTMI_LG(k) rtmi_launch_gen_f32_part##k
+#define RTMI_GO(k) rtmi_gen_f32_part_blocks_per_cu##k
+int (*const kLaunchGen[16])(unsigned, const rtmi::FastParams*, int, size_t, void*) = {
+    RTMI_LG(0), RTMI_LG(1), RTMI_LG(2),  RTMI_LG(3),  RTMI_LG(4),  RTMI_LG(5),  RTMI_LG(6),  RTMI_LG(7),
+    RTMI_LG(8), RTMI_LG(9), RTMI_LG(10), RTMI_LG(11), RTMI_LG(12), RTMI_LG(13), RTMI_LG(14), RTMI_LG(15)};
+int (*const kOccupancyGen[16])(unsigned, size_t) = {
+    RTMI_GO(0), RTMI_GO(1), RTMI_GO(2),  RTMI_GO(3),  RTMI_GO(4),  RTMI_GO(5),  RTMI_GO(6),  RTMI_GO(7),
+    RTMI_GO(8), RTMI_GO(9), RTMI_GO(10), RTMI_GO(11), RTMI_GO(12), RTMI_GO(13), RTMI_GO(14), RTMI_GO(15)};
 }  // namespace
+
+// The batched general-pixel kernel of a feature subset (two-class launches).
+extern "C" int rtmi_launch_gen_f32(const rtmi::FastParams* p, unsigned subset, int blocks, size_t shmem,
+                                   void* stream) {
+  return kLaunchGen[(subset >> 3) & 15u](subset & 127u, p, blocks, shmem, stream);
+}
+
+// Resident blocks per CU of the batched general kernel; 0: none for the subset.
+extern "C" int rtmi_gen_f32_blocks_per_cu(unsigned subset, size_t shmem) {
+  return kOccupancyGen[(subset >> 3) & 15u](subset & 127u, shmem);
+}
 
 // The lean-pixel kernel of a feature subset (two-class launches).
 extern "C" int rtmi_launch_lean_f32(const rtmi::FastParams* p, unsigned subset, int blocks, size_t shmem,

@@ -144,6 +144,7 @@ struct rt_scene {
   hipStream_t aux = nullptr;
   hipEvent_t fork = nullptr, join = nullptr;
   int64_t last_lean = 0, last_general = 0;  // rt_scene_last_split
+  int64_t last_batched = 0, last_fallback = -1;  // rt_scene_last_batch
   int32_t nobj = 0, nlight = 0, nmesh = 0;
   int32_t shadow_mesh = -1;  // the only mesh object, or -1 (FastParams.shadow_mesh)
   int32_t has_point_light = 0;
@@ -1494,6 +1495,7 @@ int launch(rt_scene* s, const rt_options* o, const Mapping& mp, float* d_out, hi
     }
     s->last_lean = 0;
     s->last_general = p.ngroups;
+    s->last_batched = 0;
     const int e = rtmi_launch_render_f64(&p, blocks, st);
     if (e) return fail(RT_E_DEVICE, "render kernel launch failed: %s", hipGetErrorString((hipError_t)e));
   } else {
@@ -1513,7 +1515,16 @@ int launch(rt_scene* s, const rt_options* o, const Mapping& mp, float* d_out, hi
       const size_t shmem = f32_table_lds(o);
       const unsigned sub = f32_subset(s, o);
       FastParams ph = p, pl = p;
-      const int hb = (int)std::max(1LL, std::min<long long>(blocks, ((long long)sp->n_heavy + 3) / 4));
+      // the general pixels: the batched kernel (k_render_gen) for scenes of
+      // one mesh object with distant lights only, no reflection (the lean
+      // kernel's subsets) when both camera lists and light grids exist
+      const int gbpc = (o->flags & RT_FLAG_NO_BATCH) || p.shadow_mesh < 0 || !p.pix_off || !p.pix_ent || !p.grids ||
+                               p.has_point_light
+                           ? 0
+                           : rtmi_gen_f32_blocks_per_cu(sub, shmem);
+      const bool gen = gbpc > 0;
+      const long long hcap = gen ? std::min<long long>((long long)gbpc * s->num_cus, blocks) : blocks;
+      const int hb = (int)std::max(1LL, std::min<long long>(hcap, ((long long)sp->n_heavy + 3) / 4));
       ph.order = sp->heavy.p;
       ph.ngroups = sp->n_heavy;
       ph.shards = std::min(kQueueShards, hb);
@@ -1534,7 +1545,7 @@ int launch(rt_scene* s, const rt_options* o, const Mapping& mp, float* d_out, hi
         HIP_TRY(hipEventRecord(s->fork, st));
         HIP_TRY(hipStreamWaitEvent(s->aux, s->fork, 0));
       }
-      int e = rtmi_launch_render_f32(&ph, sub, hb, shmem, st);
+      int e = gen ? rtmi_launch_gen_f32(&ph, sub, hb, shmem, st) : rtmi_launch_render_f32(&ph, sub, hb, shmem, st);
       if (!e) e = rtmi_launch_lean_f32(&pl, sub, lb, shmem, sl);
       if (e) return fail(RT_E_DEVICE, "render kernel launch failed: %s", hipGetErrorString((hipError_t)e));
       if (!serial) {
@@ -1544,9 +1555,11 @@ int launch(rt_scene* s, const rt_options* o, const Mapping& mp, float* d_out, hi
       blocks = hb + lb;
       s->last_lean = sp->n_lean;
       s->last_general = sp->n_heavy;
+      s->last_batched = gen ? sp->n_heavy : 0;
     } else {
       s->last_lean = 0;
       s->last_general = p.ngroups;
+      s->last_batched = 0;
       const int e = rtmi_launch_render_f32(&p, f32_subset(s, o), blocks, f32_table_lds(o), st);
       if (e) return fail(RT_E_DEVICE, "render kernel launch failed: %s", hipGetErrorString((hipError_t)e));
     }
@@ -1584,6 +1597,7 @@ int read_stats(rt_scene* s, hipStream_t st, rt_stats* out) {
   out->num_intersection_hits = h[STAT_HITS];
   out->num_shadow_rays = h[STAT_SHADOW];
   out->num_reflection_rays = h[STAT_REFL];
+  s->last_fallback = (int64_t)h[STAT_GEN_FALLBACK];
   return RT_OK;
 }
 
@@ -1753,6 +1767,14 @@ extern "C" int rt_scene_last_split(rt_scene* s, int64_t* lean_groups, int64_t* g
   std::lock_guard<std::mutex> lk(s->mu);
   *lean_groups = s->last_lean;
   *general_groups = s->last_general;
+  return RT_OK;
+}
+
+extern "C" int rt_scene_last_batch(rt_scene* s, int64_t* batched_groups, int64_t* fallback_groups) {
+  if (!s || !batched_groups || !fallback_groups) return fail(RT_E_INVALID, "null argument");
+  std::lock_guard<std::mutex> lk(s->mu);
+  *batched_groups = s->last_batched;
+  *fallback_groups = s->last_fallback;
   return RT_OK;
 }
 

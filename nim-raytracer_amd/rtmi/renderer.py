@@ -101,6 +101,14 @@ class DeviceScene:
         check(lib().rt_scene_last_split(self.h, C.byref(a), C.byref(b)))
         return int(a.value), int(b.value)
 
+    def last_batch(self):
+        """(batched, fallback) general pixel groups of the last render call:
+        those the batched general kernel took, and of them those it
+        re-rendered with the one-sample loop (as of the last call with Stats)."""
+        a, b = C.c_int64(), C.c_int64()
+        check(lib().rt_scene_last_batch(self.h, C.byref(a), C.byref(b)))
+        return int(a.value), int(b.value)
+
     def last_counters(self):
         c = abi.rt_traversal_counters()
         check(lib().rt_scene_last_counters(self.h, C.byref(c)))

@@ -1,8 +1,11 @@
 """Two-class launches of the float32 kernel (rtmi.cpp split_lists): lean
 pixels — no camera ray can hit the mesh, every light is a distant light whose
 shadow rays provably miss it — render in k_render_lean from a per-launch
-list, the rest in k_render_fast. Scheduling only: frames and Stats must be
-bit-identical to the one-kernel launch (RT_FLAG_NO_SPLIT) and to the
+list, the rest in k_render_gen (several samples per lane through each face
+list; a pixel whose shadow rays need the BVH falls back to the one-sample
+loop) or, where that does not apply, k_render_fast. Scheduling only: frames
+and Stats must be bit-identical to the general pixels in k_render_fast
+(RT_FLAG_NO_BATCH), to the one-kernel launch (RT_FLAG_NO_SPLIT) and to the
 BVH-only kernel (RT_FLAG_NO_BINNING: no pixel records, no lean path at all),
 whose parity with the oracle test_gpu_parity.py pins.
 
@@ -12,7 +15,8 @@ stochastic samplers and progressive passes (step > 1) against the records."""
 import pytest
 
 from rtmi import Antialias, Options, Precision, akGrid, scenes
-from rtmi.abi import RT_FLAG_NO_BINNING, RT_FLAG_NO_SPLIT
+from rtmi.abi import (RT_FLAG_BATCH_FALLBACK, RT_FLAG_NO_BATCH, RT_FLAG_NO_BINNING, RT_FLAG_NO_REORDER,
+                      RT_FLAG_NO_SPLIT)
 from rtmi.dist import band_rows
 from rtmi.glm import X_AXIS, degToRad, inverse, mat4, rotate, translate, vec3
 from rtmi.renderer import DeviceScene
@@ -20,12 +24,15 @@ from rtmi.scene import akCorrelatedMultiJittered, akJittered, akMultiJittered
 
 pytestmark = pytest.mark.gpu
 
-FLAG_SETS = (0, RT_FLAG_NO_SPLIT, RT_FLAG_NO_BINNING)
+FLAG_SETS = (0, RT_FLAG_NO_BATCH, RT_FLAG_BATCH_FALLBACK, RT_FLAG_NO_SPLIT, RT_FLAG_NO_BINNING)
 
 
 def _opts(w, h, m, flags=0, aa=akGrid, bias=1e-4, seed=0):
+    # NO_REORDER: a short launch (these small frames) otherwise hands its
+    # groups out longest-first from a measuring launch, and such launches
+    # keep the one kernel (rtmi.cpp split_lists) — the split would go untested
     return Options(width=w, height=h, antialias=Antialias(aa, m), bias=bias, precision=Precision.fp32,
-                   flags=flags, seed=seed)
+                   flags=flags | RT_FLAG_NO_REORDER, seed=seed)
 
 
 def _frames(ds, make_opts, y0=0, y1=None, step=1, max_step=1):
@@ -137,6 +144,8 @@ def test_split_full_c3(gpu):
     ds.render_device(_opts(1920, 1080, 16), fb)
     lean, general = ds.last_split()
     assert lean + general == 1920 * 1080 and lean > 0.8 * 1920 * 1080, (lean, general)
+    batched, fallback = ds.last_batch()
+    assert batched == general and 0 <= fallback < 0.05 * general, (batched, fallback, general)
     ds.render_device(_opts(1920, 1080, 16, RT_FLAG_NO_SPLIT), fb)
     assert ds.last_split() == (0, 1920 * 1080)
 
@@ -150,3 +159,25 @@ def test_no_split_without_records(gpu):
         fb = torch.zeros(200 * 120 * 3, dtype=torch.float32, device="cuda")
         ds.render_device(_opts(200, 120, m), fb)
         assert ds.last_split()[0] == 0, name
+
+
+def test_batched_general_pixels_and_fallback(gpu):
+    """The batched general kernel takes the general pixels of a one-mesh,
+    distant-light scene and (almost) never falls back on the bunny; the fallback
+    (forced by the test hook after a pixel's batches already ran) discards
+    their colour and Stats — the frames above compare it bit for bit."""
+    import torch
+    ds = DeviceScene(scenes.mesh_bunny())
+    fb = torch.zeros(320 * 180 * 3, dtype=torch.float32, device="cuda")
+    ds.render_device(_opts(320, 180, 16), fb)
+    lean, general = ds.last_split()
+    batched, fallback = ds.last_batch()
+    assert general > 0 and batched == general and 0 <= fallback < 0.01 * general, (general, batched, fallback)
+    ds.render_device(_opts(320, 180, 16, RT_FLAG_BATCH_FALLBACK), fb)
+    assert ds.last_batch() == (general, general)
+    ds.render_device(_opts(320, 180, 16, RT_FLAG_NO_BATCH), fb)
+    assert ds.last_batch()[0] == 0
+    for name in ("mesh_mix", "two_meshes"):  # point light / two meshes: not batched
+        d2 = DeviceScene(SCENES[name]())
+        d2.render_device(_opts(200, 120, 16), fb)
+        assert d2.last_batch()[0] == 0, name

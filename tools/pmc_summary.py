@@ -1,7 +1,8 @@
 """Summarise rocprofv3 --pmc CSVs (one counter set per pass) into
 profiles/pmc_summary.json: per render call, the per-dispatch means of every
-render kernel (the general k_render_fast and, on two-class launches, the
-lean-pixel k_render_lean — one dispatch each per call) summed over the
+render kernel (two-class launches: the lean-pixel k_render_lean and the
+batched general k_render_gen or the general k_render_fast — one dispatch
+each per call) summed over the
 kernels, plus the per-kernel means.
 
 HBM bytes per launch = (2 * FETCH_SIZE + WRITE_SIZE) * 1024: FETCH_SIZE and
@@ -18,7 +19,7 @@ import re
 import sys
 
 # the render call's kernels (a regex on the kernel name)
-KERNEL = r"k_render_fast<false|k_render_lean<"
+KERNEL = r"k_render_fast<false|k_render_lean<|k_render_gen<"
 
 
 def means(path, kernel=None):

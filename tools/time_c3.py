@@ -15,7 +15,8 @@ scene, W, H, m = {"C3": (scenes.mesh_bunny, 1920, 1080, 16), "C2": (scenes.boxes
                   "C5": (scenes.torus_scene, 3840, 2160, 16)}[cfg]
 ds = DeviceScene(scene())
 info = ds.info()
-opts = Options(width=W, height=H, antialias=Antialias(akGrid, m), bias=1e-4, precision=Precision.fp32)
+opts = Options(width=W, height=H, antialias=Antialias(akGrid, m), bias=1e-4, precision=Precision.fp32,
+               flags=int(os.environ.get("RTMI_FLAGS", "0"), 0))
 fb = torch.zeros(W * H * 3, dtype=torch.float32, device="cuda")
 st = ds.render_device(opts, fb, stats=True)
 ts = []
