@@ -1002,7 +1002,21 @@ template <unsigned F, int S>
 __device__ __forceinline__ void batch_dirs(KP p, const GroupPix& gp, int it0, const LdsF* tb, F3 (&d)[S],
                                            bool (&sv)[S]) {
   float px[S], py[S];
-  if (p->aa_kind == 1 && p->log2_grid_m >= 0) {
+  if (p->aa_kind == 1 && p->log2_grid_m >= 0 && p->log2_grid_m <= 6) {
+    // m divides 64: sample s = it * 64 + sub keeps the lane's column
+    // s & (m-1) = sub & (m-1) in every iteration — px (and the camera ray's
+    // cx) once per batch, the same values as per sample
+    const int mm = p->grid_m - 1, lg = p->log2_grid_m;
+    const float st = p->sample_step, of = p->sample_off;
+    const float pxl = (float)gp.x + __builtin_fmaf((float)(gp.sub & mm), st, of);
+#pragma unroll
+    for (int k = 0; k < S; ++k) {
+      const int s = (it0 + k) * 64 + gp.sub;
+      sv[k] = gp.valid && s < p->spp;
+      px[k] = pxl;
+      py[k] = (float)gp.y + __builtin_fmaf((float)(s >> lg), st, of);
+    }
+  } else if (p->aa_kind == 1 && p->log2_grid_m >= 0) {
     const int mm = p->grid_m - 1, lg = p->log2_grid_m;
     const float st = p->sample_step, of = p->sample_off;
 #pragma unroll
@@ -1073,16 +1087,27 @@ __device__ __forceinline__ void lean_batch(KP p, const GroupPix& gp, int it0, co
   }
   ws.v[STAT_PRIMARY] += nprim;
   const int nobj = p->nobj, mesh = p->shadow_mesh;
+#ifndef RTMI_LEAN_NOPIN
+  // the record arrays' bases pinned in SGPRs for the batch (opaque): the
+  // compiler otherwise re-reads them from the kernel arguments before every
+  // object / light visit, a dependent scalar load in front of the record's
+  const FObj* objs = p->objs;
+  const FLight* lights = p->lights;
+  asm volatile("" : "+s"(objs), "+s"(lights));
+#else
+  const FObj* objs = p->objs;
+  const FLight* lights = p->lights;
+#endif
   unsigned hitl = 0u;
   for (int i = 0; i < nobj; ++i) {
     if (i == mesh) continue;
-    const FObj ob = at(p->objs, i);
+    const FObj ob = at(objs, i);
 #pragma unroll
     for (int k = 0; k < S; ++k) {
+      // trace's rule (t >= 0 ? t : inf) < th, as two compares (th <= inf)
       const float t = analytic_t<F>(p, ob, i, o, d[k]);
-      const float tp = t >= 0.0f ? t : finf();
-      const bool c = tp < th[k];
-      th[k] = c ? tp : th[k];
+      const bool c = t >= 0.0f && t < th[k];
+      th[k] = c ? t : th[k];
       hob[k] = c ? i : hob[k];
       hitl += c ? 1u : 0u;
     }
@@ -1099,16 +1124,42 @@ __device__ __forceinline__ void lean_batch(KP p, const GroupPix& gp, int it0, co
     so[k] = f3(__builtin_fmaf(d[k].x, th[k], o.x), __builtin_fmaf(d[k].y, th[k], o.y),
                __builtin_fmaf(d[k].z, th[k], o.z));  // the hit point until N is known
   }
+  // every analytic object a plane (the mesh + plane subsets): a plane's
+  // normal does not depend on the hit point, so with ONE object hit by the
+  // batch's lit samples (the usual ground pixel) N and each light's N.L
+  // are wave-uniform — formed once, the same values as per sample
+  constexpr bool kPlanesOnly = !(F & (F_SPHERE | F_BOX));
+  int nhobj = 0;
+  F3 Nu = f3(0.0f, 0.0f, 0.0f);
   for (;;) {
     int oi = -1;
 #pragma unroll
     for (int k = S - 1; k >= 0; --k)
       if (pend[k]) oi = __builtin_amdgcn_readlane(hob[k], (int)__builtin_ctzll(pend[k]));
     if (oi < 0) break;
+    ++nhobj;
     int oi_cmp = oi;
     asm volatile("" : "+s"(oi_cmp));
-    const FObj ob = at(p->objs, oi);
+    const FObj ob = at(objs, oi);
     const RT_CONST FObjX& ox = at(p->objx, oi);
+    if constexpr (kPlanesOnly) {
+      F3 n = f3(0.0f, 1.0f, 0.0f);  // Plane normal (geom.nim:365-366)
+      if ((F & F_XF_GENERAL) && ob.xf == XF_GENERAL) {  // object_to_world * n, not re-normalised
+        const float* m = ox.o2w;
+        n = f3(__builtin_fmaf(m[0], n.x, __builtin_fmaf(m[3], n.y, m[6] * n.z)),
+               __builtin_fmaf(m[1], n.x, __builtin_fmaf(m[4], n.y, m[7] * n.z)),
+               __builtin_fmaf(m[2], n.x, __builtin_fmaf(m[5], n.y, m[8] * n.z)));
+      }
+      Nu = n;
+#pragma unroll
+      for (int k = 0; k < S; ++k) {
+        const unsigned long long mine = bal(hob[k] == oi_cmp) & pend[k];
+        pend[k] &= ~mine;
+        const bool mi = lane_in(mine);
+        N[k] = f3(mi ? n.x : N[k].x, mi ? n.y : N[k].y, mi ? n.z : N[k].z);
+      }
+      continue;
+    }
 #pragma unroll
     for (int k = 0; k < S; ++k) {
       const unsigned long long mine = bal(hob[k] == oi_cmp) & pend[k];
@@ -1126,6 +1177,7 @@ __device__ __forceinline__ void lean_batch(KP p, const GroupPix& gp, int it0, co
       N[k] = f3(mi ? n.x : N[k].x, mi ? n.y : N[k].y, mi ? n.z : N[k].z);
     }
   }
+  const bool uni = kPlanesOnly && nhobj == 1;
   const float bias = p->bias;
 #pragma unroll
   for (int k = 0; k < S; ++k)
@@ -1145,30 +1197,56 @@ __device__ __forceinline__ void lean_batch(KP p, const GroupPix& gp, int it0, co
 #pragma unroll
   for (int k = 0; k < S; ++k) nlit += pc(litm[k]);
   ws.v[STAT_SHADOW] += (unsigned)nl * nlit;
-  for (int li = 0; li < nl; ++li) {
-    const FLight L = at(p->lights, li);
-    const F3 sd = f3(-L.v[0], -L.v[1], -L.v[2]);
-    float ts[S];  // unlit samples start at 0 (take no part)
+  auto light_loop = [&](auto uniform) {
+    constexpr bool U = decltype(uniform)::value;
+    for (int li = 0; li < nl; ++li) {
+      const FLight L = at(lights, li);
+      const F3 sd = f3(-L.v[0], -L.v[1], -L.v[2]);
+      float ts[S];  // unlit samples start at 0 (take no part)
 #pragma unroll
-    for (int k = 0; k < S; ++k) ts[k] = lane_in(litm[k]) ? finf() : 0.0f;
-    for (int i = 0; i < nobj; ++i) {
-      if (i == mesh) continue;
-      const FObj ob = at(p->objs, i);
+      for (int k = 0; k < S; ++k) ts[k] = lane_in(litm[k]) ? finf() : 0.0f;
+      for (int i = 0; i < nobj; ++i) {
+        if (i == mesh) continue;
+        const FObj ob = at(objs, i);
+        if constexpr (kPlanesOnly) {
+          // Plane.intersect (geom.nim:240-248) of the parallel shadow rays:
+          // the direction's test and reciprocal once (a NaN multiplier for a
+          // direction parallel to the plane: no t >= 0, as -inf gives none)
+          F3 r0, rdu;
+          to_object<F>(p, ob, i, so[0], sd, r0, rdu);
+          const float mulp = fabsf(rdu.y) > 1e-6f ? rcp(rdu.y) : __builtin_nanf("");
+#pragma unroll
+          for (int k = 0; k < S; ++k) {
+            F3 ro, rd;
+            to_object<F>(p, ob, i, so[k], sd, ro, rd);
+            const float t = -ro.y * mulp;
+            const bool c = t >= 0.0f && t < ts[k];
+            ts[k] = c ? t : ts[k];
+            hitl += c ? 1u : 0u;
+          }
+        } else {
+#pragma unroll
+          for (int k = 0; k < S; ++k) {
+            const float t = analytic_t<F>(p, ob, i, so[k], sd);
+            const bool c = t >= 0.0f && t < ts[k];
+            ts[k] = c ? t : ts[k];
+            hitl += c ? 1u : 0u;
+          }
+        }
+      }
+      // unoccluded: shadeDiffuse (shader.nim:12-17)
+      const float ndl_u = U ? fmaxf(dot3(Nu, sd), 0.0f) : 0.0f;
 #pragma unroll
       for (int k = 0; k < S; ++k) {
-        const float t = analytic_t<F>(p, ob, i, so[k], sd);
-        const float tp = t >= 0.0f ? t : finf();
-        const bool c = tp < ts[k];
-        ts[k] = c ? tp : ts[k];
-        hitl += c ? 1u : 0u;
+        const bool vis = lane_in(litm[k]) && !(ts[k] < finf());
+        irr_add(E[k], L.ci, vis ? (U ? ndl_u : fmaxf(dot3(N[k], sd), 0.0f)) : 0.0f);
       }
     }
-#pragma unroll
-    for (int k = 0; k < S; ++k) {  // unoccluded: shadeDiffuse (shader.nim:12-17)
-      const bool vis = lane_in(litm[k]) && !(ts[k] < finf());
-      irr_add(E[k], L.ci, vis ? fmaxf(dot3(N[k], sd), 0.0f) : 0.0f);
-    }
-  }
+  };
+  if (uni)
+    light_loop(Bool<true>{});
+  else
+    light_loop(Bool<false>{});
   ws.v[STAT_HITS] += wave_sum(hitl);
   // albedo / pi per distinct object hit, then the samples' colours in order
   // (the sky: the background, renderer.nim:74-75)
@@ -1353,9 +1431,8 @@ __device__ __forceinline__ bool gen_batch(KP p, const GroupPix& gp, int it0, con
 #pragma unroll
     for (int k = 0; k < S; ++k) {
       const float t = analytic_t<F>(p, ob, i, o, d[k]);
-      const float tp = t >= 0.0f ? t : finf();
-      const bool c = tp < th[k];
-      th[k] = c ? tp : th[k];
+      const bool c = t >= 0.0f && t < th[k];  // (t >= 0 ? t : inf) < th, th <= inf
+      th[k] = c ? t : th[k];
       hob[k] = c ? i : hob[k];
       hitl += c ? 1u : 0u;
     }
@@ -1520,9 +1597,8 @@ __device__ __forceinline__ bool gen_batch(KP p, const GroupPix& gp, int it0, con
 #pragma unroll
       for (int k = 0; k < S; ++k) {
         const float t = analytic_t<F>(p, ob, i, so[k], sd);
-        const float tp = t >= 0.0f ? t : finf();
-        const bool c = tp < ts[k];
-        ts[k] = c ? tp : ts[k];
+        const bool c = t >= 0.0f && t < ts[k];
+        ts[k] = c ? t : ts[k];
         hitl += c ? 1u : 0u;
       }
     }
