@@ -164,6 +164,7 @@ struct rt_scene {
     std::array<int64_t, 17> key;
     DevBuf<unsigned> cost;         // cycles per pixel group, written by the measuring launch
     DevBuf<int32_t> perm;          // the expensive-first order, once built
+    std::vector<int32_t> host_perm;  // the same order on the host (two-class launches split it)
     hipEvent_t measured = nullptr; // recorded after the measuring launch
     ~Order() {
       cost.release();
@@ -173,7 +174,7 @@ struct rt_scene {
   };
   std::vector<std::unique_ptr<Order>> orders;  // most recently used first, at most 8
   struct Split {                   // one launch mapping's lean / general pixel group lists
-    std::array<int64_t, 13> key;
+    std::array<int64_t, 14> key;
     DevBuf<int32_t> lean, heavy;
     int n_lean = 0, n_heavy = 0;
     ~Split() {
@@ -1042,6 +1043,7 @@ struct OrderUse {
   const int32_t* order = nullptr;  // FastParams.order
   unsigned* cost = nullptr;        // FastParams.cost (the measuring launch)
   rt_scene::Order* entry = nullptr;
+  const std::vector<int32_t>* host_order = nullptr;  // the order on the host
 };
 
 int order_policy() {
@@ -1132,9 +1134,11 @@ OrderUse group_order(rt_scene* s, const rt_options* o, const Mapping& mp, const 
     std::vector<int32_t> perm(c.size());
     for (size_t g = 0; g < c.size(); ++g) perm[(size_t)start[bucket[g]]++] = (int32_t)g;
     if (e.perm.upload(perm) != RT_OK) return u;
+    e.host_perm.swap(perm);
     e.cost.release();
   }
   u.order = e.perm.p;
+  u.host_order = &e.host_perm;
   return u;
 }
 
@@ -1214,7 +1218,8 @@ bool sampler_in_pixel(int32_t aa_kind) {
 }
 
 void fill_fast(rt_scene* s, const rt_options* o, const Mapping& mp, float* fb, FastParams& p, int* blocks,
-               rt_scene::Order** measuring) {
+               rt_scene::Order** measuring,
+               const std::vector<int32_t>** host_order) {
   std::memset(&p, 0, sizeof p);
   p.objs = s->f32.objs.p;
   p.objx = s->f32.objx.p;
@@ -1331,6 +1336,7 @@ void fill_fast(rt_scene* s, const rt_options* o, const Mapping& mp, float* fb, F
   p.order = ou.order;
   p.cost = ou.cost;
   *measuring = ou.entry;
+  *host_order = ou.host_order;
   *blocks = pl.blocks;
 }
 
@@ -1423,12 +1429,14 @@ void fill_params(rt_scene* s, const PrecisionData<R>& pd, const rt_options* o, c
 // list (they render nothing). Lists are built per launch mapping on the
 // host from the records and cached (LRU, 8). Scheduling only: the image
 // and Stats are those of the one-kernel launch.
-rt_scene::Split* split_lists(rt_scene* s, const rt_options* o, const Mapping& mp, const FastParams& p) {
+rt_scene::Split* split_lists(rt_scene* s, const rt_options* o, const Mapping& mp, const FastParams& p,
+                             const std::vector<int32_t>* host_order) {
   if (o->flags & (RT_FLAG_NO_SPLIT | RT_FLAG_COUNT_TRAVERSAL)) return nullptr;
-  // short launches with a longest-first order (group_order) keep the one
-  // kernel: there the fixed cost of a second launch and the fork / join
-  // outweighs the lean kernel (C3 in 8 bands: 0.316 vs 0.331 ms per rank)
-  if (p.lanes_per_px != 64 || !p.pix_info || p.order || p.cost || s->nlight > 8) return nullptr;
+  // a short launch with a longest-first order (group_order: a multi-GPU
+  // rank's band set) keeps that order within each list (C3 in 8 bands,
+  // rank time: one kernel in LPT order 0.316 ms)
+  if (p.lanes_per_px != 64 || !p.pix_info || p.cost || s->nlight > 8) return nullptr;
+  if (p.order && (!host_order || (long long)host_order->size() != (long long)p.ngroups)) return nullptr;
   const unsigned sub = f32_subset(s, o);
   if (rtmi_lean_f32_blocks_per_cu(sub, f32_table_lds(o)) <= 0) return nullptr;
   rt_scene::PixelBins* pb = s->pixel_bins.empty() ? nullptr : s->pixel_bins[0].get();
@@ -1438,8 +1446,9 @@ rt_scene::Split* split_lists(rt_scene* s, const rt_options* o, const Mapping& mp
   const std::vector<uint32_t>& host_info = pb->records[0]->host;
   int64_t bias_bits;
   std::memcpy(&bias_bits, &o->bias, sizeof bias_bits);
-  const std::array<int64_t, 13> key = {o->width, o->height, bias_bits, mp.mode, mp.y0,   mp.nrows, mp.ncols,
-                                       mp.step,  mp.max_step, mp.band_h, mp.rank, mp.world, s->nlight};
+  const std::array<int64_t, 14> key = {o->width,   o->height,  bias_bits, mp.mode,  mp.y0,    mp.nrows, mp.ncols,
+                                       mp.step,    mp.max_step, mp.band_h, mp.rank, mp.world, s->nlight,
+                                       p.order ? 1 : 0};
   size_t i = 0;
   while (i < s->splits.size() && s->splits[i]->key != key) ++i;
   if (i < s->splits.size()) {
@@ -1448,7 +1457,8 @@ rt_scene::Split* split_lists(rt_scene* s, const rt_options* o, const Mapping& mp
   }
   const uint32_t full = (1u << s->nlight) - 1u;
   std::vector<int32_t> lean, heavy;
-  for (int64_t g = 0; g < (int64_t)p.ngroups; ++g) {  // group_pixel (rt_fast.h) for one-pixel groups
+  for (int64_t gi = 0; gi < (int64_t)p.ngroups; ++gi) {  // group_pixel (rt_fast.h) for one-pixel groups
+    const int64_t g = p.order ? (int64_t)(*host_order)[(size_t)gi] : gi;
     const int k = (int)(g / mp.ncols), j = (int)(g % mp.ncols);
     const int x = j * mp.step;
     int y;
@@ -1501,7 +1511,8 @@ int launch(rt_scene* s, const rt_options* o, const Mapping& mp, float* d_out, hi
   } else {
     FastParams p;
     rt_scene::Order* measuring = nullptr;
-    fill_fast(s, o, mp, d_out, p, &blocks, &measuring);
+    const std::vector<int32_t>* host_order = nullptr;
+    fill_fast(s, o, mp, d_out, p, &blocks, &measuring, &host_order);
     if (p.ngroups == 0) return RT_OK;
     // diagnostic (tools/cost_map.py): RTMI_COST_DUMP=<file> records every
     // pixel group's duration (s_memtime cycles) of this launch into <file>
@@ -1510,7 +1521,7 @@ int launch(rt_scene* s, const rt_options* o, const Mapping& mp, float* d_out, hi
     if (cost_dump && !measuring && !p.cost) {
       if (dbg_cost.alloc((size_t)p.ngroups) == RT_OK) p.cost = dbg_cost.p;
     }
-    rt_scene::Split* sp = (cost_dump || measuring) ? nullptr : split_lists(s, o, mp, p);
+    rt_scene::Split* sp = (cost_dump || measuring) ? nullptr : split_lists(s, o, mp, p, host_order);
     if (sp) {  // two-class launch: the general kernel on its list, then the lean kernel on its own
       const size_t shmem = f32_table_lds(o);
       const unsigned sub = f32_subset(s, o);

@@ -181,3 +181,28 @@ def test_batched_general_pixels_and_fallback(gpu):
         d2 = DeviceScene(SCENES[name]())
         d2.render_device(_opts(200, 120, 16), fb)
         assert d2.last_batch()[0] == 0, name
+
+
+def test_split_in_longest_first_launches(gpu):
+    """A multi-GPU rank's band set is a short launch: its first launch
+    measures per-group costs, later ones hand the groups out longest-first —
+    and split them into the lean and batched general lists in that order.
+    Same frames and Stats as the one-kernel launch in screen order."""
+    import torch
+    ds = DeviceScene(scenes.mesh_bunny())
+    w, h, world = 640, 360, 8
+    rows = band_rows(h, 4, world)
+    for r in (0, 5):
+        ref = torch.full((rows * w * 3,), -7.0, dtype=torch.float32, device="cuda")
+        o_ref = Options(width=w, height=h, antialias=Antialias(akGrid, 16), bias=1e-4, precision=Precision.fp32,
+                        flags=RT_FLAG_NO_SPLIT | RT_FLAG_NO_REORDER)
+        st_ref = ds.render_bands_device(o_ref, ref, 4, r, world)
+        o = Options(width=w, height=h, antialias=Antialias(akGrid, 16), bias=1e-4, precision=Precision.fp32)
+        splits = []
+        for _ in range(3):  # measuring launch, then ordered (split) launches
+            b = torch.full((rows * w * 3,), -7.0, dtype=torch.float32, device="cuda")
+            st = ds.render_bands_device(o, b, 4, r, world)
+            splits.append(ds.last_split())
+            assert st == st_ref, (r, st, st_ref)
+            assert torch.equal(b, ref), (r, float((b - ref).abs().max()))
+        assert splits[0][0] == 0 and splits[-1][0] > 0, splits

@@ -36,6 +36,8 @@ for band_h in [int(b) for b in os.environ.get("BANDS", "16,8,4").split(",")]:
                 torch.cuda.synchronize()
                 ts.append(a.elapsed_time(b))
             per.append(sorted(ts)[len(ts) // 2])
+            if rank == 0:
+                res[f"world{world}_split"] = list(ds.last_split())
         res[f"world{world}_max_ms"] = round(max(per), 3)
         res[f"world{world}_mean_ms"] = round(sum(per) / world, 3)
     res["render_speedup_8"] = round(res["world1_max_ms"] / res["world8_max_ms"], 2)
