@@ -994,6 +994,18 @@ __device__ __forceinline__ F3 camera_dir(KP p, const GroupPix& gp, int s, const 
   return camera_ray_dir(p, px, py);
 }
 
+// The object of the lowest pending lane of the lowest pending sample (-1:
+// none). A branch per sample: the branch-free form (a readlane per sample,
+// scalar selects) measured 5 % slower on C3.
+template <int S>
+__device__ __forceinline__ int first_pending(const unsigned long long (&pend)[S], const int (&hob)[S]) {
+  int oi = -1;
+#pragma unroll
+  for (int k = S - 1; k >= 0; --k)
+    if (pend[k]) oi = __builtin_amdgcn_readlane(hob[k], (int)__builtin_ctzll(pend[k]));
+  return oi;
+}
+
 // Sample positions of a batch (S samples per lane: iterations it0 .. it0+S-1
 // of a one-pixel wave) and their camera-ray directions; akGrid with m a
 // power of two (C2-C5) as s = (s & (m-1), s >> log2 m), the sampler decided
@@ -1002,6 +1014,9 @@ template <unsigned F, int S>
 __device__ __forceinline__ void batch_dirs(KP p, const GroupPix& gp, int it0, const LdsF* tb, F3 (&d)[S],
                                            bool (&sv)[S]) {
   float px[S], py[S];
+  // validity without short-circuit branches (a per-lane && became an
+  // exec-mask branch with the argument load inside, per sample)
+  const int spp = p->spp;
   if (p->aa_kind == 1 && p->log2_grid_m >= 0 && p->log2_grid_m <= 6) {
     // m divides 64: sample s = it * 64 + sub keeps the lane's column
     // s & (m-1) = sub & (m-1) in every iteration — px (and the camera ray's
@@ -1012,7 +1027,7 @@ __device__ __forceinline__ void batch_dirs(KP p, const GroupPix& gp, int it0, co
 #pragma unroll
     for (int k = 0; k < S; ++k) {
       const int s = (it0 + k) * 64 + gp.sub;
-      sv[k] = gp.valid && s < p->spp;
+      sv[k] = gp.valid & (s < spp);
       px[k] = pxl;
       py[k] = (float)gp.y + __builtin_fmaf((float)(s >> lg), st, of);
     }
@@ -1022,7 +1037,7 @@ __device__ __forceinline__ void batch_dirs(KP p, const GroupPix& gp, int it0, co
 #pragma unroll
     for (int k = 0; k < S; ++k) {
       const int s = (it0 + k) * 64 + gp.sub;
-      sv[k] = gp.valid && s < p->spp;
+      sv[k] = gp.valid & (s < spp);
       px[k] = (float)gp.x + __builtin_fmaf((float)(s & mm), st, of);
       py[k] = (float)gp.y + __builtin_fmaf((float)(s >> lg), st, of);
     }
@@ -1030,8 +1045,8 @@ __device__ __forceinline__ void batch_dirs(KP p, const GroupPix& gp, int it0, co
 #pragma unroll
     for (int k = 0; k < S; ++k) {
       const int s = (it0 + k) * 64 + gp.sub;
-      sv[k] = gp.valid && s < p->spp;
-      camera_pos<F>(p, gp, s < p->spp ? s : 0, tb, px[k], py[k]);
+      sv[k] = gp.valid & (s < spp);
+      camera_pos<F>(p, gp, s < spp ? s : 0, tb, px[k], py[k]);
     }
   }
 #pragma unroll
@@ -1099,8 +1114,14 @@ __device__ __forceinline__ void lean_batch(KP p, const GroupPix& gp, int it0, co
   const FLight* lights = p->lights;
 #endif
   unsigned hitl = 0u;
-  for (int i = 0; i < nobj; ++i) {
-    if (i == mesh) continue;
+  // the analytic objects in scene order
+  // (one loop with a skip test: two index ranges around the mesh measured
+  // 2 % slower, the loop body compiled twice)
+  auto analytic_objects = [&](auto&& body) {
+    for (int i = 0; i < nobj; ++i)
+      if (i != mesh) body(i);
+  };
+  analytic_objects([&](const int i) {
     const FObj ob = at(objs, i);
 #pragma unroll
     for (int k = 0; k < S; ++k) {
@@ -1111,7 +1132,7 @@ __device__ __forceinline__ void lean_batch(KP p, const GroupPix& gp, int it0, co
       hob[k] = c ? i : hob[k];
       hitl += c ? 1u : 0u;
     }
-  }
+  });
   // shade (renderer.nim:71-127): normals per distinct object hit, the shadow
   // origins hitW + N * bias. A hit has t < inf (it beat the initial limit).
   unsigned long long litm[S], pend[S];
@@ -1130,12 +1151,9 @@ __device__ __forceinline__ void lean_batch(KP p, const GroupPix& gp, int it0, co
   // are wave-uniform — formed once, the same values as per sample
   constexpr bool kPlanesOnly = !(F & (F_SPHERE | F_BOX));
   int nhobj = 0;
-  F3 Nu = f3(0.0f, 0.0f, 0.0f);
+  F3 Nu = f3(0.0f, 0.0f, 0.0f), alb_u = f3(0.0f, 0.0f, 0.0f);
   for (;;) {
-    int oi = -1;
-#pragma unroll
-    for (int k = S - 1; k >= 0; --k)
-      if (pend[k]) oi = __builtin_amdgcn_readlane(hob[k], (int)__builtin_ctzll(pend[k]));
+    const int oi = first_pending<S>(pend, hob);
     if (oi < 0) break;
     ++nhobj;
     int oi_cmp = oi;
@@ -1151,6 +1169,7 @@ __device__ __forceinline__ void lean_batch(KP p, const GroupPix& gp, int it0, co
                __builtin_fmaf(m[2], n.x, __builtin_fmaf(m[5], n.y, m[8] * n.z)));
       }
       Nu = n;
+      alb_u = f3(ox.albedo_pi[0], ox.albedo_pi[1], ox.albedo_pi[2]);
 #pragma unroll
       for (int k = 0; k < S; ++k) {
         const unsigned long long mine = bal(hob[k] == oi_cmp) & pend[k];
@@ -1205,8 +1224,7 @@ __device__ __forceinline__ void lean_batch(KP p, const GroupPix& gp, int it0, co
       float ts[S];  // unlit samples start at 0 (take no part)
 #pragma unroll
       for (int k = 0; k < S; ++k) ts[k] = lane_in(litm[k]) ? finf() : 0.0f;
-      for (int i = 0; i < nobj; ++i) {
-        if (i == mesh) continue;
+      analytic_objects([&](const int i) {
         const FObj ob = at(objs, i);
         if constexpr (kPlanesOnly) {
           // Plane.intersect (geom.nim:240-248) of the parallel shadow rays:
@@ -1233,7 +1251,7 @@ __device__ __forceinline__ void lean_batch(KP p, const GroupPix& gp, int it0, co
             hitl += c ? 1u : 0u;
           }
         }
-      }
+      });
       // unoccluded: shadeDiffuse (shader.nim:12-17)
       const float ndl_u = U ? fmaxf(dot3(Nu, sd), 0.0f) : 0.0f;
 #pragma unroll
@@ -1248,27 +1266,33 @@ __device__ __forceinline__ void lean_batch(KP p, const GroupPix& gp, int it0, co
   else
     light_loop(Bool<false>{});
   ws.v[STAT_HITS] += wave_sum(hitl);
-  // albedo / pi per distinct object hit, then the samples' colours in order
-  // (the sky: the background, renderer.nim:74-75)
-#pragma unroll
-  for (int k = 0; k < S; ++k) pend[k] = litm[k];
-  for (;;) {
-    int oi = -1;
-#pragma unroll
-    for (int k = S - 1; k >= 0; --k)
-      if (pend[k]) oi = __builtin_amdgcn_readlane(hob[k], (int)__builtin_ctzll(pend[k]));
-    if (oi < 0) break;
-    int oi_cmp = oi;
-    asm volatile("" : "+s"(oi_cmp));
-    const RT_CONST FObjX& ox = at(p->objx, oi);
-    const F3 alb = f3(ox.albedo_pi[0], ox.albedo_pi[1], ox.albedo_pi[2]);
+  // albedo / pi per distinct object hit (one object: from the normal pass),
+  // then the samples' colours in order
+  if (uni) {
 #pragma unroll
     for (int k = 0; k < S; ++k) {
-      const unsigned long long mine = bal(hob[k] == oi_cmp) & pend[k];
-      pend[k] &= ~mine;
-      const F3 a = mul3(alb, E[k]);
-      const bool mi = lane_in(mine);
+      const F3 a = mul3(alb_u, E[k]);
+      const bool mi = lane_in(litm[k]);
       E[k] = f3(mi ? a.x : E[k].x, mi ? a.y : E[k].y, mi ? a.z : E[k].z);
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < S; ++k) pend[k] = litm[k];
+    for (;;) {
+      const int oi = first_pending<S>(pend, hob);
+      if (oi < 0) break;
+      int oi_cmp = oi;
+      asm volatile("" : "+s"(oi_cmp));
+      const RT_CONST FObjX& ox = at(p->objx, oi);
+      const F3 alb = f3(ox.albedo_pi[0], ox.albedo_pi[1], ox.albedo_pi[2]);
+#pragma unroll
+      for (int k = 0; k < S; ++k) {
+        const unsigned long long mine = bal(hob[k] == oi_cmp) & pend[k];
+        pend[k] &= ~mine;
+        const F3 a = mul3(alb, E[k]);
+        const bool mi = lane_in(mine);
+        E[k] = f3(mi ? a.x : E[k].x, mi ? a.y : E[k].y, mi ? a.z : E[k].z);
+      }
     }
   }
   const F3 bg = f3(p->bg[0], p->bg[1], p->bg[2]);
@@ -1306,12 +1330,15 @@ __device__ __forceinline__ void tri_test_t(const RT_CONST TriFast& T, F3 o, F3 d
 // whose bit is set in fl (wave-uniform), each face record fetched once for
 // all of them. Camera rays (KEY): list_search's (t, face) key. Shadow rays
 // (!KEY): tri_test_t and the exact early exit (a sample's lane retires once
-// it holds a hit with t <= stop; the search ends when no lane of a listed
-// sample is left).
+// it holds a hit with t <= stop; the search ends when no lane the list is
+// for — own[k], the lanes whose ray lies in this cell — is left: the other
+// lanes test these faces only as a harmless superset, their own cell is
+// searched in its turn).
 template <int S, bool KEY>
 __device__ __forceinline__ void list_search_batch(KP p, const int32_t* ent, int b, int e, unsigned fl,
                                                   const F3 (&ro)[S], const F3 (&rd)[S], const float (&stop)[S],
-                                                  unsigned long long (&key)[S], float (&best)[S], float (&tc)[S]) {
+                                                  const unsigned long long (&own)[S], unsigned long long (&key)[S],
+                                                  float (&best)[S], float (&tc)[S]) {
   for (int k0 = b; k0 < e; k0 += 4) {
     const RT_CONST int32_t* q = cp(ent) + k0;
     const int r[4] = {q[0], q[1], q[2], q[3]};
@@ -1332,7 +1359,7 @@ __device__ __forceinline__ void list_search_batch(KP p, const int32_t* ent, int 
       for (int k = 0; k < S; ++k)
         if ((fl >> k) & 1u) {
           tc[k] = tc[k] <= stop[k] ? -1.0f : tc[k];
-          left |= bal(tc[k] >= 0.0f);
+          left |= bal(tc[k] >= 0.0f) & own[k];
         }
       if (left == 0ull) break;
     }
@@ -1399,10 +1426,13 @@ __device__ __forceinline__ bool gen_batch(KP p, const GroupPix& gp, int it0, con
       // an empty pixel list: no camera ray of the pixel can hit the mesh
       // (trace's no_mesh: the gate's verdict cannot matter)
       if ((pinfo & kPixCount) == 0u || ob.root < 0) continue;
+#ifdef RTMI_DIAG_GEN_NOCAM
+      continue;  // diagnostic build only (wrong images): the camera searches' share
+#endif
       F3 ro[S], rd[S];
       unsigned long long key[S], key0[S];
       float tc[S], unused[S];
-      unsigned long long anyp = 0ull;
+      unsigned long long anyp = 0ull, nomask[S];
 #pragma unroll
       for (int k = 0; k < S; ++k) {
         to_object<F>(p, ob, i, o, d[k], ro[k], rd[k]);
@@ -1411,12 +1441,13 @@ __device__ __forceinline__ bool gen_batch(KP p, const GroupPix& gp, int it0, con
         key0[k] = part ? tkey(th[k], 0u) : 0ull;
         key[k] = key0[k];
         unused[k] = 0.0f;
+        nomask[k] = 0ull;
         anyp |= bal(part);
       }
       if (anyp != 0ull) {  // the wave's one pixel: one list for every sample
         const int pu = __builtin_amdgcn_readfirstlane(gp.y * p->width + gp.x);
         list_search_batch<S, true>(p, p->pix_ent, cp(p->pix_off)[pu], cp(p->pix_off)[pu + 1], (1u << S) - 1u, ro, rd,
-                                   unused, key, unused, tc);
+                                   unused, nomask, key, unused, tc);
       }
 #pragma unroll
       for (int k = 0; k < S; ++k) {  // found => 0 <= t < th: the hit counts (trace's update rule)
@@ -1451,10 +1482,7 @@ __device__ __forceinline__ bool gen_batch(KP p, const GroupPix& gp, int it0, con
                __builtin_fmaf(d[k].z, th[k], o.z));  // the hit point until N is known
   }
   for (;;) {
-    int oi = -1;
-#pragma unroll
-    for (int k = S - 1; k >= 0; --k)
-      if (pend[k]) oi = __builtin_amdgcn_readlane(hob[k], (int)__builtin_ctzll(pend[k]));
+    const int oi = first_pending<S>(pend, hob);
     if (oi < 0) break;
     int oi_cmp = oi;
     asm volatile("" : "+s"(oi_cmp));
@@ -1518,6 +1546,9 @@ __device__ __forceinline__ bool gen_batch(KP p, const GroupPix& gp, int it0, con
       const FObj ob = at(p->objs, i);
       if (i == mesh) {
         if ((li < 8 && ((skipw >> li) & 1u) != 0u) || ob.root < 0) continue;
+#ifdef RTMI_DIAG_GEN_NOSHADOW
+        continue;  // diagnostic build only (wrong images): the shadow searches' share
+#endif
         F3 ro[S], rd[S];
         unsigned long long pm[S], anyp = 0ull;
 #pragma unroll
@@ -1527,6 +1558,9 @@ __device__ __forceinline__ bool gen_batch(KP p, const GroupPix& gp, int it0, con
           anyp |= pm[k];
         }
         if (anyp == 0ull) continue;  // no lane enters the mesh's box
+#ifdef RTMI_DIAG_GEN_NOSHADOWSEARCH
+        continue;  // diagnostic build only (wrong images): the gated shadow searches' share
+#endif
         if (!p->grids || p->grids[li].gu <= 0) return false;  // the BVH: the caller's one-sample loop
         // mesh_search: the exact early exit's stop distance (the analytic
         // objects after the mesh), clamped below each lane's initial limit
@@ -1569,22 +1603,30 @@ __device__ __forceinline__ bool gen_batch(KP p, const GroupPix& gp, int it0, con
         const int32_t* bent = p->grid_ent + G.ent_base;
         // every distinct cell of the batch's shadow rays in turn (each round
         // retires at least the lane the cell was taken from)
+#ifdef RTMI_DIAG_GEN_COUNT
+        wi.v[STAT_LANE_NODES] += 1u;  // diagnostic: searched (light, batch) visits
+#endif
         while (left != 0ull) {
           int kb = -1;
 #pragma unroll
           for (int k = S - 1; k >= 0; --k)
             if (todo[k]) kb = __builtin_amdgcn_readlane(cell[k], (int)__builtin_ctzll(todo[k]));
           unsigned fl = 0u;
+          unsigned long long own[S];
           left = 0ull;
 #pragma unroll
           for (int k = 0; k < S; ++k) {
-            const unsigned long long m = bal(cell[k] == kb) & todo[k];
-            fl |= m != 0ull ? (1u << k) : 0u;
-            todo[k] &= ~m;
+            own[k] = bal(cell[k] == kb) & todo[k];
+            fl |= own[k] != 0ull ? (1u << k) : 0u;
+            todo[k] &= ~own[k];
             left |= todo[k];
           }
+#ifdef RTMI_DIAG_GEN_COUNT
+          wi.v[STAT_NODE_FETCH] += 1u;  // diagnostic: cells searched
+          wi.v[STAT_TRI_FETCH] += (unsigned)(cp(p->grid_off)[kb + 1] - cp(p->grid_off)[kb]) * (unsigned)__builtin_popcount(fl);
+#endif
           list_search_batch<S, false>(p, bent, cp(p->grid_off)[kb], cp(p->grid_off)[kb + 1], fl, ro, rd, stop,
-                                      unused, best, tc);
+                                      own, unused, best, tc);
         }
 #pragma unroll
         for (int k = 0; k < S; ++k) {  // found => 0 <= t < ts: the hit counts
@@ -1621,6 +1663,9 @@ __device__ __forceinline__ bool gen_batch(KP p, const GroupPix& gp, int it0, con
   }
   wi.v[STAT_PRIMARY] += nprim;
   wi.v[STAT_SHADOW] += (unsigned)nl * nlit;
+#ifdef RTMI_DIAG_GEN_COUNT
+  wi.v[STAT_LANE_TRIS] += 1u;  // diagnostic: batches
+#endif
   wi.v[STAT_HITS] += wave_sum(hitl);
   return true;
 }
@@ -1772,7 +1817,7 @@ __global__ __launch_bounds__(256) RTMI_OCC void k_render_fast(const FastParams p
       for (int it = it_begin; it < iters; ++it) {
         if (!decltype(lean)::value) p = params();
         const int s = it * L + gp.sub;  // this lane's sample index
-        const bool sv = gp.valid && s < p->spp;
+        const bool sv = gp.valid & (s < p->spp);
         const F3 d = camera_dir<F>(p, gp, s < p->spp ? s : 0, tb);
         const F3 o = f3(p->cam[0], p->cam[1], p->cam[2]);
         ws.v[STAT_PRIMARY] += pc(bal(sv));
@@ -1864,7 +1909,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RTMI_LEAN_W
   const int iters = p->iters;
   while (g < p->ngroups) {
     const int gg = cp(p->order)[g];
-    const GroupPix gp = group_pixel(p, gg, lane);
+    GroupPix gp = group_pixel(p, gg, lane);
+    gp.valid = true;  // the lists hold only pixels of the launch (rtmi.cpp split_lists)
     const LdsF* tb = sample_table<F>(p, gp, sample_lds, wib, 64);
     Acc acc;
     acc.v = f3(0.0f, 0.0f, 0.0f);
@@ -1926,7 +1972,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RTMI_GEN_WA
     p = params();
     const int iters = p->iters;
     const int gg = cp(p->order)[g];
-    const GroupPix gp = group_pixel(p, gg, lane_id_fresh());
+    GroupPix gp = group_pixel(p, gg, lane_id_fresh());
+    gp.valid = true;  // the lists hold only pixels of the launch (rtmi.cpp split_lists)
     const LdsF* tb = sample_table<F>(p, gp, sample_lds, wib, 64);
     // the pixel's record (every listed group is one valid pixel)
     const unsigned pinfo = at(p->pix_info, __builtin_amdgcn_readfirstlane(gp.y * p->width + gp.x));
@@ -1944,13 +1991,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RTMI_GEN_WA
       ws.v[STAT_PRIMARY] += wi.v[STAT_PRIMARY];
       ws.v[STAT_SHADOW] += wi.v[STAT_SHADOW];
       ws.v[STAT_HITS] += wi.v[STAT_HITS];
+#ifdef RTMI_DIAG_GEN_COUNT
+      for (int q = STAT_NODE_FETCH; q <= STAT_LANE_TRIS; ++q) ws.v[q] += wi.v[q];
+#endif
     } else {  // some shadow ray needs the BVH: the whole pixel by the one-sample loop
       acc.v = f3(0.0f, 0.0f, 0.0f);
       ws.v[STAT_GEN_FALLBACK] += 1u;
       for (int i2 = 0; i2 < iters; ++i2) {
         p = params();
         const int s = i2 * 64 + gp.sub;
-        const bool sv = gp.valid && s < p->spp;
+        const bool sv = gp.valid & (s < p->spp);
         const F3 d = camera_dir<F>(p, gp, s < p->spp ? s : 0, tb);
         const F3 o = f3(p->cam[0], p->cam[1], p->cam[2]);
         ws.v[STAT_PRIMARY] += pc(bal(sv));
