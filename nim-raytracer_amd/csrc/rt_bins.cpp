@@ -10,6 +10,7 @@
 #include <cstdlib>
 #include <limits>
 #include <thread>
+#include <unordered_map>
 
 namespace rtmi {
 
@@ -79,6 +80,52 @@ inline bool never_passes(double det_upper, double rd_max, double nlen) {
 // Separating-axis test of a 2D triangle against the box [x0, x1] x [y0, y1]
 // (the box axes are the caller's bounding-rectangle loop): false only when
 // one triangle edge has all four box corners strictly outside it.
+// Area of the 2D triangle q[0..5] (x, y pairs) inside the box [x0, x1] x
+// [y0, y1]: Sutherland-Hodgman against the four edges, then the shoelace.
+inline double clipped_area(const double* q, double x0, double y0, double x1, double y1) {
+  double a[16][2], b[16][2];
+  int n = 3;
+  for (int k = 0; k < 3; ++k) {
+    a[k][0] = q[2 * k];
+    a[k][1] = q[2 * k + 1];
+  }
+  // edge e: keep points with s * p[axis] <= s * lim
+  const int axis[4] = {0, 0, 1, 1};
+  const double lim[4] = {x0, x1, y0, y1}, sgn[4] = {-1.0, 1.0, -1.0, 1.0};
+  for (int ei = 0; ei < 4 && n > 0; ++ei) {
+    const int ax = axis[ei];
+    int m = 0;
+    for (int k = 0; k < n; ++k) {
+      const double* P = a[k];
+      const double* Q = a[(k + 1) % n];
+      const double dp = sgn[ei] * (P[ax] - lim[ei]), dq = sgn[ei] * (Q[ax] - lim[ei]);
+      if (dp <= 0.0) {
+        b[m][0] = P[0];
+        b[m][1] = P[1];
+        ++m;
+      }
+      if ((dp < 0.0 && dq > 0.0) || (dp > 0.0 && dq < 0.0)) {
+        const double t = dp / (dp - dq);
+        b[m][0] = P[0] + t * (Q[0] - P[0]);
+        b[m][1] = P[1] + t * (Q[1] - P[1]);
+        ++m;
+      }
+    }
+    n = m;
+    for (int k = 0; k < n; ++k) {
+      a[k][0] = b[k][0];
+      a[k][1] = b[k][1];
+    }
+  }
+  double area = 0.0;
+  for (int k = 0; k < n; ++k) {
+    const double* P = a[k];
+    const double* Q = a[(k + 1) % n];
+    area += P[0] * Q[1] - Q[0] * P[1];
+  }
+  return 0.5 * std::fabs(area);
+}
+
 inline bool tri_meets_box(const double* q, double x0, double y0, double x1, double y1) {
   const double area = (q[2] - q[0]) * (q[5] - q[1]) - (q[3] - q[1]) * (q[4] - q[0]);
   if (!(area != 0.0)) return true;  // degenerate (or NaN): keep
@@ -309,7 +356,36 @@ bool build_light_grid(const std::vector<BinTri>& tris, const double w2o[16], con
           put((size_t)r * (size_t)gu + (size_t)c, tris[i].rec);
       }
   };
-  return fill_bins((size_t)gu * (size_t)gv, tris.size(), emit, out->off, out->ent, why);
+  if (!fill_bins((size_t)gu * (size_t)gv, tris.size(), emit, out->off, out->ent, why)) return false;
+  // each cell's faces ordered by the share of the cell their projection
+  // covers, largest first: a shadow ray in the umbra meets the covering face
+  // first, and the kernels' early exit (checked after a cell's first face)
+  // retires it after one test. Order never changes a result (any order
+  // finds the same closest t; an early exit only needs some hit <= stop).
+  std::unordered_map<int32_t, int32_t> face_of;
+  face_of.reserve(tris.size());
+  for (size_t i = 0; i < tris.size(); ++i)
+    if (!std::isnan(box[4 * i])) face_of.emplace(tris[i].rec, (int32_t)i);
+  const double hc = 1.0 / ih;
+  std::vector<std::pair<double, int32_t>> row;
+  for (int r = 0; r < gv; ++r)
+    for (int c = 0; c < gu; ++c) {
+      const size_t cell = (size_t)r * (size_t)gu + (size_t)c;
+      const int32_t b = out->off[cell], e = out->off[cell + 1];
+      if (e - b < 2) continue;
+      const double cu0 = (double)g.u0 + c * hc, cv0 = (double)g.v0 + r * hc;
+      row.clear();
+      for (int32_t k = b; k < e; ++k) {
+        const int32_t rec = out->ent[(size_t)k];
+        const auto it = face_of.find(rec);
+        const double cov = it == face_of.end() ? 0.0 : clipped_area(&proj[6 * (size_t)it->second], cu0, cv0, cu0 + hc, cv0 + hc);
+        row.emplace_back(-cov, rec);
+      }
+      std::stable_sort(row.begin(), row.end(),
+                       [](const std::pair<double, int32_t>& x, const std::pair<double, int32_t>& y) { return x.first < y.first; });
+      for (int32_t k = b; k < e; ++k) out->ent[(size_t)k] = row[(size_t)(k - b)].second;
+    }
+  return true;
 }
 
 void grid_occupancy(const LightGridHost& lg, GridOcc* out) {

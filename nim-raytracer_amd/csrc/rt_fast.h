@@ -368,6 +368,12 @@ __device__ __forceinline__ void list_search(KP p, const int32_t* ent, int b, int
 #ifdef RTMI_DIAG_NOLIST
   return;  // diagnostic build only: the binned searches' share of the frame
 #endif
+  if (early && b < e) {  // a light cell's first face alone (the one covering most of the cell)
+    tri_test(*rec<TriFast>(p, cp(ent)[b]), o, d, key, tc);
+    tc = tc <= stop ? -1.0f : tc;
+    if (bal(tc >= 0.0f) == 0ull) return;
+    ++b;
+  }
   for (int k = b; k < e; k += 4) {
     const RT_CONST int32_t* q = cp(ent) + k;
     const int r0 = q[0], r1 = q[1], r2 = q[2], r3 = q[3];
@@ -1339,6 +1345,23 @@ __device__ __forceinline__ void list_search_batch(KP p, const int32_t* ent, int 
                                                   const F3 (&ro)[S], const F3 (&rd)[S], const float (&stop)[S],
                                                   const unsigned long long (&own)[S], unsigned long long (&key)[S],
                                                   float (&best)[S], float (&tc)[S]) {
+  if constexpr (!KEY) {
+    // a cell's first face alone: it is the one covering most of the cell
+    // (rt_bins.cpp), so lanes in the umbra retire after one test
+    if (b < e) {
+      const RT_CONST TriFast& T = *rec<TriFast>(p, cp(ent)[b]);
+      unsigned long long left = 0ull;
+#pragma unroll
+      for (int k = 0; k < S; ++k)
+        if ((fl >> k) & 1u) {
+          tri_test_t(T, ro[k], rd[k], best[k], tc[k]);
+          tc[k] = tc[k] <= stop[k] ? -1.0f : tc[k];
+          left |= bal(tc[k] >= 0.0f) & own[k];
+        }
+      if (left == 0ull) return;
+      ++b;
+    }
+  }
   for (int k0 = b; k0 < e; k0 += 4) {
     const RT_CONST int32_t* q = cp(ent) + k0;
     const int r[4] = {q[0], q[1], q[2], q[3]};
@@ -1773,9 +1796,10 @@ __global__ __launch_bounds__(256) RTMI_OCC void k_render_fast(const FastParams p
   qj = __builtin_amdgcn_readfirstlane(qj);
   // reservations RTMI_QUEUE_AHEAD items ahead (lane 0 holds them): the
   // atomic's round trip overlaps that many items
-  int qj_next = 0, qj_next2 = 0;
+  int qj_next = 0;
   if (__lane_id() == 0) qj_next = (int)atomicAdd(head, 1u);
 #if RTMI_QUEUE_AHEAD >= 2
+  int qj_next2 = 0;
   if (__lane_id() == 0) qj_next2 = (int)atomicAdd(head, 1u);
 #endif
   int g = qj * p->shards + shard;
