@@ -182,6 +182,12 @@ typedef struct rt_options {
  * batches at its last one and re-renders the pixel with the one-sample loop
  * (the path it takes when a shadow ray needs the BVH). Same image and Stats. */
 #define RT_FLAG_BATCH_FALLBACK 0x40u
+/* float32 kernel, two-class launches: render lean pixels with the general
+ * lean kernel. By default, in scenes whose only analytic object is one
+ * translated plane (a mesh on a ground plane) with one or two distant lights
+ * and akGrid sampling of m | 64 with spp a multiple of 256, they render in a
+ * kernel specialised for that case. Scheduling only: same image and Stats. */
+#define RT_FLAG_NO_LEAN1 0x80u
 
 /* Stats (src/renderer/stats.nim:4-13) plus ray counts for Mray/s. */
 typedef struct rt_stats {
@@ -410,6 +416,10 @@ int rt_scene_last_split(rt_scene *scene, int64_t *lean_groups, int64_t *general_
  * because a shadow ray needed the BVH (as of the last call that returned
  * Stats; -1 before any). Diagnostics for tests and the benchmark. */
 int rt_scene_last_batch(rt_scene *scene, int64_t *batched_groups, int64_t *fallback_groups);
+/* Which kernel rendered the last call's lean pixels: 0 none (no two-class
+ * launch), 1 the general lean kernel, 2 the one-plane lean kernel (see
+ * RT_FLAG_NO_LEAN1). Host-side bookkeeping, no wait. */
+int rt_scene_last_lean_kernel(rt_scene *scene, int32_t *kind);
 
 /* ---- helpers ----------------------------------------------------------- */
 

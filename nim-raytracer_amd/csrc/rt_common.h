@@ -264,6 +264,9 @@ enum : unsigned {
 };
 // float32 kernel work queue: 64 head words, 128 B apart, zeroed per launch
 constexpr int kQueueShards = 64, kQueueStride = 32;
+// k_render_lean work item: a run of this many lean-list entries (the list
+// padded with -1 to a whole number of runs), fetched with one scalar load
+constexpr int kLeanRun = 4;
 
 }  // namespace rtmi
 
@@ -274,6 +277,8 @@ int rtmi_launch_render_f64(const rtmi::RenderParams<double>* p, int blocks, void
 int rtmi_render_f32_blocks_per_cu(int count, unsigned subset, size_t shmem);
 int rtmi_launch_lean_f32(const rtmi::FastParams* p, unsigned subset, int blocks, size_t shmem, void* stream);
 int rtmi_lean_f32_blocks_per_cu(unsigned subset, size_t shmem);
+int rtmi_launch_lean1_f32(const rtmi::FastParams* p, int nl, int blocks, void* stream);
+int rtmi_lean1_f32_blocks_per_cu(int nl);
 int rtmi_launch_gen_f32(const rtmi::FastParams* p, unsigned subset, int blocks, size_t shmem, void* stream);
 int rtmi_gen_f32_blocks_per_cu(unsigned subset, size_t shmem);
 int rtmi_launch_ppm_encode(const float* fb, long long n, int bits, int srgb, void* out, void* stream);

@@ -919,14 +919,16 @@ __device__ __forceinline__ GroupPix group_pixel(KP p, int g, int lane) {
 // origin is the camera's, p->cam[0..2]). Camera constants are folded on the
 // host: ((2 x r)/w - r) f == (x - w/2) (2 r f / w), exact 0 on the centre
 // column / row as the reference's own formula gives there. Every FMA is
-// explicit, so all instances of the sample loop round alike.
+// explicit, so all instances of the sample loop round alike. The cx terms
+// are innermost: a lane whose samples share a column (akGrid, m | 64) forms
+// them once per pixel (k_render_lean1) with the same roundings.
 __device__ __forceinline__ F3 camera_ray_dir(KP p, float px, float py) {
   const float cx = (px - p->cam_b) * p->cam_a;
   const float cy = (p->cam_d - py) * p->cam_c;
-  const float rl = rsq(__builtin_fmaf(cx, cx, __builtin_fmaf(cy, cy, 1.0f)));
-  return f3(__builtin_fmaf(cx, p->cam[3], __builtin_fmaf(cy, p->cam[6], -p->cam[9])) * rl,
-            __builtin_fmaf(cx, p->cam[4], __builtin_fmaf(cy, p->cam[7], -p->cam[10])) * rl,
-            __builtin_fmaf(cx, p->cam[5], __builtin_fmaf(cy, p->cam[8], -p->cam[11])) * rl);
+  const float rl = rsq(__builtin_fmaf(cy, cy, __builtin_fmaf(cx, cx, 1.0f)));
+  return f3(__builtin_fmaf(cy, p->cam[6], __builtin_fmaf(cx, p->cam[3], -p->cam[9])) * rl,
+            __builtin_fmaf(cy, p->cam[7], __builtin_fmaf(cx, p->cam[4], -p->cam[10])) * rl,
+            __builtin_fmaf(cy, p->cam[8], __builtin_fmaf(cx, p->cam[5], -p->cam[11])) * rl);
 }
 
 // Sum of a per-lane count over the wave (DPP row sums, then the rows).
@@ -1931,24 +1933,185 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RTMI_LEAN_W
   int g = qj * p->shards + shard;
   int nflush = 0;
   const int iters = p->iters;
+  // a work item is a run of kLeanRun list entries (p->ngroups counts runs;
+  // the host pads the list with -1): one dequeue and one scalar load per
+  // run, and the next run's entries are loaded while this run renders (the
+  // per-item dequeue + dependent list read measured ~40 % of an all-lean
+  // frame with one pixel per item)
+  static_assert(kLeanRun == 4, "a run is one s_load_dwordx4");
+  using Run = int32_t __attribute__((ext_vector_type(4)));
+  const RT_CONST Run* runs = (const RT_CONST Run*)cp(p->order);
+  Run ent = g < p->ngroups ? runs[g] : Run{-1, -1, -1, -1};
   while (g < p->ngroups) {
-    const int gg = cp(p->order)[g];
-    GroupPix gp = group_pixel(p, gg, lane);
-    gp.valid = true;  // the lists hold only pixels of the launch (rtmi.cpp split_lists)
-    const LdsF* tb = sample_table<F>(p, gp, sample_lds, wib, 64);
-    Acc acc;
-    acc.v = f3(0.0f, 0.0f, 0.0f);
-    int it = 0;
-    for (; it + kLeanBatch <= iters; it += kLeanBatch) lean_batch<F, kLeanBatch>(p, gp, it, tb, acc, ws);
-    for (; it < iters; ++it) lean_batch<F, 1>(p, gp, it, tb, acc, ws);
-    finish_item(p, gp, acc.v, 64);
+    qj = __builtin_amdgcn_readfirstlane(qj_next);
+    if (lane == 0) qj_next = (int)atomicAdd(head, 1u);
+    const int gn = qj * p->shards + shard;
+    const Run ent_next = gn < p->ngroups ? runs[gn] : Run{-1, -1, -1, -1};
+#pragma unroll 1
+    for (int r = 0; r < kLeanRun; ++r) {
+      const int gg = ent.x;  // the entries shift down (static swizzles, no indexed SGPR access)
+      ent = Run{ent.y, ent.z, ent.w, -1};
+      if (gg < 0) break;  // padding: the list's last run
+      GroupPix gp = group_pixel(p, gg, lane);
+      gp.valid = true;  // the lists hold only pixels of the launch (rtmi.cpp split_lists)
+      const LdsF* tb = sample_table<F>(p, gp, sample_lds, wib, 64);
+      Acc acc;
+      acc.v = f3(0.0f, 0.0f, 0.0f);
+      int it = 0;
+      for (; it + kLeanBatch <= iters; it += kLeanBatch) lean_batch<F, kLeanBatch>(p, gp, it, tb, acc, ws);
+      for (; it < iters; ++it) lean_batch<F, 1>(p, gp, it, tb, acc, ws);
+      finish_item(p, gp, acc.v, 64);
+    }
     if (++nflush >= p->stat_flush) {
       flush_stats(ws, lds_tot[wib], lane);
       nflush = 0;
     }
+    ent = ent_next;
+    g = gn;
+  }
+  flush_stats(ws, lds_tot[wib], lane);
+  const int wave = (int)(blockIdx.x * (blockDim.x >> 6) + threadIdx.x / 64u);
+  if (lane < kStatSlots) p->partials[(size_t)wave * kStatSlots + lane] = lds_tot[wib][lane];
+}
+
+// Lean pixels of a scene whose only analytic object is one plane (C3-C5: the
+// mesh on a ground plane), every transform a translation, NL distant lights
+// (1 or 2), akGrid with m | 64 and spp a multiple of 64 (every sample valid,
+// a lane's samples share one column) — rtmi.cpp lean1_ok decides. The same
+// per-sample arithmetic as lean_batch's uniform single-plane case, with what
+// that case leaves wave-uniform or per lane formed once:
+//  * the camera ray needs only its y direction (the plane test, the hit
+//    point's height); the cx terms of camera_ray_dir are per lane and pixel;
+//  * a plane's normal is (0, 1, 0), so every lit sample of the pixel has the
+//    same N, N.L per light and albedo: shadeDiffuse's term per light is one
+//    select of a uniform value, the colour lit ? albedo x E : background;
+//  * "t >= 0 and below the running limit" is, against a first (and only)
+//    object, one class test of t (finite, >= 0 incl. -0);
+//  * sample validity, object dispatch, the mesh skip and the per-object
+//    loops are gone (one plane, all samples valid).
+// Frames and Stats bit-identical to k_render_lean / k_render_fast
+// (tests/test_gpu_split.py, RT_FLAG_NO_LEAN1).
+// "t >= 0 and below the running limit" against a first object (limit
+// +inf): ordered t >= 0 and t < +inf, as two compares straight to a mask
+__device__ __forceinline__ unsigned long long m_hit0(float t) { return m_ge(t, 0.0f) & m_lt(t, finf()); }
+template <int NL>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k_render_lean1(
+    const FastParams params_by_value) {
+  (void)params_by_value;
+  constexpr int S = 4;  // samples per lane per batch: the host requires iters % 4 == 0
+  const KP p = params();
+  __shared__ unsigned long long lds_tot[4][kStatSlots];
+  const int wib = (int)(threadIdx.x >> 6);
+  const int lane = (int)__lane_id();
+  if (lane < kStatSlots) lds_tot[wib][lane] = 0ull;
+  Stats32 ws;
+#pragma unroll
+  for (int k = 0; k < kStatSlots; ++k) ws.v[k] = 0u;
+  const int shard = (int)(blockIdx.x % (unsigned int)p->shards);
+  unsigned int* head = p->queue + shard * kQueueStride;
+  int qj = 0;
+  if (lane == 0) qj = (int)atomicAdd(head, 1u);
+  qj = __builtin_amdgcn_readfirstlane(qj);
+  int qj_next = 0;
+  if (lane == 0) qj_next = (int)atomicAdd(head, 1u);
+  int g = qj * p->shards + shard;
+  int nflush = 0;
+  const int iters = p->iters;
+  // the scene's one analytic object (the other is the mesh): a plane whose
+  // world -> object transform is a translation
+  const int po = p->shadow_mesh == 0 ? 1 : 0;
+  const FObj pl = at(p->objs, po);
+  const RT_CONST FObjX& plx = at(p->objx, po);
+  const float nroy = -(p->cam[1] + pl.t[1]);  // -(camera origin in plane space).y: Plane.intersect's -o.y
+  const float ty = pl.t[1], oy = p->cam[1], bias = p->bias;
+  // per light: the parallel shadow rays' plane reciprocal (a NaN multiplier
+  // when parallel: no t >= 0), N.L with N = (0, 1, 0) (dot3's roundings), ci
+  float mulp[NL], ndl[NL], ci[NL][3];
+#pragma unroll
+  for (int l = 0; l < NL; ++l) {
+    const FLight L = at(p->lights, l);
+    const F3 sd = f3(-L.v[0], -L.v[1], -L.v[2]);
+    mulp[l] = fabsf(sd.y) > 1e-6f ? rcp(sd.y) : __builtin_nanf("");
+    ndl[l] = fmaxf(dot3(f3(0.0f, 1.0f, 0.0f), sd), 0.0f);
+    ci[l][0] = L.ci[0];
+    ci[l][1] = L.ci[1];
+    ci[l][2] = L.ci[2];
+  }
+  const F3 alb = f3(plx.albedo_pi[0], plx.albedo_pi[1], plx.albedo_pi[2]);
+  const F3 bg = f3(p->bg[0], p->bg[1], p->bg[2]);
+  const int mm = p->grid_m - 1, lg = p->log2_grid_m;
+  const float st = p->sample_step, of = p->sample_off;
+  static_assert(kLeanRun == 4, "a run is one s_load_dwordx4");
+  using Run = int32_t __attribute__((ext_vector_type(4)));
+  const RT_CONST Run* runs = (const RT_CONST Run*)cp(p->order);
+  Run ent = g < p->ngroups ? runs[g] : Run{-1, -1, -1, -1};
+  while (g < p->ngroups) {
     qj = __builtin_amdgcn_readfirstlane(qj_next);
     if (lane == 0) qj_next = (int)atomicAdd(head, 1u);
-    g = qj * p->shards + shard;
+    const int gn = qj * p->shards + shard;
+    const Run ent_next = gn < p->ngroups ? runs[gn] : Run{-1, -1, -1, -1};
+#pragma unroll 1
+    for (int r = 0; r < kLeanRun; ++r) {
+      const int gg = ent.x;
+      ent = Run{ent.y, ent.z, ent.w, -1};
+      if (gg < 0) break;
+      GroupPix gp = group_pixel(p, gg, lane);
+      gp.valid = true;
+      // the lane's column: camera_ray_dir's cx terms, once per pixel
+      const float px = (float)gp.x + __builtin_fmaf((float)(gp.sub & mm), st, of);
+      const float cx = (px - p->cam_b) * p->cam_a;
+      const float q0 = __builtin_fmaf(cx, cx, 1.0f);
+      const float ay = __builtin_fmaf(cx, p->cam[4], -p->cam[10]);
+      const float pyb = (float)gp.y;
+      Acc acc;
+      acc.v = f3(0.0f, 0.0f, 0.0f);
+      unsigned nlit = 0u, nocc = 0u;
+#pragma unroll 1
+      for (int it0 = 0; it0 < iters; it0 += S) {
+        float soy[S];
+        unsigned long long litm[S];
+#pragma unroll
+        for (int k = 0; k < S; ++k) {
+          // castPrimaryRay's direction, y only; Plane.intersect; trace's rule
+          const int s = (it0 + k) * 64 + gp.sub;
+          const float py = pyb + __builtin_fmaf((float)(s >> lg), st, of);
+          const float cy = (p->cam_d - py) * p->cam_c;
+          const float rl = rsq(__builtin_fmaf(cy, cy, q0));
+          const float dy = __builtin_fmaf(cy, p->cam[7], ay) * rl;
+          const float t = fabsf(dy) > 1e-6f ? nroy * rcp(dy) : -finf();
+          litm[k] = m_hit0(t);  // the camera ray hits the plane: a hit, and a lit sample
+          nlit += pc(litm[k]);
+          // the shadow origin's height: hitW.y + N.y * bias (N.y = 1)
+          soy[k] = __builtin_fmaf(1.0f, bias, __builtin_fmaf(dy, t, oy));
+        }
+#pragma unroll
+        for (int k = 0; k < S; ++k) {
+          const bool lit = lane_in(litm[k]);
+          F3 E = f3(0.0f, 0.0f, 0.0f);
+#pragma unroll
+          for (int l = 0; l < NL; ++l) {
+            const float ts = -(soy[k] + ty) * mulp[l];
+            const unsigned long long occ = m_hit0(ts) & litm[k];  // the shadow ray hits the plane
+            nocc += pc(occ);
+            const float x = lane_in(litm[k] & ~occ) ? ndl[l] : 0.0f;
+            E = f3(__builtin_fmaf(ci[l][0], x, E.x), __builtin_fmaf(ci[l][1], x, E.y),
+                   __builtin_fmaf(ci[l][2], x, E.z));
+          }
+          const F3 a = mul3(alb, E);
+          acc_add3(acc, lit ? a.x : bg.x, lit ? a.y : bg.y, lit ? a.z : bg.z);
+        }
+      }
+      ws.v[STAT_PRIMARY] += (unsigned)(64 * iters);
+      ws.v[STAT_SHADOW] += (unsigned)NL * nlit;
+      ws.v[STAT_HITS] += nlit + nocc;  // camera hits (= lit samples) + shadow hits
+      finish_item(p, gp, acc.v, 64);
+    }
+    if (++nflush >= p->stat_flush) {
+      flush_stats(ws, lds_tot[wib], lane);
+      nflush = 0;
+    }
+    ent = ent_next;
+    g = gn;
   }
   flush_stats(ws, lds_tot[wib], lane);
   const int wave = (int)(blockIdx.x * (blockDim.x >> 6) + threadIdx.x / 64u);

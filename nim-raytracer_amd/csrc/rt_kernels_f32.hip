@@ -53,6 +53,9 @@ __global__ __launch_bounds__(256) void k_unshard_scalar(const float* __restrict_
 
 // the instrumented (RT_FLAG_COUNT_TRAVERSAL) kernel: all features
 template __global__ void fast::k_render_fast<true, fast::F_ALL>(const FastParams);
+// lean pixels of one-plane scenes (rtmi.cpp lean1_ok), one or two lights
+template __global__ void fast::k_render_lean1<1>(const FastParams);
+template __global__ void fast::k_render_lean1<2>(const FastParams);
 
 }  // namespace rtmi
 
@@ -116,6 +119,24 @@ extern "C" int rtmi_launch_lean_f32(const rtmi::FastParams* p, unsigned subset, 
 // Resident blocks per CU of the lean-pixel kernel; 0: no lean kernel for the subset.
 extern "C" int rtmi_lean_f32_blocks_per_cu(unsigned subset, size_t shmem) {
   return kOccupancyLean[(subset >> 3) & 15u](subset & 127u, shmem);
+}
+
+// The one-plane lean-pixel kernel for nl (1 or 2) distant lights.
+extern "C" int rtmi_launch_lean1_f32(const rtmi::FastParams* p, int nl, int blocks, void* stream) {
+  if (nl == 1)
+    hipLaunchKernelGGL(rtmi::fast::k_render_lean1<1>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, *p);
+  else if (nl == 2)
+    hipLaunchKernelGGL(rtmi::fast::k_render_lean1<2>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, *p);
+  else
+    return (int)hipErrorInvalidValue;
+  return (int)hipGetLastError();
+}
+
+extern "C" int rtmi_lean1_f32_blocks_per_cu(int nl) {
+  int nb = 0;
+  const hipError_t e = nl == 1 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, rtmi::fast::k_render_lean1<1>, 256, 0)
+                               : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, rtmi::fast::k_render_lean1<2>, 256, 0);
+  return e == hipSuccess && nb > 0 ? nb : 1;
 }
 
 extern "C" int rtmi_launch_render_f32(const rtmi::FastParams* p, unsigned subset, int blocks, size_t shmem,

@@ -144,6 +144,7 @@ struct rt_scene {
   hipStream_t aux = nullptr;
   hipEvent_t fork = nullptr, join = nullptr;
   int64_t last_lean = 0, last_general = 0;  // rt_scene_last_split
+  int32_t last_lean_kind = 0;                // rt_scene_last_lean_kernel
   int64_t last_batched = 0, last_fallback = -1;  // rt_scene_last_batch
   int32_t nobj = 0, nlight = 0, nmesh = 0;
   int32_t shadow_mesh = -1;  // the only mesh object, or -1 (FastParams.shadow_mesh)
@@ -1480,12 +1481,27 @@ rt_scene::Split* split_lists(rt_scene* s, const rt_options* o, const Mapping& mp
   e->key = key;
   e->n_lean = (int)lean.size();
   e->n_heavy = (int)heavy.size();
-  if (lean.empty()) lean.push_back(0);  // keep both allocations non-empty
+  // k_render_lean takes runs of kLeanRun entries: padded with -1
+  while (lean.size() % kLeanRun) lean.push_back(-1);
+  if (lean.empty()) lean.assign(kLeanRun, -1);  // keep both allocations non-empty
   if (heavy.empty()) heavy.push_back(0);
   if (e->lean.upload(lean) != RT_OK || e->heavy.upload(heavy) != RT_OK) return nullptr;
   s->splits.insert(s->splits.begin(), std::move(e));
   if (s->splits.size() > 8) s->splits.pop_back();
   return s->splits[0].get();
+}
+
+// k_render_lean1 (rt_fast.h) renders the lean pixels when the scene's only
+// analytic object is one plane and every transform a translation (the
+// mesh + plane feature subset, nothing else), with one or two distant lights,
+// and akGrid sampling with m | 64 whose samples fill whole 4-sample batches
+// of every lane (spp a multiple of 256): every sample is valid and a lane's
+// samples share one column. Off with RT_FLAG_NO_LEAN1.
+bool lean1_ok(const rt_scene* s, const rt_options* o, const FastParams& p, unsigned sub) {
+  return !(o->flags & RT_FLAG_NO_LEAN1) && sub == SUB_MESH && p.nobj == 2 && p.shadow_mesh >= 0 &&
+         (p.nlight == 1 || p.nlight == 2) && !p.has_point_light && p.aa_kind == RT_AA_GRID &&
+         p.log2_grid_m >= 0 && p.log2_grid_m <= 6 && p.lanes_per_px == 64 && p.spp % 256 == 0 &&
+         p.iters * 64 == p.spp && p.iters % 4 == 0 && s->nobj == 2;
 }
 
 int launch(rt_scene* s, const rt_options* o, const Mapping& mp, float* d_out, hipStream_t st) {
@@ -1504,6 +1520,7 @@ int launch(rt_scene* s, const rt_options* o, const Mapping& mp, float* d_out, hi
       p.sample_scratch = s->f64_tables.p;
     }
     s->last_lean = 0;
+    s->last_lean_kind = 0;
     s->last_general = p.ngroups;
     s->last_batched = 0;
     const int e = rtmi_launch_render_f64(&p, blocks, st);
@@ -1539,11 +1556,16 @@ int launch(rt_scene* s, const rt_options* o, const Mapping& mp, float* d_out, hi
       ph.order = sp->heavy.p;
       ph.ngroups = sp->n_heavy;
       ph.shards = std::min(kQueueShards, hb);
-      const long long lcap = (long long)rtmi_lean_f32_blocks_per_cu(sub, shmem) * s->num_cus;
+      const bool lean1 = lean1_ok(s, o, p, sub);
+      const long long lcap =
+          (long long)(lean1 ? rtmi_lean1_f32_blocks_per_cu(p.nlight) : rtmi_lean_f32_blocks_per_cu(sub, shmem)) *
+          s->num_cus;
+      const int lruns = (sp->n_lean + kLeanRun - 1) / kLeanRun;  // k_render_lean's work items
       const int lb = (int)std::max(1LL, std::min<long long>(std::min<long long>(lcap, s->max_waves / 4),
-                                                            ((long long)sp->n_lean + 3) / 4));
+                                                            ((long long)lruns + 3) / 4));
       pl.order = sp->lean.p;
-      pl.ngroups = sp->n_lean;
+      pl.ngroups = lruns;
+      pl.stat_flush = std::max(1, p.stat_flush / kLeanRun);
       pl.shards = std::min(kQueueShards, lb);
       pl.queue = s->queue.p + (size_t)kQueueShards * kQueueStride;
       pl.partials = s->partials.p + (size_t)hb * 4 * kStatSlots;
@@ -1557,7 +1579,7 @@ int launch(rt_scene* s, const rt_options* o, const Mapping& mp, float* d_out, hi
         HIP_TRY(hipStreamWaitEvent(s->aux, s->fork, 0));
       }
       int e = gen ? rtmi_launch_gen_f32(&ph, sub, hb, shmem, st) : rtmi_launch_render_f32(&ph, sub, hb, shmem, st);
-      if (!e) e = rtmi_launch_lean_f32(&pl, sub, lb, shmem, sl);
+      if (!e) e = lean1 ? rtmi_launch_lean1_f32(&pl, p.nlight, lb, sl) : rtmi_launch_lean_f32(&pl, sub, lb, shmem, sl);
       if (e) return fail(RT_E_DEVICE, "render kernel launch failed: %s", hipGetErrorString((hipError_t)e));
       if (!serial) {
         HIP_TRY(hipEventRecord(s->join, s->aux));
@@ -1565,10 +1587,12 @@ int launch(rt_scene* s, const rt_options* o, const Mapping& mp, float* d_out, hi
       }
       blocks = hb + lb;
       s->last_lean = sp->n_lean;
+      s->last_lean_kind = lean1 ? 2 : 1;
       s->last_general = sp->n_heavy;
       s->last_batched = gen ? sp->n_heavy : 0;
     } else {
       s->last_lean = 0;
+      s->last_lean_kind = 0;
       s->last_general = p.ngroups;
       s->last_batched = 0;
       const int e = rtmi_launch_render_f32(&p, f32_subset(s, o), blocks, f32_table_lds(o), st);
@@ -1778,6 +1802,13 @@ extern "C" int rt_scene_last_split(rt_scene* s, int64_t* lean_groups, int64_t* g
   std::lock_guard<std::mutex> lk(s->mu);
   *lean_groups = s->last_lean;
   *general_groups = s->last_general;
+  return RT_OK;
+}
+
+extern "C" int rt_scene_last_lean_kernel(rt_scene* s, int32_t* kind) {
+  if (!s || !kind) return fail(RT_E_INVALID, "null argument");
+  std::lock_guard<std::mutex> lk(s->mu);
+  *kind = s->last_lean_kind;
   return RT_OK;
 }
 

@@ -25,6 +25,7 @@ RT_FLAG_NO_BINNING = 0x8
 RT_FLAG_NO_SPLIT = 0x10
 RT_FLAG_NO_BATCH = 0x20
 RT_FLAG_BATCH_FALLBACK = 0x40
+RT_FLAG_NO_LEAN1 = 0x80
 RT_BVH_SAH = 0
 RT_OBJ_SLASH_INDICES = 0x1
 RT_BVH_PLOC = 1
@@ -173,6 +174,7 @@ SIGNATURES = {
     "rt_band_rows": (C.c_int, [C.c_int32, C.c_int32, C.c_int32, C.POINTER(C.c_int32)]),
     "rt_scene_last_counters": (C.c_int, [_P, C.POINTER(rt_traversal_counters)]),
     "rt_scene_last_split": (C.c_int, [_P, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
+    "rt_scene_last_lean_kernel": (C.c_int, [_P, C.POINTER(C.c_int32)]),
     "rt_scene_last_batch": (C.c_int, [_P, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
     "rt_mat4_inverse": (C.c_int, [C.POINTER(C.c_double), C.POINTER(C.c_double)]),
     "rt_load_geom": (C.c_int, [C.c_char_p, C.POINTER(C.c_int64), C.POINTER(C.c_double)]),

@@ -101,6 +101,13 @@ class DeviceScene:
         check(lib().rt_scene_last_split(self.h, C.byref(a), C.byref(b)))
         return int(a.value), int(b.value)
 
+    def last_lean_kernel(self):
+        """0: the last call had no lean-pixel kernel, 1: the general one,
+        2: the one-plane lean kernel (k_render_lean1)."""
+        k = C.c_int32()
+        check(lib().rt_scene_last_lean_kernel(self.h, C.byref(k)))
+        return int(k.value)
+
     def last_batch(self):
         """(batched, fallback) general pixel groups of the last render call:
         those the batched general kernel took, and of them those it
