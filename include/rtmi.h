@@ -188,6 +188,10 @@ typedef struct rt_options {
  * and akGrid sampling of m | 64 with spp a multiple of 256, they render in a
  * kernel specialised for that case. Scheduling only: same image and Stats. */
 #define RT_FLAG_NO_LEAN1 0x80u
+/* float32 kernel, two-class launches in the same one-plane scenes: render the
+ * general pixels with the general batched kernel instead of the one
+ * specialised for them. Scheduling only: same image and Stats. */
+#define RT_FLAG_NO_GEN1 0x100u
 
 /* Stats (src/renderer/stats.nim:4-13) plus ray counts for Mray/s. */
 typedef struct rt_stats {
@@ -416,9 +420,11 @@ int rt_scene_last_split(rt_scene *scene, int64_t *lean_groups, int64_t *general_
  * because a shadow ray needed the BVH (as of the last call that returned
  * Stats; -1 before any). Diagnostics for tests and the benchmark. */
 int rt_scene_last_batch(rt_scene *scene, int64_t *batched_groups, int64_t *fallback_groups);
-/* Which kernel rendered the last call's lean pixels: 0 none (no two-class
- * launch), 1 the general lean kernel, 2 the one-plane lean kernel (see
- * RT_FLAG_NO_LEAN1). Host-side bookkeeping, no wait. */
+/* Which kernels rendered the last call's two classes: bits 0-1 the lean
+ * pixels' (0 none — no two-class launch, 1 the general lean kernel, 2 the
+ * one-plane lean kernel, RT_FLAG_NO_LEAN1), bits 2-3 the general pixels'
+ * (0 the one-sample kernel, 1 the general batched kernel, 2 the one-plane
+ * batched kernel, RT_FLAG_NO_GEN1). Host-side bookkeeping, no wait. */
 int rt_scene_last_lean_kernel(rt_scene *scene, int32_t *kind);
 
 /* ---- helpers ----------------------------------------------------------- */

@@ -1471,8 +1471,8 @@ __device__ __forceinline__ bool gen_batch(KP p, const GroupPix& gp, int it0, con
       }
       if (anyp != 0ull) {  // the wave's one pixel: one list for every sample
         const int pu = __builtin_amdgcn_readfirstlane(gp.y * p->width + gp.x);
-        list_search_batch<S, true>(p, p->pix_ent, cp(p->pix_off)[pu], cp(p->pix_off)[pu + 1], (1u << S) - 1u, ro, rd,
-                                   unused, nomask, key, unused, tc);
+        list_search_batch<S, true>(p, p->pix_ent, cp(p->pix_off)[pu], cp(p->pix_off)[pu + 1], (1u << S) - 1u,
+                                   ro, rd, unused, nomask, key, unused, tc);
       }
 #pragma unroll
       for (int k = 0; k < S; ++k) {  // found => 0 <= t < th: the hit counts (trace's update rule)
@@ -1691,6 +1691,273 @@ __device__ __forceinline__ bool gen_batch(KP p, const GroupPix& gp, int it0, con
 #ifdef RTMI_DIAG_GEN_COUNT
   wi.v[STAT_LANE_TRIS] += 1u;  // diagnostic: batches
 #endif
+  wi.v[STAT_HITS] += wave_sum(hitl);
+  return true;
+}
+
+// General pixels of the one-plane scenes (k_render_lean1's: one mesh + one
+// translated plane, distant lights, akGrid m | 64, every sample valid):
+// gen_batch with the two objects written out in scene order instead of the
+// object / dispatch loops — the plane's camera and shadow tests in
+// k_render_lean1's form, its normal (0, 1, 0), the albedo a select of the
+// two objects' (no LDS stash), the camera's cx terms per lane and pixel.
+// The mesh searches (pixel list, light-grid cells, the early exit's stop)
+// are gen_batch's, unchanged. Returns false, before adding anything, where
+// gen_batch does (a shadow ray that needs the BVH). Frames and Stats
+// bit-identical to gen_batch (tests/test_gpu_split.py, RT_FLAG_NO_GEN1).
+template <int S, int NL>
+__device__ __forceinline__ bool gen1_batch(KP p, const GroupPix& gp, int it0, unsigned pinfo, Acc& acc,
+                                           Stats32& wi) {
+  p = params();
+  const int mesh = p->shadow_mesh, po = 1 - mesh;  // the scene's two objects
+  const F3 o = f3(p->cam[0], p->cam[1], p->cam[2]);
+  F3 d[S];
+  {
+    const int mm = p->grid_m - 1, lg = p->log2_grid_m;
+    const float st = p->sample_step, of = p->sample_off;
+    const float px = (float)gp.x + __builtin_fmaf((float)(gp.sub & mm), st, of);
+    const float cx = (px - p->cam_b) * p->cam_a;
+    const float q0 = __builtin_fmaf(cx, cx, 1.0f);
+    const float ax = __builtin_fmaf(cx, p->cam[3], -p->cam[9]), ay = __builtin_fmaf(cx, p->cam[4], -p->cam[10]),
+                az = __builtin_fmaf(cx, p->cam[5], -p->cam[11]);
+#pragma unroll
+    for (int k = 0; k < S; ++k) {  // camera_ray_dir, the cx terms formed once
+      const int s = (it0 + k) * 64 + gp.sub;
+      const float py = (float)gp.y + __builtin_fmaf((float)(s >> lg), st, of);
+      const float cy = (p->cam_d - py) * p->cam_c;
+      const float rl = rsq(__builtin_fmaf(cy, cy, q0));
+      d[k] = f3(__builtin_fmaf(cy, p->cam[6], ax) * rl, __builtin_fmaf(cy, p->cam[7], ay) * rl,
+                __builtin_fmaf(cy, p->cam[8], az) * rl);
+    }
+  }
+  float th[S];
+  bool hm[S];  // the closest hit is the mesh's
+  int htri[S];
+#pragma unroll
+  for (int k = 0; k < S; ++k) {
+    th[k] = finf();
+    hm[k] = false;
+    htri[k] = -1;
+  }
+  unsigned hitl = 0u;
+  const FObj mob = at(p->objs, mesh);
+  const float pty = at(p->objs, po).t[1];
+  // trace (renderer.nim:47-67) of the camera rays: the two objects in order
+  auto camera_plane = [&]() {
+    const float nroy = -(o.y + pty);
+#pragma unroll
+    for (int k = 0; k < S; ++k) {
+      const float t = fabsf(d[k].y) > 1e-6f ? nroy * rcp(d[k].y) : -finf();
+      const bool c = t >= 0.0f && t < th[k];
+      th[k] = c ? t : th[k];
+      hm[k] = c ? false : hm[k];
+      hitl += c ? 1u : 0u;
+    }
+  };
+  auto camera_mesh = [&]() {
+    if ((pinfo & kPixCount) == 0u || mob.root < 0) return;  // an empty pixel list: no camera ray can hit it
+    F3 ro[S], rd[S];
+    unsigned long long key[S], key0[S], anyp = 0ull, nomask[S];
+    float tc[S], unused[S];
+#pragma unroll
+    for (int k = 0; k < S; ++k) {
+      ro[k] = f3(o.x + mob.t[0], o.y + mob.t[1], o.z + mob.t[2]);
+      rd[k] = d[k];
+      const bool part = mesh_gate(mob, slab_ray(ro[k], rd[k]));
+      tc[k] = part ? th[k] : -1.0f;
+      key0[k] = part ? tkey(th[k], 0u) : 0ull;
+      key[k] = key0[k];
+      unused[k] = 0.0f;
+      nomask[k] = 0ull;
+      anyp |= bal(part);
+    }
+    if (anyp != 0ull) {
+      const KP q = params();
+      const int pu = __builtin_amdgcn_readfirstlane(gp.y * q->width + gp.x);
+      list_search_batch<S, true>(q, q->pix_ent, cp(q->pix_off)[pu], cp(q->pix_off)[pu + 1], (1u << S) - 1u,
+                                 ro, rd, unused, nomask, key, unused, tc);
+    }
+#pragma unroll
+    for (int k = 0; k < S; ++k) {
+      const bool c = key[k] != key0[k];
+      th[k] = c ? __uint_as_float((unsigned int)(key[k] >> 32)) : th[k];
+      hm[k] = c ? true : hm[k];
+      htri[k] = c ? (int)(unsigned int)key[k] : htri[k];
+      hitl += c ? 1u : 0u;
+    }
+  };
+  if (mesh == 0) {
+    camera_mesh();
+    camera_plane();
+  } else {
+    camera_plane();
+    camera_mesh();
+  }
+  // shade (renderer.nim:71-127): N = the face normal (renderer.nim:84-88) or
+  // the plane's (0, 1, 0); the shadow origins hitW + N * bias
+  p = params();
+  unsigned long long litm[S], anylit = 0ull, anymesh = 0ull;
+  unsigned nlit = 0u;
+  F3 N[S], so[S];
+#pragma unroll
+  for (int k = 0; k < S; ++k) {
+    litm[k] = m_lt(th[k], finf()) & m_ge(th[k], 0.0f);
+    anylit |= litm[k];
+    nlit += pc(litm[k]);
+    anymesh |= bal(hm[k]) & litm[k];
+    so[k] = f3(__builtin_fmaf(d[k].x, th[k], o.x), __builtin_fmaf(d[k].y, th[k], o.y),
+               __builtin_fmaf(d[k].z, th[k], o.z));
+  }
+  const int nbase = at(p->objx, mesh).normal_base;
+#pragma unroll
+  for (int k = 0; k < S; ++k) {
+    const bool lt = lane_in(litm[k]);
+    F3 n = f3(0.0f, 1.0f, 0.0f);
+    if (anymesh != 0ull) {  // every lane loads (face 0 for the others): no exec-mask branch
+      const bool mi = lt && hm[k];
+      const float* fn = p->normals + 3 * (size_t)(nbase + (mi ? htri[k] : 0));
+      n = f3(mi ? fn[0] : n.x, mi ? fn[1] : n.y, mi ? fn[2] : n.z);
+    }
+    N[k] = f3(lt ? n.x : 0.0f, lt ? n.y : 0.0f, lt ? n.z : 0.0f);
+  }
+  const float bias = p->bias;
+#pragma unroll
+  for (int k = 0; k < S; ++k)
+    so[k] = f3(__builtin_fmaf(N[k].x, bias, so[k].x), __builtin_fmaf(N[k].y, bias, so[k].y),
+               __builtin_fmaf(N[k].z, bias, so[k].z));
+  // one shadow ray per distant light and lit sample
+  F3 E[S];
+#pragma unroll
+  for (int k = 0; k < S; ++k) E[k] = f3(0.0f, 0.0f, 0.0f);
+  const unsigned skipw = pinfo >> 24;
+  if (anylit != 0ull) {
+#pragma unroll
+    for (int li = 0; li < NL; ++li) {
+      p = params();
+      const FLight L = at(p->lights, li);
+      const F3 sd = f3(-L.v[0], -L.v[1], -L.v[2]);
+      // the plane's shadow test (lean1's form: NaN multiplier when parallel)
+      const float mulp = fabsf(sd.y) > 1e-6f ? rcp(sd.y) : __builtin_nanf("");
+      float ts[S], tpl[S];
+#pragma unroll
+      for (int k = 0; k < S; ++k) {
+        ts[k] = lane_in(litm[k]) ? finf() : 0.0f;
+        tpl[k] = -(so[k].y + pty) * mulp;
+      }
+      auto shadow_plane = [&]() {
+#pragma unroll
+        for (int k = 0; k < S; ++k) {
+          const bool c = tpl[k] >= 0.0f && tpl[k] < ts[k];
+          ts[k] = c ? tpl[k] : ts[k];
+          hitl += c ? 1u : 0u;
+        }
+      };
+      // the mesh (gen_batch's search), false: the BVH would be needed
+      auto shadow_mesh = [&]() -> bool {
+        if (((skipw >> li) & 1u) != 0u || mob.root < 0) return true;
+#ifdef RTMI_DIAG_GEN_NOSHADOW
+        return true;
+#endif
+        F3 ro[S], rd[S];
+        unsigned long long pm[S], anyp = 0ull;
+#pragma unroll
+        for (int k = 0; k < S; ++k) {
+          ro[k] = f3(so[k].x + mob.t[0], so[k].y + mob.t[1], so[k].z + mob.t[2]);
+          rd[k] = sd;
+          pm[k] = bal(lane_in(litm[k]) && mesh_gate(mob, slab_ray(ro[k], rd[k])));
+          anyp |= pm[k];
+        }
+        if (anyp == 0ull) return true;
+        const KP q = params();
+        if (!q->grids || q->grids[li].gu <= 0) return false;
+        // the exact early exit's stop: the plane after the mesh (if it is)
+        float stop[S], tc[S], best[S];
+        unsigned long long unused[S];
+#pragma unroll
+        for (int k = 0; k < S; ++k) {
+          stop[k] = finf();
+          if (mesh == 0) stop[k] = tpl[k] >= 0.0f ? fminf(stop[k], tpl[k]) : stop[k];
+        }
+        const RT_CONST LightGrid& G = cp(q->grids)[li];
+        int cell[S];
+        unsigned long long todo[S], left = 0ull, unsafe = 0ull;
+#pragma unroll
+        for (int k = 0; k < S; ++k) {
+          const bool part = lane_in(pm[k]);
+          stop[k] = fminf(stop[k], __uint_as_float(__float_as_uint(ts[k]) - 1u));
+          tc[k] = part ? ts[k] : -1.0f;
+          best[k] = part ? ts[k] : 0.0f;
+          unused[k] = 0ull;
+          const F3 r = ro[k];
+          const float gu = __builtin_fmaf(r.x, G.e1[0], __builtin_fmaf(r.y, G.e1[1], r.z * G.e1[2]));
+          const float gv = __builtin_fmaf(r.x, G.e2[0], __builtin_fmaf(r.y, G.e2[1], r.z * G.e2[2]));
+          const float fu = (gu - G.u0) * G.inv_h, fv = (gv - G.v0) * G.inv_h;
+          const bool safe = fmaxf(fmaxf(fabsf(r.x), fabsf(r.y)), fabsf(r.z)) <= G.rmax;
+          const bool on = fu >= 0.0f && fu < (float)G.gu && fv >= 0.0f && fv < (float)G.gv;
+          cell[k] = safe && on ? G.off_base + (int)fv * G.gu + (int)fu : -1;
+          todo[k] = bal(part && cell[k] >= 0);
+          unsafe |= bal(part && !safe);
+          left |= todo[k];
+        }
+        if (unsafe != 0ull) return false;
+        const int32_t* bent = q->grid_ent + G.ent_base;
+        while (left != 0ull) {
+          int kb = -1;
+#pragma unroll
+          for (int k = S - 1; k >= 0; --k)
+            if (todo[k]) kb = __builtin_amdgcn_readlane(cell[k], (int)__builtin_ctzll(todo[k]));
+          unsigned fl = 0u;
+          unsigned long long own[S];
+          left = 0ull;
+#pragma unroll
+          for (int k = 0; k < S; ++k) {
+            own[k] = bal(cell[k] == kb) & todo[k];
+            fl |= own[k] != 0ull ? (1u << k) : 0u;
+            todo[k] &= ~own[k];
+            left |= todo[k];
+          }
+          list_search_batch<S, false>(q, bent, cp(q->grid_off)[kb], cp(q->grid_off)[kb + 1], fl, ro, rd, stop,
+                                      own, unused, best, tc);
+        }
+#pragma unroll
+        for (int k = 0; k < S; ++k) {  // found => 0 <= t < ts: the hit counts
+          const bool c = lane_in(pm[k]) && __float_as_uint(best[k]) != __float_as_uint(ts[k]);
+          ts[k] = c ? best[k] : ts[k];
+          hitl += c ? 1u : 0u;
+        }
+        return true;
+      };
+      if (mesh == 0) {
+        if (!shadow_mesh()) return false;
+        shadow_plane();
+      } else {
+        shadow_plane();
+        if (!shadow_mesh()) return false;
+      }
+#pragma unroll
+      for (int k = 0; k < S; ++k) {  // unoccluded: shadeDiffuse (shader.nim:12-17)
+        const bool vis = lane_in(litm[k]) && !(ts[k] < finf());
+        irr_add(E[k], L.ci, vis ? fmaxf(dot3(N[k], sd), 0.0f) : 0.0f);
+      }
+    }
+  }
+  // the samples' colours in order: albedo / pi x E (the hit object's), the
+  // background for the sky (every sample valid: not lit = sky)
+  p = params();
+  const RT_CONST FObjX& mx = at(p->objx, mesh);
+  const RT_CONST FObjX& px_ = at(p->objx, po);
+  const F3 am = f3(mx.albedo_pi[0], mx.albedo_pi[1], mx.albedo_pi[2]);
+  const F3 ap = f3(px_.albedo_pi[0], px_.albedo_pi[1], px_.albedo_pi[2]);
+  const F3 bg = f3(p->bg[0], p->bg[1], p->bg[2]);
+#pragma unroll
+  for (int k = 0; k < S; ++k) {
+    const bool lt = lane_in(litm[k]);
+    const F3 alb = f3(hm[k] ? am.x : ap.x, hm[k] ? am.y : ap.y, hm[k] ? am.z : ap.z);
+    const F3 a = mul3(alb, E[k]);
+    acc_add3(acc, lt ? a.x : bg.x, lt ? a.y : bg.y, lt ? a.z : bg.z);
+  }
+  wi.v[STAT_PRIMARY] += (unsigned)(64 * S);
+  wi.v[STAT_SHADOW] += (unsigned)NL * nlit;
   wi.v[STAT_HITS] += wave_sum(hitl);
   return true;
 }
@@ -2192,6 +2459,83 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RTMI_GEN_WA
         const F3 o = f3(p->cam[0], p->cam[1], p->cam[2]);
         ws.v[STAT_PRIMARY] += pc(bal(sv));
         shade_path<false, F, false>(p, o, d, sv, sv ? gp.y * p->width + gp.x : -1, pinfo, ls, acc, ws);
+      }
+    }
+    p = params();
+    finish_item(p, gp, acc.v, 64);
+    const int lane = lane_id_fresh();
+    if (++nflush >= p->stat_flush) {
+      flush_stats(ws, lds_tot[wib], lane);
+      nflush = 0;
+    }
+    qj = __builtin_amdgcn_readfirstlane(qj_next);
+    if (lane == 0) qj_next = (int)atomicAdd(head, 1u);
+    g = qj * p->shards + shard;
+  }
+  p = params();
+  const int lane = (int)__lane_id();
+  flush_stats(ws, lds_tot[wib], lane);
+  const int wave = (int)(blockIdx.x * (blockDim.x >> 6) + threadIdx.x / 64u);
+  if (lane < kStatSlots) p->partials[(size_t)wave * kStatSlots + lane] = lds_tot[wib][lane];
+}
+
+// The batched general-pixel kernel of the one-plane scenes (rtmi.cpp
+// one_plane_ok): k_render_gen with gen1_batch, NL distant lights.
+#ifndef RTMI_GEN1_WAVES
+#define RTMI_GEN1_WAVES 7
+#endif
+template <int NL>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RTMI_GEN1_WAVES))) void k_render_gen1(
+    const FastParams params_by_value) {
+  (void)params_by_value;
+  constexpr unsigned F = F_PLANE | F_MESH;
+  KP p = params();
+  __shared__ float lds[4][kLdsSlots][64];  // shade_path's scratch (the fallback)
+  __shared__ unsigned long long lds_tot[4][kStatSlots];
+  const int wib = (int)(threadIdx.x >> 6);
+  LdsF* ls = (LdsF*)&lds[wib][0][__lane_id()];
+  if (__lane_id() < (unsigned)kStatSlots) lds_tot[wib][__lane_id()] = 0ull;
+  Stats32 ws;
+#pragma unroll
+  for (int k = 0; k < kStatSlots; ++k) ws.v[k] = 0u;
+  const int shard = (int)(blockIdx.x % (unsigned int)p->shards);
+  unsigned int* head = p->queue + shard * kQueueStride;
+  int qj = 0;
+  if (__lane_id() == 0) qj = (int)atomicAdd(head, 1u);
+  qj = __builtin_amdgcn_readfirstlane(qj);
+  int qj_next = 0;
+  if (__lane_id() == 0) qj_next = (int)atomicAdd(head, 1u);
+  int g = qj * p->shards + shard;
+  int nflush = 0;
+  while (g < p->ngroups) {
+    p = params();
+    const int iters = p->iters;
+    const int gg = cp(p->order)[g];
+    GroupPix gp = group_pixel(p, gg, lane_id_fresh());
+    gp.valid = true;  // the lists hold only pixels of the launch (rtmi.cpp split_lists)
+    const unsigned pinfo = at(p->pix_info, __builtin_amdgcn_readfirstlane(gp.y * p->width + gp.x));
+    Acc acc;
+    acc.v = f3(0.0f, 0.0f, 0.0f);
+    Stats32 wi;
+#pragma unroll
+    for (int k = 0; k < kStatSlots; ++k) wi.v[k] = 0u;
+    bool ok = true;
+    for (int it = 0; ok && it < iters; it += kGenBatch) ok = gen1_batch<kGenBatch, NL>(p, gp, it, pinfo, acc, wi);
+    if (params()->flags & RT_DEV_FLAG_FALLBACK) ok = false;  // test hook (RT_FLAG_BATCH_FALLBACK)
+    if (ok) {
+      ws.v[STAT_PRIMARY] += wi.v[STAT_PRIMARY];
+      ws.v[STAT_SHADOW] += wi.v[STAT_SHADOW];
+      ws.v[STAT_HITS] += wi.v[STAT_HITS];
+    } else {  // some shadow ray needs the BVH: the whole pixel by the one-sample loop
+      acc.v = f3(0.0f, 0.0f, 0.0f);
+      ws.v[STAT_GEN_FALLBACK] += 1u;
+      for (int i2 = 0; i2 < iters; ++i2) {
+        p = params();
+        const int s = i2 * 64 + gp.sub;
+        const F3 d = camera_dir<F>(p, gp, s, nullptr);
+        const F3 o = f3(p->cam[0], p->cam[1], p->cam[2]);
+        ws.v[STAT_PRIMARY] += 64u;
+        shade_path<false, F, false>(p, o, d, true, gp.y * p->width + gp.x, pinfo, ls, acc, ws);
       }
     }
     p = params();

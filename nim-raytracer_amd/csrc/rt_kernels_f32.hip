@@ -56,6 +56,9 @@ template __global__ void fast::k_render_fast<true, fast::F_ALL>(const FastParams
 // lean pixels of one-plane scenes (rtmi.cpp lean1_ok), one or two lights
 template __global__ void fast::k_render_lean1<1>(const FastParams);
 template __global__ void fast::k_render_lean1<2>(const FastParams);
+// general pixels of the same scenes
+template __global__ void fast::k_render_gen1<1>(const FastParams);
+template __global__ void fast::k_render_gen1<2>(const FastParams);
 
 }  // namespace rtmi
 
@@ -136,6 +139,24 @@ extern "C" int rtmi_lean1_f32_blocks_per_cu(int nl) {
   int nb = 0;
   const hipError_t e = nl == 1 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, rtmi::fast::k_render_lean1<1>, 256, 0)
                                : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, rtmi::fast::k_render_lean1<2>, 256, 0);
+  return e == hipSuccess && nb > 0 ? nb : 1;
+}
+
+// The one-plane batched general-pixel kernel for nl (1 or 2) distant lights.
+extern "C" int rtmi_launch_gen1_f32(const rtmi::FastParams* p, int nl, int blocks, void* stream) {
+  if (nl == 1)
+    hipLaunchKernelGGL(rtmi::fast::k_render_gen1<1>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, *p);
+  else if (nl == 2)
+    hipLaunchKernelGGL(rtmi::fast::k_render_gen1<2>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, *p);
+  else
+    return (int)hipErrorInvalidValue;
+  return (int)hipGetLastError();
+}
+
+extern "C" int rtmi_gen1_f32_blocks_per_cu(int nl) {
+  int nb = 0;
+  const hipError_t e = nl == 1 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, rtmi::fast::k_render_gen1<1>, 256, 0)
+                               : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, rtmi::fast::k_render_gen1<2>, 256, 0);
   return e == hipSuccess && nb > 0 ? nb : 1;
 }
 

@@ -1496,9 +1496,10 @@ rt_scene::Split* split_lists(rt_scene* s, const rt_options* o, const Mapping& mp
 // mesh + plane feature subset, nothing else), with one or two distant lights,
 // and akGrid sampling with m | 64 whose samples fill whole 4-sample batches
 // of every lane (spp a multiple of 256): every sample is valid and a lane's
-// samples share one column. Off with RT_FLAG_NO_LEAN1.
+// samples share one column. Off with RT_FLAG_NO_LEAN1. The general pixels of
+// the same launches go to k_render_gen1 (off with RT_FLAG_NO_GEN1).
 bool lean1_ok(const rt_scene* s, const rt_options* o, const FastParams& p, unsigned sub) {
-  return !(o->flags & RT_FLAG_NO_LEAN1) && sub == SUB_MESH && p.nobj == 2 && p.shadow_mesh >= 0 &&
+  return sub == SUB_MESH && p.nobj == 2 && p.shadow_mesh >= 0 &&
          (p.nlight == 1 || p.nlight == 2) && !p.has_point_light && p.aa_kind == RT_AA_GRID &&
          p.log2_grid_m >= 0 && p.log2_grid_m <= 6 && p.lanes_per_px == 64 && p.spp % 256 == 0 &&
          p.iters * 64 == p.spp && p.iters % 4 == 0 && s->nobj == 2;
@@ -1551,12 +1552,16 @@ int launch(rt_scene* s, const rt_options* o, const Mapping& mp, float* d_out, hi
                            ? 0
                            : rtmi_gen_f32_blocks_per_cu(sub, shmem);
       const bool gen = gbpc > 0;
-      const long long hcap = gen ? std::min<long long>((long long)gbpc * s->num_cus, blocks) : blocks;
+      const bool one_plane = lean1_ok(s, o, p, sub);
+      const bool gen1 = gen && one_plane && !(o->flags & RT_FLAG_NO_GEN1);
+      const long long hcap =
+          gen ? std::min<long long>((long long)(gen1 ? rtmi_gen1_f32_blocks_per_cu(p.nlight) : gbpc) * s->num_cus, blocks)
+              : blocks;
       const int hb = (int)std::max(1LL, std::min<long long>(hcap, ((long long)sp->n_heavy + 3) / 4));
       ph.order = sp->heavy.p;
       ph.ngroups = sp->n_heavy;
       ph.shards = std::min(kQueueShards, hb);
-      const bool lean1 = lean1_ok(s, o, p, sub);
+      const bool lean1 = one_plane && !(o->flags & RT_FLAG_NO_LEAN1);
       const long long lcap =
           (long long)(lean1 ? rtmi_lean1_f32_blocks_per_cu(p.nlight) : rtmi_lean_f32_blocks_per_cu(sub, shmem)) *
           s->num_cus;
@@ -1578,7 +1583,9 @@ int launch(rt_scene* s, const rt_options* o, const Mapping& mp, float* d_out, hi
         HIP_TRY(hipEventRecord(s->fork, st));
         HIP_TRY(hipStreamWaitEvent(s->aux, s->fork, 0));
       }
-      int e = gen ? rtmi_launch_gen_f32(&ph, sub, hb, shmem, st) : rtmi_launch_render_f32(&ph, sub, hb, shmem, st);
+      int e = gen1  ? rtmi_launch_gen1_f32(&ph, p.nlight, hb, st)
+              : gen ? rtmi_launch_gen_f32(&ph, sub, hb, shmem, st)
+                    : rtmi_launch_render_f32(&ph, sub, hb, shmem, st);
       if (!e) e = lean1 ? rtmi_launch_lean1_f32(&pl, p.nlight, lb, sl) : rtmi_launch_lean_f32(&pl, sub, lb, shmem, sl);
       if (e) return fail(RT_E_DEVICE, "render kernel launch failed: %s", hipGetErrorString((hipError_t)e));
       if (!serial) {
@@ -1587,7 +1594,7 @@ int launch(rt_scene* s, const rt_options* o, const Mapping& mp, float* d_out, hi
       }
       blocks = hb + lb;
       s->last_lean = sp->n_lean;
-      s->last_lean_kind = lean1 ? 2 : 1;
+      s->last_lean_kind = (lean1 ? 2 : 1) | ((gen1 ? 2 : gen ? 1 : 0) << 2);
       s->last_general = sp->n_heavy;
       s->last_batched = gen ? sp->n_heavy : 0;
     } else {

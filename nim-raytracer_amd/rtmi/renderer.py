@@ -102,8 +102,9 @@ class DeviceScene:
         return int(a.value), int(b.value)
 
     def last_lean_kernel(self):
-        """0: the last call had no lean-pixel kernel, 1: the general one,
-        2: the one-plane lean kernel (k_render_lean1)."""
+        """Kernels of the last call's two classes: bits 0-1 the lean pixels'
+        (0 none, 1 k_render_lean, 2 k_render_lean1), bits 2-3 the general
+        pixels' (0 k_render_fast, 1 k_render_gen, 2 k_render_gen1)."""
         k = C.c_int32()
         check(lib().rt_scene_last_lean_kernel(self.h, C.byref(k)))
         return int(k.value)

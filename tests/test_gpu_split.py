@@ -1,7 +1,8 @@
 """Two-class launches of the float32 kernel (rtmi.cpp split_lists): lean
 pixels — no camera ray can hit the mesh, every light is a distant light whose
 shadow rays provably miss it — render in k_render_lean from a per-launch
-list (k_render_lean1 in one-plane scenes, RT_FLAG_NO_LEAN1 turns it off), the rest in k_render_gen (several samples per lane through each face
+list (k_render_lean1 in one-plane scenes, RT_FLAG_NO_LEAN1 turns it off), the rest in
+k_render_gen1 (one-plane scenes, RT_FLAG_NO_GEN1), k_render_gen (several samples per lane through each face
 list; a pixel whose shadow rays need the BVH falls back to the one-sample
 loop) or, where that does not apply, k_render_fast. Scheduling only: frames
 and Stats must be bit-identical to the general pixels in k_render_fast
@@ -15,8 +16,8 @@ stochastic samplers and progressive passes (step > 1) against the records."""
 import pytest
 
 from rtmi import Antialias, Options, Precision, akGrid, scenes
-from rtmi.abi import (RT_FLAG_BATCH_FALLBACK, RT_FLAG_NO_BATCH, RT_FLAG_NO_BINNING, RT_FLAG_NO_LEAN1,
-                      RT_FLAG_NO_REORDER, RT_FLAG_NO_SPLIT)
+from rtmi.abi import (RT_FLAG_BATCH_FALLBACK, RT_FLAG_NO_BATCH, RT_FLAG_NO_BINNING, RT_FLAG_NO_GEN1,
+                      RT_FLAG_NO_LEAN1, RT_FLAG_NO_REORDER, RT_FLAG_NO_SPLIT)
 from rtmi.dist import band_rows
 from rtmi.glm import X_AXIS, degToRad, inverse, mat4, rotate, translate, vec3
 from rtmi.renderer import DeviceScene
@@ -24,7 +25,7 @@ from rtmi.scene import akCorrelatedMultiJittered, akJittered, akMultiJittered
 
 pytestmark = pytest.mark.gpu
 
-FLAG_SETS = (0, RT_FLAG_NO_LEAN1, RT_FLAG_NO_BATCH, RT_FLAG_BATCH_FALLBACK, RT_FLAG_NO_SPLIT, RT_FLAG_NO_BINNING)
+FLAG_SETS = (0, RT_FLAG_NO_LEAN1, RT_FLAG_NO_GEN1, RT_FLAG_NO_BATCH, RT_FLAG_BATCH_FALLBACK, RT_FLAG_NO_SPLIT, RT_FLAG_NO_BINNING)
 
 
 def _opts(w, h, m, flags=0, aa=akGrid, bias=1e-4, seed=0):
@@ -146,35 +147,36 @@ def test_split_full_c3(gpu):
     assert lean + general == 1920 * 1080 and lean > 0.8 * 1920 * 1080, (lean, general)
     batched, fallback = ds.last_batch()
     assert batched == general and 0 <= fallback < 0.05 * general, (batched, fallback, general)
-    assert ds.last_lean_kernel() == 2  # the one-plane lean kernel
+    assert ds.last_lean_kernel() == 2 | 2 << 2  # the one-plane lean and general kernels
     ds.render_device(_opts(1920, 1080, 16, RT_FLAG_NO_LEAN1), fb)
-    assert ds.last_lean_kernel() == 1
+    assert ds.last_lean_kernel() == 1 | 2 << 2
+    ds.render_device(_opts(1920, 1080, 16, RT_FLAG_NO_GEN1), fb)
+    assert ds.last_lean_kernel() == 2 | 1 << 2
     ds.render_device(_opts(1920, 1080, 16, RT_FLAG_NO_SPLIT), fb)
     assert ds.last_split() == (0, 1920 * 1080) and ds.last_lean_kernel() == 0
 
 
 @pytest.mark.parametrize("m", [16, 32])
 def test_lean1_kernel_choice(gpu, m):
-    """k_render_lean1 takes the lean pixels of one-plane scenes at spp a
-    multiple of 256 (m = 16, 32) with one or two distant lights; the
-    general lean kernel takes the others — frames equal either way (the
-    FLAG_SETS comparisons above)."""
+    """k_render_lean1 / k_render_gen1 take the lean / general pixels of
+    one-plane scenes at spp a multiple of 256 (m = 16, 32) with one or two
+    distant lights; the general kernels take the others — frames equal
+    either way (here and in the FLAG_SETS comparisons above)."""
     import torch
-    from rtmi.abi import RT_FLAG_NO_LEAN1 as NO1
     one = scenes.mesh_bunny()
     one.lights = one.lights[:1]
-    for scene, want in ((scenes.mesh_bunny(), 2), (one, 2), (_reflective_ground(False), 0)):
+    for scene, want in ((scenes.mesh_bunny(), 2 | 2 << 2), (one, 2 | 2 << 2), (_reflective_ground(False), 0)):
         ds = DeviceScene(scene)
         fb = torch.zeros(256 * 144 * 3, dtype=torch.float32, device="cuda")
         st = ds.render_device(_opts(256, 144, m), fb)
         assert ds.last_lean_kernel() == want, (want, ds.last_lean_kernel())
         fb2 = torch.zeros_like(fb)
-        st2 = ds.render_device(_opts(256, 144, m, NO1), fb2)
+        st2 = ds.render_device(_opts(256, 144, m, RT_FLAG_NO_LEAN1 | RT_FLAG_NO_GEN1), fb2)
         assert st == st2 and torch.equal(fb, fb2)
     ds = DeviceScene(scenes.mesh_bunny())
     fb = torch.zeros(256 * 144 * 3, dtype=torch.float32, device="cuda")
     ds.render_device(_opts(256, 144, 8), fb)  # 64 spp: one iteration, no whole batch of 4
-    assert ds.last_lean_kernel() == 1
+    assert ds.last_lean_kernel() == 1 | 1 << 2
 
 
 def test_no_split_without_records(gpu):

@@ -8,5 +8,5 @@ timeout -k 10 600 python -u -m pytest tests/test_gpu_split.py tests/test_gpu_par
 rc=$?
 tail -5 $O/tests.log
 [ $rc -eq 0 ] || exit $rc
-for f in 0 0x80 0 0x80; do RTMI_FLAGS=$f REPS=7 timeout -k 10 120 python tools/time_c3.py >> $O/time.json 2>>$O/time.err || exit 1; done
+for f in 0 0x100 0 0x100; do RTMI_FLAGS=$f REPS=7 timeout -k 10 120 python tools/time_c3.py >> $O/time.json 2>>$O/time.err || exit 1; done
 cat $O/time.json
