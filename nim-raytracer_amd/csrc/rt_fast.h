@@ -1343,10 +1343,11 @@ __device__ __forceinline__ void tri_test_t(const RT_CONST TriFast& T, F3 o, F3 d
 // lanes test these faces only as a harmless superset, their own cell is
 // searched in its turn).
 template <int S, bool KEY>
-__device__ __forceinline__ void list_search_batch(KP p, const int32_t* ent, int b, int e, unsigned fl,
+__device__ __forceinline__ int list_search_batch(KP p, const int32_t* ent, int b, int e, unsigned fl,
                                                   const F3 (&ro)[S], const F3 (&rd)[S], const float (&stop)[S],
                                                   const unsigned long long (&own)[S], unsigned long long (&key)[S],
                                                   float (&best)[S], float (&tc)[S]) {
+  const int b_in = b;  // returns the number of faces tested (diagnostics)
   if constexpr (!KEY) {
     // a cell's first face alone: it is the one covering most of the cell
     // (rt_bins.cpp), so lanes in the umbra retire after one test
@@ -1360,7 +1361,7 @@ __device__ __forceinline__ void list_search_batch(KP p, const int32_t* ent, int 
           tc[k] = tc[k] <= stop[k] ? -1.0f : tc[k];
           left |= bal(tc[k] >= 0.0f) & own[k];
         }
-      if (left == 0ull) return;
+      if (left == 0ull) return 1;
       ++b;
     }
   }
@@ -1386,9 +1387,10 @@ __device__ __forceinline__ void list_search_batch(KP p, const int32_t* ent, int 
           tc[k] = tc[k] <= stop[k] ? -1.0f : tc[k];
           left |= bal(tc[k] >= 0.0f) & own[k];
         }
-      if (left == 0ull) break;
+      if (left == 0ull) return min(e, k0 + 4) - b_in;
     }
   }
+  return e - b_in;
 }
 
 // The mesh's AABB gate (TriangleMesh.intersect, geom.nim:339-341) in the
@@ -1912,12 +1914,21 @@ __device__ __forceinline__ bool gen1_batch(KP p, const GroupPix& gp, int it0, un
 #pragma unroll
           for (int k = 0; k < S; ++k) {
             own[k] = bal(cell[k] == kb) & todo[k];
-            fl |= own[k] != 0ull ? (1u << k) : 0u;
             todo[k] &= ~own[k];
             left |= todo[k];
+            fl |= own[k] != 0ull ? (1u << k) : 0u;
+#ifdef RTMI_DIAG_GEN_COUNT
+            wi.v[STAT_LANE_NODES] += pc(own[k]);  // diagnostic: rays in searched cells
+#endif
           }
-          list_search_batch<S, false>(q, bent, cp(q->grid_off)[kb], cp(q->grid_off)[kb + 1], fl, ro, rd, stop,
-                                      own, unused, best, tc);
+          const int nt = list_search_batch<S, false>(q, bent, cp(q->grid_off)[kb], cp(q->grid_off)[kb + 1], fl, ro, rd,
+                                                     stop, own, unused, best, tc);
+#ifdef RTMI_DIAG_GEN_COUNT
+          wi.v[STAT_NODE_FETCH] += 1u;                                      // diagnostic: cells searched
+          wi.v[STAT_TRI_FETCH] += (unsigned)nt * (unsigned)__builtin_popcount(fl);  // wave face tests
+#else
+          (void)nt;
+#endif
         }
 #pragma unroll
         for (int k = 0; k < S; ++k) {  // found => 0 <= t < ts: the hit counts
@@ -2385,6 +2396,183 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
   if (lane < kStatSlots) p->partials[(size_t)wave * kStatSlots + lane] = lds_tot[wib][lane];
 }
 
+// A one-pixel group's placement computed per lane (g differs per lane):
+// group_pixel for tile 1 x 1 (lanes_per_px = 64), without the validity test
+// (list entries are pixels of the launch).
+__device__ __forceinline__ GroupPix lane_pixel(KP p, int g) {
+  GroupPix r;
+  r.sub = 0;
+  r.valid = true;
+  const int k = (int)(((unsigned long long)(unsigned)g * p->tx_magic) >> p->tx_shift);  // g / tiles_x
+  const int j = g - k * p->tiles_x;
+  r.x = j * p->step;
+  if (p->mode == 0) {
+    r.y = p->y0 + k * p->step;
+    r.out_row = r.y;
+  } else {
+    int rr;
+    const int lb = div_small(k, p->band_h, p->inv_band_h, rr);
+    r.y = (lb * p->world + p->rank) * p->band_h + rr;
+    r.out_row = k;
+  }
+  return r;
+}
+
+// The one-plane lean pixels with four lanes per pixel (k_render_lean1's
+// arithmetic per sample, a different assignment of samples to lanes): lane
+// 4i + q of a wave renders "virtual lanes" 16q .. 16q + 15 of pixel i of a
+// 16-pixel work item — the samples k_render_lean1's lanes 16q .. 16q + 15
+// carry — each virtual lane's samples added in sample order as there, the 16
+// virtual lanes in the balanced pairwise order of wave_total's DPP row scan
+// (a binary-counter stack), and the four quarters as its row broadcasts pair
+// them: ((R0 + R1) + (R2 + R3)). So every pixel is the same float sum as in
+// k_render_lean1, bit for bit, with no per-pixel wave reduction and the
+// per-pixel set-up spread over 16 pixels at once.
+template <int NL>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k_render_lean1q(
+    const FastParams params_by_value) {
+  (void)params_by_value;
+  const KP p = params();
+  __shared__ unsigned long long lds_tot[4][kStatSlots];
+  const int wib = (int)(threadIdx.x >> 6);
+  const int lane = (int)__lane_id();
+  if (lane < kStatSlots) lds_tot[wib][lane] = 0ull;
+  Stats32 ws;
+#pragma unroll
+  for (int k = 0; k < kStatSlots; ++k) ws.v[k] = 0u;
+  const int shard = (int)(blockIdx.x % (unsigned int)p->shards);
+  unsigned int* head = p->queue + shard * kQueueStride;
+  int qj = 0;
+  if (lane == 0) qj = (int)atomicAdd(head, 1u);
+  qj = __builtin_amdgcn_readfirstlane(qj);
+  int qj_next = 0;
+  if (lane == 0) qj_next = (int)atomicAdd(head, 1u);
+  int g = qj * p->shards + shard;
+  int nflush = 0;
+  const int iters = p->iters;
+  const int po = p->shadow_mesh == 0 ? 1 : 0;
+  const FObj pl = at(p->objs, po);
+  const RT_CONST FObjX& plx = at(p->objx, po);
+  const float nroy = -(p->cam[1] + pl.t[1]);
+  const float ty = pl.t[1], oy = p->cam[1], bias = p->bias;
+  float mulp[NL], ndl[NL], ci[NL][3];
+#pragma unroll
+  for (int l = 0; l < NL; ++l) {
+    const FLight L = at(p->lights, l);
+    const F3 sd = f3(-L.v[0], -L.v[1], -L.v[2]);
+    mulp[l] = fabsf(sd.y) > 1e-6f ? rcp(sd.y) : __builtin_nanf("");
+    ndl[l] = fmaxf(dot3(f3(0.0f, 1.0f, 0.0f), sd), 0.0f);
+    ci[l][0] = L.ci[0];
+    ci[l][1] = L.ci[1];
+    ci[l][2] = L.ci[2];
+  }
+  const F3 alb = f3(plx.albedo_pi[0], plx.albedo_pi[1], plx.albedo_pi[2]);
+  const F3 bg = f3(p->bg[0], p->bg[1], p->bg[2]);
+  const int mm = p->grid_m - 1, lg = p->log2_grid_m;
+  const float st = p->sample_step, of = p->sample_off;
+  const int q = lane & 3;  // this lane's quarter of its pixel's virtual lanes
+  while (g < p->ngroups) {
+    const int gg = p->order[g * 16 + (lane >> 2)];  // this lane's pixel (list entry; -1: padding)
+    qj = __builtin_amdgcn_readfirstlane(qj_next);
+    if (lane == 0) qj_next = (int)atomicAdd(head, 1u);
+    const unsigned long long vmask = bal(gg >= 0);
+    const GroupPix gp = lane_pixel(p, gg >= 0 ? gg : 0);
+    const float pxb = (float)gp.x, pyb = (float)gp.y;
+    unsigned nlit = 0u, nocc = 0u;
+    // the binary-counter stack of the 16 virtual lanes' partial sums
+    F3 s0 = f3(0.0f, 0.0f, 0.0f), s1 = s0, s2 = s0, s3 = s0;
+#pragma unroll 1
+    for (int j = 0; j < 16; ++j) {
+      const int jv = q * 16 + j;  // the virtual lane (k_render_lean1's lane)
+      const float px = pxb + __builtin_fmaf((float)(jv & mm), st, of);
+      const float cx = (px - p->cam_b) * p->cam_a;
+      const float q0 = __builtin_fmaf(cx, cx, 1.0f);
+      const float ay = __builtin_fmaf(cx, p->cam[4], -p->cam[10]);
+      F3 acc = f3(0.0f, 0.0f, 0.0f);
+      // iters is a multiple of 4 (rtmi.cpp lean1_ok): four samples per step
+#pragma unroll 1
+      for (int it0 = 0; it0 < iters; it0 += 4)
+#pragma unroll
+      for (int it = it0; it < it0 + 4; ++it) {
+        const int s = it * 64 + jv;
+        const float py = pyb + __builtin_fmaf((float)(s >> lg), st, of);
+        const float cy = (p->cam_d - py) * p->cam_c;
+        const float rl = rsq(__builtin_fmaf(cy, cy, q0));
+        const float dy = __builtin_fmaf(cy, p->cam[7], ay) * rl;
+        const float t = fabsf(dy) > 1e-6f ? nroy * rcp(dy) : -finf();
+        const unsigned long long litm = m_hit0(t) & vmask;
+        nlit += pc(litm);
+        const bool lit = lane_in(litm);
+        const float soy = __builtin_fmaf(1.0f, bias, __builtin_fmaf(dy, t, oy));
+        F3 E = f3(0.0f, 0.0f, 0.0f);
+#pragma unroll
+        for (int l = 0; l < NL; ++l) {
+          const float ts = -(soy + ty) * mulp[l];
+          const unsigned long long occ = m_hit0(ts) & litm;
+          nocc += pc(occ);
+          const float x = lane_in(litm & ~occ) ? ndl[l] : 0.0f;
+          E = f3(__builtin_fmaf(ci[l][0], x, E.x), __builtin_fmaf(ci[l][1], x, E.y), __builtin_fmaf(ci[l][2], x, E.z));
+        }
+        const F3 a = mul3(alb, E);
+        acc = f3(acc.x + (lit ? a.x : bg.x), acc.y + (lit ? a.y : bg.y), acc.z + (lit ? a.z : bg.z));
+      }
+      // push: pair with the stack while j has trailing ones (uniform branches)
+      F3 t = acc;
+      if (j & 1) {
+        t = f3(s0.x + t.x, s0.y + t.y, s0.z + t.z);
+        if (j & 2) {
+          t = f3(s1.x + t.x, s1.y + t.y, s1.z + t.z);
+          if (j & 4) {
+            t = f3(s2.x + t.x, s2.y + t.y, s2.z + t.z);
+            if (j & 8) t = f3(s3.x + t.x, s3.y + t.y, s3.z + t.z);
+            else s3 = t;
+          } else {
+            s2 = t;
+          }
+        } else {
+          s1 = t;
+        }
+      } else {
+        s0 = t;
+      }
+      if (j == 15) s0 = t;  // the row's sum
+    }
+    // the quarters: ((R0 + R1) + (R2 + R3)) by quad permutes (DPP)
+    F3 r = s0;
+    r = f3(r.x + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(r.x), 0xB1, 0xf, 0xf, false)),
+           r.y + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(r.y), 0xB1, 0xf, 0xf, false)),
+           r.z + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(r.z), 0xB1, 0xf, 0xf, false)));
+    r = f3(r.x + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(r.x), 0x4E, 0xf, 0xf, false)),
+           r.y + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(r.y), 0x4E, 0xf, 0xf, false)),
+           r.z + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(r.z), 0x4E, 0xf, 0xf, false)));
+    if (gg >= 0 && q == 0) {  // renderer.nim:159 (1 / samples.len), :204-209 (the pixel or its block)
+      const F3 c = f3(r.x * p->inv_len, r.y * p->inv_len, r.z * p->inv_len);
+      if (p->mode == 0 && p->step > 1) {
+        const int xe = min(gp.x + p->step, p->width), ye = min(gp.y + p->step, p->height);
+        for (int yy = gp.y; yy < ye; ++yy)
+          for (int xx = gp.x; xx < xe; ++xx) {
+            float* o = p->fb + ((size_t)yy * p->width + xx) * 3;
+            o[0] = c.x; o[1] = c.y; o[2] = c.z;
+          }
+      } else {
+        float* o = p->fb + ((size_t)gp.out_row * p->width + gp.x) * 3;
+        o[0] = c.x; o[1] = c.y; o[2] = c.z;
+      }
+    }
+    ws.v[STAT_PRIMARY] += pc(vmask) * 16u * (unsigned)iters;
+    ws.v[STAT_SHADOW] += (unsigned)NL * nlit;
+    ws.v[STAT_HITS] += nlit + nocc;
+    if (++nflush >= p->stat_flush) {
+      flush_stats(ws, lds_tot[wib], lane);
+      nflush = 0;
+    }
+    g = qj * p->shards + shard;
+  }
+  flush_stats(ws, lds_tot[wib], lane);
+  const int wave = (int)(blockIdx.x * (blockDim.x >> 6) + threadIdx.x / 64u);
+  if (lane < kStatSlots) p->partials[(size_t)wave * kStatSlots + lane] = lds_tot[wib][lane];
+}
+
 // The batched general-pixel kernel (two-class launches, rtmi.cpp
 // split_lists): the launch's non-lean pixel groups (p->order lists them),
 // each rendered by gen_batch from its pixel record, or — when a batch needs
@@ -2526,6 +2714,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RTMI_GEN1_W
       ws.v[STAT_PRIMARY] += wi.v[STAT_PRIMARY];
       ws.v[STAT_SHADOW] += wi.v[STAT_SHADOW];
       ws.v[STAT_HITS] += wi.v[STAT_HITS];
+#ifdef RTMI_DIAG_GEN_COUNT
+      for (int q = STAT_NODE_FETCH; q <= STAT_LANE_TRIS; ++q) ws.v[q] += wi.v[q];
+#endif
     } else {  // some shadow ray needs the BVH: the whole pixel by the one-sample loop
       acc.v = f3(0.0f, 0.0f, 0.0f);
       ws.v[STAT_GEN_FALLBACK] += 1u;

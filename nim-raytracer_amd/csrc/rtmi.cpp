@@ -1481,9 +1481,10 @@ rt_scene::Split* split_lists(rt_scene* s, const rt_options* o, const Mapping& mp
   e->key = key;
   e->n_lean = (int)lean.size();
   e->n_heavy = (int)heavy.size();
-  // k_render_lean takes runs of kLeanRun entries: padded with -1
-  while (lean.size() % kLeanRun) lean.push_back(-1);
-  if (lean.empty()) lean.assign(kLeanRun, -1);  // keep both allocations non-empty
+  // k_render_lean takes runs of kLeanRun entries, k_render_lean1q items of
+  // 16: padded with -1 to a multiple of 64
+  while (lean.size() % 64) lean.push_back(-1);
+  if (lean.empty()) lean.assign(64, -1);  // keep both allocations non-empty
   if (heavy.empty()) heavy.push_back(0);
   if (e->lean.upload(lean) != RT_OK || e->heavy.upload(heavy) != RT_OK) return nullptr;
   s->splits.insert(s->splits.begin(), std::move(e));
@@ -1565,12 +1566,15 @@ int launch(rt_scene* s, const rt_options* o, const Mapping& mp, float* d_out, hi
       const long long lcap =
           (long long)(lean1 ? rtmi_lean1_f32_blocks_per_cu(p.nlight) : rtmi_lean_f32_blocks_per_cu(sub, shmem)) *
           s->num_cus;
-      const int lruns = (sp->n_lean + kLeanRun - 1) / kLeanRun;  // k_render_lean's work items
+      // work items: runs of kLeanRun pixels (k_render_lean, k_render_lean1),
+      // 16 pixels (k_render_lean1q)
+      const int lrun = (lean1 && rtmi_lean1_quads()) ? 16 : kLeanRun;
+      const int lruns = (sp->n_lean + lrun - 1) / lrun;
       const int lb = (int)std::max(1LL, std::min<long long>(std::min<long long>(lcap, s->max_waves / 4),
                                                             ((long long)lruns + 3) / 4));
       pl.order = sp->lean.p;
       pl.ngroups = lruns;
-      pl.stat_flush = std::max(1, p.stat_flush / kLeanRun);
+      pl.stat_flush = std::max(1, p.stat_flush / lrun);
       pl.shards = std::min(kQueueShards, lb);
       pl.queue = s->queue.p + (size_t)kQueueShards * kQueueStride;
       pl.partials = s->partials.p + (size_t)hb * 4 * kStatSlots;

@@ -1,4 +1,4 @@
-# lean1 kernel: split/parity GPU tests, then C3 timing with and without it
+# split/parity/bins GPU tests, then C3 timing A/B (env var toggles)
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
@@ -8,5 +8,8 @@ timeout -k 10 600 python -u -m pytest tests/test_gpu_split.py tests/test_gpu_par
 rc=$?
 tail -5 $O/tests.log
 [ $rc -eq 0 ] || exit $rc
-for f in 0 0x100 0 0x100; do RTMI_FLAGS=$f REPS=7 timeout -k 10 120 python tools/time_c3.py >> $O/time.json 2>>$O/time.err || exit 1; done
+for i in 1 2; do
+  REPS=7 timeout -k 10 120 python tools/time_c3.py >> $O/time.json 2>>$O/time.err || exit 1
+  RTMI_LEAN1Q=0 REPS=7 timeout -k 10 120 python tools/time_c3.py >> $O/time.json 2>>$O/time.err || exit 1
+done
 cat $O/time.json
