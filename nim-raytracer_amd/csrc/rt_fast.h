@@ -2270,8 +2270,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RTMI_LEAN_W
 // Frames and Stats bit-identical to k_render_lean / k_render_fast
 // (tests/test_gpu_split.py, RT_FLAG_NO_LEAN1).
 // "t >= 0 and below the running limit" against a first object (limit
-// +inf): ordered t >= 0 and t < +inf, as two compares straight to a mask
-__device__ __forceinline__ unsigned long long m_hit0(float t) { return m_ge(t, 0.0f) & m_lt(t, finf()); }
+// +inf): t in [-0, +inf), NaN excluded.
+// One v_cmp_class straight into a lane mask: classes -0, +0, +denormal,
+// +normal (the kernels run with fp32 denormals preserved,
+// .amdhsa_float_denorm_mode_32 3, so compares see denormals as such). The
+// builtin's bool went through a VGPR and back (v_cndmask + v_cmp).
+__device__ __forceinline__ unsigned long long m_hit0(float t) {
+  unsigned long long m;
+  asm("v_cmp_class_f32_e64 %0, %1, %2" : "=s"(m) : "v"(t), "v"(0x1E0));
+  return m;
+}
 template <int NL>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k_render_lean1(
     const FastParams params_by_value) {
@@ -2467,7 +2475,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
     ci[l][2] = L.ci[2];
   }
   const F3 alb = f3(plx.albedo_pi[0], plx.albedo_pi[1], plx.albedo_pi[2]);
-  const F3 bg = f3(p->bg[0], p->bg[1], p->bg[2]);
+  F3 bg = f3(p->bg[0], p->bg[1], p->bg[2]);
+  // the background in VGPRs for the whole kernel: a select against an SGPR
+  // operand with the mask in VCC needs a v_mov per use (constant bus)
+  asm volatile("" : "+v"(bg.x), "+v"(bg.y), "+v"(bg.z));
   const int mm = p->grid_m - 1, lg = p->log2_grid_m;
   const float st = p->sample_step, of = p->sample_off;
   const int q = lane & 3;  // this lane's quarter of its pixel's virtual lanes
@@ -2488,14 +2499,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
       const float cx = (px - p->cam_b) * p->cam_a;
       const float q0 = __builtin_fmaf(cx, cx, 1.0f);
       const float ay = __builtin_fmaf(cx, p->cam[4], -p->cam[10]);
+      // the sample row (it * 64 + jv) >> lg == it * (64 >> lg) + (jv >> lg)
+      // (m | 64), as a float stepped by 64 >> lg: exact small integers
+      float sjf = (float)(jv >> lg);
+      const float rows = (float)(64 >> lg);
       F3 acc = f3(0.0f, 0.0f, 0.0f);
       // iters is a multiple of 4 (rtmi.cpp lean1_ok): four samples per step
 #pragma unroll 1
       for (int it0 = 0; it0 < iters; it0 += 4)
 #pragma unroll
       for (int it = it0; it < it0 + 4; ++it) {
-        const int s = it * 64 + jv;
-        const float py = pyb + __builtin_fmaf((float)(s >> lg), st, of);
+        const float py = pyb + __builtin_fmaf(sjf, st, of);
+        sjf += rows;
         const float cy = (p->cam_d - py) * p->cam_c;
         const float rl = rsq(__builtin_fmaf(cy, cy, q0));
         const float dy = __builtin_fmaf(cy, p->cam[7], ay) * rl;
