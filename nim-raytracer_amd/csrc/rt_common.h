@@ -277,7 +277,7 @@ int rtmi_launch_render_f64(const rtmi::RenderParams<double>* p, int blocks, void
 int rtmi_render_f32_blocks_per_cu(int count, unsigned subset, size_t shmem);
 int rtmi_launch_lean_f32(const rtmi::FastParams* p, unsigned subset, int blocks, size_t shmem, void* stream);
 int rtmi_lean_f32_blocks_per_cu(unsigned subset, size_t shmem);
-int rtmi_launch_lean1_f32(const rtmi::FastParams* p, int nl, int blocks, void* stream);
+int rtmi_launch_lean1_f32(const rtmi::FastParams* p, int nl, int lp, int blocks, void* stream);
 int rtmi_lean1_f32_blocks_per_cu(int nl);
 int rtmi_lean1_quads();
 int rtmi_launch_gen1_f32(const rtmi::FastParams* p, int nl, int blocks, void* stream);

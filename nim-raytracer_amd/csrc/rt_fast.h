@@ -2426,17 +2426,20 @@ __device__ __forceinline__ GroupPix lane_pixel(KP p, int g) {
   return r;
 }
 
-// The one-plane lean pixels with four lanes per pixel (k_render_lean1's
+// The one-plane lean pixels with LP lanes per pixel (k_render_lean1's
 // arithmetic per sample, a different assignment of samples to lanes): lane
-// 4i + q of a wave renders "virtual lanes" 16q .. 16q + 15 of pixel i of a
-// 16-pixel work item — the samples k_render_lean1's lanes 16q .. 16q + 15
-// carry — each virtual lane's samples added in sample order as there, the 16
-// virtual lanes in the balanced pairwise order of wave_total's DPP row scan
-// (a binary-counter stack), and the four quarters as its row broadcasts pair
-// them: ((R0 + R1) + (R2 + R3)). So every pixel is the same float sum as in
-// k_render_lean1, bit for bit, with no per-pixel wave reduction and the
-// per-pixel set-up spread over 16 pixels at once.
-template <int NL>
+// LP i + q of a wave renders "virtual lanes" V q .. V q + V - 1 (V = 64 / LP)
+// of pixel i of a (64 / LP)-pixel work item — the samples k_render_lean1's
+// lanes V q .. carry — each virtual lane's samples added in sample order as
+// there, a lane's V virtual lanes in the balanced pairwise order of
+// wave_total's DPP row scan (a binary-counter stack), then the lanes of the
+// pixel pairwise by xor shuffles (1, 2, 4, 8, ...): wave_total is that
+// balanced tree over the 64 lanes (row scans, then rows as ((R0 + R1) +
+// (R2 + R3))). So every pixel is the same float sum as in k_render_lean1,
+// bit for bit, with no per-pixel wave reduction and the per-pixel set-up
+// spread over 64 / LP pixels at once. LP = 4 (16 pixels per item) for whole
+// frames, 16 (4 per item) for short launches (rtmi.cpp).
+template <int NL, int LP>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k_render_lean1q(
     const FastParams params_by_value) {
   (void)params_by_value;
@@ -2481,20 +2484,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
   asm volatile("" : "+v"(bg.x), "+v"(bg.y), "+v"(bg.z));
   const int mm = p->grid_m - 1, lg = p->log2_grid_m;
   const float st = p->sample_step, of = p->sample_off;
-  const int q = lane & 3;  // this lane's quarter of its pixel's virtual lanes
+  static_assert(LP == 4 || LP == 8 || LP == 16, "lanes per pixel");
+  constexpr int V = 64 / LP;   // virtual lanes per lane
+  constexpr int PPI = 64 / LP; // pixels per work item
+  const int q = lane & (LP - 1);  // this lane's share of its pixel's virtual lanes
   while (g < p->ngroups) {
-    const int gg = p->order[g * 16 + (lane >> 2)];  // this lane's pixel (list entry; -1: padding)
+    const int gg = p->order[g * PPI + lane / LP];  // this lane's pixel (list entry; -1: padding)
     qj = __builtin_amdgcn_readfirstlane(qj_next);
     if (lane == 0) qj_next = (int)atomicAdd(head, 1u);
     const unsigned long long vmask = bal(gg >= 0);
     const GroupPix gp = lane_pixel(p, gg >= 0 ? gg : 0);
     const float pxb = (float)gp.x, pyb = (float)gp.y;
     unsigned nlit = 0u, nocc = 0u;
-    // the binary-counter stack of the 16 virtual lanes' partial sums
+    // the binary-counter stack of the V virtual lanes' partial sums
     F3 s0 = f3(0.0f, 0.0f, 0.0f), s1 = s0, s2 = s0, s3 = s0;
 #pragma unroll 1
-    for (int j = 0; j < 16; ++j) {
-      const int jv = q * 16 + j;  // the virtual lane (k_render_lean1's lane)
+    for (int j = 0; j < V; ++j) {
+      const int jv = q * V + j;  // the virtual lane (k_render_lean1's lane)
       const float px = pxb + __builtin_fmaf((float)(jv & mm), st, of);
       const float cx = (px - p->cam_b) * p->cam_a;
       const float q0 = __builtin_fmaf(cx, cx, 1.0f);
@@ -2550,9 +2556,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
       } else {
         s0 = t;
       }
-      if (j == 15) s0 = t;  // the row's sum
+      if (j == V - 1) s0 = t;  // the lane's sum
     }
-    // the quarters: ((R0 + R1) + (R2 + R3)) by quad permutes (DPP)
+    // the pixel's lanes pairwise: xor 1 and 2 by quad permutes (DPP), then
+    // xor 4, 8, ... by shuffles
     F3 r = s0;
     r = f3(r.x + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(r.x), 0xB1, 0xf, 0xf, false)),
            r.y + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(r.y), 0xB1, 0xf, 0xf, false)),
@@ -2560,6 +2567,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
     r = f3(r.x + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(r.x), 0x4E, 0xf, 0xf, false)),
            r.y + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(r.y), 0x4E, 0xf, 0xf, false)),
            r.z + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(r.z), 0x4E, 0xf, 0xf, false)));
+#pragma unroll
+    for (int off = 4; off < LP; off <<= 1)
+      r = f3(r.x + __shfl_xor(r.x, off), r.y + __shfl_xor(r.y, off), r.z + __shfl_xor(r.z, off));
     if (gg >= 0 && q == 0) {  // renderer.nim:159 (1 / samples.len), :204-209 (the pixel or its block)
       const F3 c = f3(r.x * p->inv_len, r.y * p->inv_len, r.z * p->inv_len);
       if (p->mode == 0 && p->step > 1) {
@@ -2574,7 +2584,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
         o[0] = c.x; o[1] = c.y; o[2] = c.z;
       }
     }
-    ws.v[STAT_PRIMARY] += pc(vmask) * 16u * (unsigned)iters;
+    ws.v[STAT_PRIMARY] += pc(vmask) * (unsigned)V * (unsigned)iters;
     ws.v[STAT_SHADOW] += (unsigned)NL * nlit;
     ws.v[STAT_HITS] += nlit + nocc;
     if (++nflush >= p->stat_flush) {

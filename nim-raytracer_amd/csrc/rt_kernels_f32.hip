@@ -58,8 +58,10 @@ template __global__ void fast::k_render_fast<true, fast::F_ALL>(const FastParams
 // lean pixels of one-plane scenes (rtmi.cpp lean1_ok), one or two lights
 template __global__ void fast::k_render_lean1<1>(const FastParams);
 template __global__ void fast::k_render_lean1<2>(const FastParams);
-template __global__ void fast::k_render_lean1q<1>(const FastParams);
-template __global__ void fast::k_render_lean1q<2>(const FastParams);
+template __global__ void fast::k_render_lean1q<1, 4>(const FastParams);
+template __global__ void fast::k_render_lean1q<2, 4>(const FastParams);
+template __global__ void fast::k_render_lean1q<1, 16>(const FastParams);
+template __global__ void fast::k_render_lean1q<2, 16>(const FastParams);
 // general pixels of the same scenes
 template __global__ void fast::k_render_gen1<1>(const FastParams);
 template __global__ void fast::k_render_gen1<2>(const FastParams);
@@ -128,9 +130,9 @@ extern "C" int rtmi_lean_f32_blocks_per_cu(unsigned subset, size_t shmem) {
   return kOccupancyLean[(subset >> 3) & 15u](subset & 127u, shmem);
 }
 
-// k_render_lean1q (four lanes per pixel, 16 pixels per work item) instead of
-// k_render_lean1 (one pixel per wave, a run of 4 per item); RTMI_LEAN1Q=0
-// picks the latter (diagnostic A/B).
+// k_render_lean1q (lp = 4 or 16 lanes per pixel, 64 / lp pixels per work
+// item) instead of k_render_lean1 (lp = 64: one pixel per wave, a run of 4
+// per item); RTMI_LEAN1Q=0 picks the latter (diagnostic A/B).
 extern "C" int rtmi_lean1_quads() {
   static const int q = [] {
     const char* e = std::getenv("RTMI_LEAN1Q");
@@ -139,13 +141,18 @@ extern "C" int rtmi_lean1_quads() {
   return q;
 }
 
-// The one-plane lean-pixel kernel for nl (1 or 2) distant lights.
-extern "C" int rtmi_launch_lean1_f32(const rtmi::FastParams* p, int nl, int blocks, void* stream) {
-  if (rtmi_lean1_quads()) {
-    if (nl == 1)
-      hipLaunchKernelGGL(rtmi::fast::k_render_lean1q<1>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, *p);
+// The one-plane lean-pixel kernel for nl (1 or 2) distant lights, lp lanes per pixel.
+extern "C" int rtmi_launch_lean1_f32(const rtmi::FastParams* p, int nl, int lp, int blocks, void* stream) {
+  if (lp == 4 || lp == 16) {
+    using namespace rtmi::fast;
+    if (nl == 1 && lp == 4)
+      hipLaunchKernelGGL((k_render_lean1q<1, 4>), dim3(blocks), dim3(256), 0, (hipStream_t)stream, *p);
+    else if (nl == 2 && lp == 4)
+      hipLaunchKernelGGL((k_render_lean1q<2, 4>), dim3(blocks), dim3(256), 0, (hipStream_t)stream, *p);
+    else if (nl == 1)
+      hipLaunchKernelGGL((k_render_lean1q<1, 16>), dim3(blocks), dim3(256), 0, (hipStream_t)stream, *p);
     else if (nl == 2)
-      hipLaunchKernelGGL(rtmi::fast::k_render_lean1q<2>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, *p);
+      hipLaunchKernelGGL((k_render_lean1q<2, 16>), dim3(blocks), dim3(256), 0, (hipStream_t)stream, *p);
     else
       return (int)hipErrorInvalidValue;
     return (int)hipGetLastError();

@@ -1558,7 +1558,11 @@ int launch(rt_scene* s, const rt_options* o, const Mapping& mp, float* d_out, hi
       const long long hcap =
           gen ? std::min<long long>((long long)(gen1 ? rtmi_gen1_f32_blocks_per_cu(p.nlight) : gbpc) * s->num_cus, blocks)
               : blocks;
-      const int hb = (int)std::max(1LL, std::min<long long>(hcap, ((long long)sp->n_heavy + 3) / 4));
+      // diagnostic: RTMI_GEN_WAVES_CAP / RTMI_LEAN_WAVES_CAP = resident waves per SIMD each kernel may take
+      static const int gen_cap = std::getenv("RTMI_GEN_WAVES_CAP") ? std::atoi(std::getenv("RTMI_GEN_WAVES_CAP")) : 0;
+      static const int lean_cap = std::getenv("RTMI_LEAN_WAVES_CAP") ? std::atoi(std::getenv("RTMI_LEAN_WAVES_CAP")) : 0;
+      const long long hcap2 = gen_cap > 0 ? std::min<long long>(hcap, (long long)gen_cap * s->num_cus) : hcap;
+      const int hb = (int)std::max(1LL, std::min<long long>(hcap2, ((long long)sp->n_heavy + 3) / 4));
       ph.order = sp->heavy.p;
       ph.ngroups = sp->n_heavy;
       ph.shards = std::min(kQueueShards, hb);
@@ -1567,10 +1571,15 @@ int launch(rt_scene* s, const rt_options* o, const Mapping& mp, float* d_out, hi
           (long long)(lean1 ? rtmi_lean1_f32_blocks_per_cu(p.nlight) : rtmi_lean_f32_blocks_per_cu(sub, shmem)) *
           s->num_cus;
       // work items: runs of kLeanRun pixels (k_render_lean, k_render_lean1),
-      // 16 pixels (k_render_lean1q)
-      const int lrun = (lean1 && rtmi_lean1_quads()) ? 16 : kLeanRun;
+      // 64 / lp pixels (k_render_lean1q, lp lanes per pixel): 16 per item
+      // unless that leaves fewer than 8 items per resident wave (a short
+      // launch, e.g. a multi-GPU rank's bands), then 4
+      const long long lwaves = 4LL * std::min<long long>(lcap, s->max_waves / 4);
+      const int lp = !(lean1 && rtmi_lean1_quads()) ? 64 : ((long long)(sp->n_lean + 15) / 16 >= 8 * lwaves ? 4 : 16);
+      const int lrun = lp == 64 ? kLeanRun : 64 / lp;
       const int lruns = (sp->n_lean + lrun - 1) / lrun;
-      const int lb = (int)std::max(1LL, std::min<long long>(std::min<long long>(lcap, s->max_waves / 4),
+      const long long lcap2 = lean_cap > 0 ? std::min<long long>(lcap, (long long)lean_cap * s->num_cus) : lcap;
+      const int lb = (int)std::max(1LL, std::min<long long>(std::min<long long>(lcap2, s->max_waves / 4),
                                                             ((long long)lruns + 3) / 4));
       pl.order = sp->lean.p;
       pl.ngroups = lruns;
@@ -1587,10 +1596,16 @@ int launch(rt_scene* s, const rt_options* o, const Mapping& mp, float* d_out, hi
         HIP_TRY(hipEventRecord(s->fork, st));
         HIP_TRY(hipStreamWaitEvent(s->aux, s->fork, 0));
       }
-      int e = gen1  ? rtmi_launch_gen1_f32(&ph, p.nlight, hb, st)
-              : gen ? rtmi_launch_gen_f32(&ph, sub, hb, shmem, st)
-                    : rtmi_launch_render_f32(&ph, sub, hb, shmem, st);
-      if (!e) e = lean1 ? rtmi_launch_lean1_f32(&pl, p.nlight, lb, sl) : rtmi_launch_lean_f32(&pl, sub, lb, shmem, sl);
+      static const bool lean_first = std::getenv("RTMI_LEAN_FIRST") != nullptr;  // diagnostic
+      auto launch_lean = [&]() {
+        return lean1 ? rtmi_launch_lean1_f32(&pl, p.nlight, lp, lb, sl) : rtmi_launch_lean_f32(&pl, sub, lb, shmem, sl);
+      };
+      int e = lean_first ? launch_lean() : 0;
+      if (!e)
+        e = gen1  ? rtmi_launch_gen1_f32(&ph, p.nlight, hb, st)
+            : gen ? rtmi_launch_gen_f32(&ph, sub, hb, shmem, st)
+                  : rtmi_launch_render_f32(&ph, sub, hb, shmem, st);
+      if (!e && !lean_first) e = launch_lean();
       if (e) return fail(RT_E_DEVICE, "render kernel launch failed: %s", hipGetErrorString((hipError_t)e));
       if (!serial) {
         HIP_TRY(hipEventRecord(s->join, s->aux));

@@ -12,6 +12,7 @@ from rtmi.renderer import DeviceScene  # noqa: E402
 
 cfg = os.environ.get("CONFIG", "C3")
 scene, W, H, m = {"C3": (scenes.mesh_bunny, 1920, 1080, 16), "C2": (scenes.boxes2, 1920, 1080, 8),
+                  "C4": (scenes.mesh_bunny, 3840, 2160, 32),
                   "C5": (scenes.torus_scene, 3840, 2160, 16)}[cfg]
 ds = DeviceScene(scene())
 info = ds.info()
