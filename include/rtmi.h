@@ -192,6 +192,11 @@ typedef struct rt_options {
  * general pixels with the general batched kernel instead of the one
  * specialised for them. Scheduling only: same image and Stats. */
 #define RT_FLAG_NO_GEN1 0x100u
+/* _device calls with out == NULL: the caller will not read this call's Stats
+ * (rt_scene_last_stats then fails), so the per-call Stats reduction is not
+ * launched — the render kernels are all the call puts on the stream. Ignored
+ * when out != NULL or with RT_FLAG_COUNT_TRAVERSAL. */
+#define RT_FLAG_NO_STATS 0x200u
 
 /* Stats (src/renderer/stats.nim:4-13) plus ray counts for Mray/s. */
 typedef struct rt_stats {
@@ -295,7 +300,8 @@ int rt_band_rows(int32_t height, int32_t band_h, int32_t world,
                  int32_t *out_rows);
 
 /* Stats of the last render call on this scene (waits for it): for
- * asynchronous _device calls made with out == NULL. */
+ * asynchronous _device calls made with out == NULL (RT_E_INVALID if that
+ * call set RT_FLAG_NO_STATS). */
 int rt_scene_last_stats(rt_scene *scene, rt_stats *out);
 
 /* ---- one process, several GPUs (SURVEY.md 8(b) rt_render_frame_multi) ---- */

@@ -145,6 +145,7 @@ struct rt_scene {
   hipEvent_t fork = nullptr, join = nullptr;
   int64_t last_lean = 0, last_general = 0;  // rt_scene_last_split
   int32_t last_lean_kind = 0;                // rt_scene_last_lean_kernel
+  bool stats_kept = true;                    // the last call reduced its Stats (no RT_FLAG_NO_STATS)
   int64_t last_batched = 0, last_fallback = -1;  // rt_scene_last_batch
   int32_t nobj = 0, nlight = 0, nmesh = 0;
   int32_t shadow_mesh = -1;  // the only mesh object, or -1 (FastParams.shadow_mesh)
@@ -1506,7 +1507,7 @@ bool lean1_ok(const rt_scene* s, const rt_options* o, const FastParams& p, unsig
          p.iters * 64 == p.spp && p.iters % 4 == 0 && s->nobj == 2;
 }
 
-int launch(rt_scene* s, const rt_options* o, const Mapping& mp, float* d_out, hipStream_t st) {
+int launch(rt_scene* s, const rt_options* o, const Mapping& mp, float* d_out, hipStream_t st, bool reduce) {
   int blocks = 1;
   if (o->precision == RT_FP64) {
     RenderParams<double> p;
@@ -1636,6 +1637,7 @@ int launch(rt_scene* s, const rt_options* o, const Mapping& mp, float* d_out, hi
       }
     }
   }
+  if (!reduce) return RT_OK;  // nobody reads this call's Stats: no reduction launch
   const int e = rtmi_launch_reduce_stats(s->partials.p, blocks * 4, s->acc.p, st);
   if (e) return fail(RT_E_DEVICE, "stats reduction launch failed: %s", hipGetErrorString((hipError_t)e));
   return RT_OK;
@@ -1674,14 +1676,18 @@ struct DeviceGuard {
 };
 
 // Common device-side body: order after the previous call, clear the
-// counters, launch, record completion.
+// counters, launch, record completion. With RT_FLAG_NO_STATS (and no `out`,
+// no traversal counting) the call's Stats are not reduced: it launches its
+// render kernels and nothing else, and rt_scene_last_stats reports that.
 int render_device(rt_scene* s, const rt_options* o, const Mapping& mp, float* d_out, hipStream_t st,
-                  rt_stats* out) {
+                  rt_stats* out, bool need_stats = false) {
+  const bool reduce = need_stats || out || !(o->flags & RT_FLAG_NO_STATS) || (o->flags & RT_FLAG_COUNT_TRAVERSAL);
+  s->stats_kept = reduce;
   HIP_TRY(hipStreamWaitEvent(st, s->done, 0));
-  HIP_TRY(hipMemsetAsync(s->acc.p, 0, kStatSlots * sizeof(unsigned long long), st));
+  if (reduce) HIP_TRY(hipMemsetAsync(s->acc.p, 0, kStatSlots * sizeof(unsigned long long), st));
   if (o->precision == RT_FP32)
     HIP_TRY(hipMemsetAsync(s->queue.p, 0, (size_t)2 * kQueueShards * kQueueStride * sizeof(unsigned int), st));
-  int rc = launch(s, o, mp, d_out, st);
+  int rc = launch(s, o, mp, d_out, st, reduce);
   if (rc) return rc;
   HIP_TRY(hipEventRecord(s->done, st));
   if (out) return read_stats(s, st, out);
@@ -1742,7 +1748,7 @@ extern "C" int rt_render_lines(rt_scene* s, const rt_options* o, float* fb, int3
   const size_t off = (size_t)r0 * o->width * 3, cnt = (size_t)(r1 - r0) * o->width * 3;
   hipStream_t st = s->stream;
   HIP_TRY(hipMemcpyAsync(s->fb_scratch.p + off, fb + off, cnt * sizeof(float), hipMemcpyHostToDevice, st));
-  if ((rc = render_device(s, o, mp, s->fb_scratch.p, st, nullptr))) return rc;
+  if ((rc = render_device(s, o, mp, s->fb_scratch.p, st, nullptr, true))) return rc;
   HIP_TRY(hipMemcpyAsync(fb + off, s->fb_scratch.p + off, cnt * sizeof(float), hipMemcpyDeviceToHost, st));
   if ((rc = read_stats(s, st, &local))) return rc;
   if (out) *out = local;
@@ -1776,6 +1782,7 @@ extern "C" int rt_render_bands_device(rt_scene* s, const rt_options* o, float* d
 extern "C" int rt_scene_last_stats(rt_scene* s, rt_stats* out) {
   if (!s || !out) return fail(RT_E_INVALID, "null argument");
   std::lock_guard<std::mutex> lk(s->mu);
+  if (!s->stats_kept) return fail(RT_E_INVALID, "the last render call set RT_FLAG_NO_STATS");
   DeviceGuard g(s->device);
   HIP_TRY(hipStreamWaitEvent(s->stream, s->done, 0));
   return read_stats(s, s->stream, out);

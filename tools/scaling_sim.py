@@ -16,7 +16,8 @@ from rtmi.renderer import DeviceScene  # noqa: E402
 W, H, M = 1920, 1080, 16
 REPS = int(os.environ.get("REPS", "5"))
 ds = DeviceScene(scenes.mesh_bunny())
-opts = Options(width=W, height=H, antialias=Antialias(akGrid, M), bias=1e-4, precision=Precision.fp32)
+opts = Options(width=W, height=H, antialias=Antialias(akGrid, M), bias=1e-4, precision=Precision.fp32,
+               flags=int(os.environ.get("RTMI_FLAGS", "0"), 0))
 stream = torch.cuda.current_stream()
 for band_h in [int(b) for b in os.environ.get("BANDS", "16,8,4").split(",")]:
     res = {"band_h": band_h}
