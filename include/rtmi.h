@@ -197,6 +197,10 @@ typedef struct rt_options {
  * launched — the render kernels are all the call puts on the stream. Ignored
  * when out != NULL or with RT_FLAG_COUNT_TRAVERSAL. */
 #define RT_FLAG_NO_STATS 0x200u
+/* float32 kernel, one-plane two-class launches: launch the general and the
+ * lean pixels' kernels separately. By default both lists run in one merged
+ * kernel (general items first, then lean ones). Same image and Stats. */
+#define RT_FLAG_NO_MIX 0x400u
 
 /* Stats (src/renderer/stats.nim:4-13) plus ray counts for Mray/s. */
 typedef struct rt_stats {
@@ -430,7 +434,8 @@ int rt_scene_last_batch(rt_scene *scene, int64_t *batched_groups, int64_t *fallb
  * pixels' (0 none — no two-class launch, 1 the general lean kernel, 2 the
  * one-plane lean kernel, RT_FLAG_NO_LEAN1), bits 2-3 the general pixels'
  * (0 the one-sample kernel, 1 the general batched kernel, 2 the one-plane
- * batched kernel, RT_FLAG_NO_GEN1). Host-side bookkeeping, no wait. */
+ * batched kernel, RT_FLAG_NO_GEN1); 3 in both: the merged one-plane kernel
+ * (RT_FLAG_NO_MIX). Host-side bookkeeping, no wait. */
 int rt_scene_last_lean_kernel(rt_scene *scene, int32_t *kind);
 
 /* ---- helpers ----------------------------------------------------------- */

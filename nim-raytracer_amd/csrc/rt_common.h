@@ -248,6 +248,9 @@ struct FastParams {
   uint32_t tx_magic;               // g / tiles_x == (g * tx_magic) >> tx_shift for 0 <= g < 2^31
   int32_t tx_shift;
   int32_t stat_flush;              // work items between flushes of the 32-bit wave Stats counters
+  // k_render_mix1's second list (lean pixels, k_render_lean1q items) and its shard count
+  const int32_t* order2;
+  int32_t ngroups2, shards2;
 };
 
 enum : int32_t {
@@ -282,6 +285,8 @@ int rtmi_lean1_f32_blocks_per_cu(int nl);
 int rtmi_lean1_quads();
 int rtmi_launch_gen1_f32(const rtmi::FastParams* p, int nl, int blocks, void* stream);
 int rtmi_gen1_f32_blocks_per_cu(int nl);
+int rtmi_launch_mix1_f32(const rtmi::FastParams* p, int nl, int lp, int blocks, void* stream);
+int rtmi_mix1_f32_blocks_per_cu(int nl);
 int rtmi_launch_gen_f32(const rtmi::FastParams* p, unsigned subset, int blocks, size_t shmem, void* stream);
 int rtmi_gen_f32_blocks_per_cu(unsigned subset, size_t shmem);
 int rtmi_launch_ppm_encode(const float* fb, long long n, int bits, int srgb, void* out, void* stream);

@@ -2439,27 +2439,22 @@ __device__ __forceinline__ GroupPix lane_pixel(KP p, int g) {
 // bit for bit, with no per-pixel wave reduction and the per-pixel set-up
 // spread over 64 / LP pixels at once. LP = 4 (16 pixels per item) for whole
 // frames, 16 (4 per item) for short launches (rtmi.cpp).
+// k_render_lean1q's work loop over one list (order: 64 / LP entries per
+// item, ngroups items, dequeued from the shard heads at `queue`); also the
+// second phase of k_render_mix1.
 template <int NL, int LP>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k_render_lean1q(
-    const FastParams params_by_value) {
-  (void)params_by_value;
-  const KP p = params();
-  __shared__ unsigned long long lds_tot[4][kStatSlots];
-  const int wib = (int)(threadIdx.x >> 6);
+__device__ __forceinline__ void lean1q_loop(KP p, const int32_t* order, int ngroups, unsigned int* queue, int shards,
+                                            Stats32& ws, unsigned long long* tot, int& nflush) {
   const int lane = (int)__lane_id();
-  if (lane < kStatSlots) lds_tot[wib][lane] = 0ull;
-  Stats32 ws;
-#pragma unroll
-  for (int k = 0; k < kStatSlots; ++k) ws.v[k] = 0u;
-  const int shard = (int)(blockIdx.x % (unsigned int)p->shards);
-  unsigned int* head = p->queue + shard * kQueueStride;
+  const int shard = (int)(blockIdx.x % (unsigned int)shards);
+  unsigned int* head = queue + shard * kQueueStride;
   int qj = 0;
   if (lane == 0) qj = (int)atomicAdd(head, 1u);
   qj = __builtin_amdgcn_readfirstlane(qj);
   int qj_next = 0;
   if (lane == 0) qj_next = (int)atomicAdd(head, 1u);
-  int g = qj * p->shards + shard;
-  int nflush = 0;
+  int g = qj * shards + shard;
+  if (g >= ngroups) return;
   const int iters = p->iters;
   const int po = p->shadow_mesh == 0 ? 1 : 0;
   const FObj pl = at(p->objs, po);
@@ -2479,7 +2474,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
   }
   const F3 alb = f3(plx.albedo_pi[0], plx.albedo_pi[1], plx.albedo_pi[2]);
   F3 bg = f3(p->bg[0], p->bg[1], p->bg[2]);
-  // the background in VGPRs for the whole kernel: a select against an SGPR
+  // the background in VGPRs for the whole loop: a select against an SGPR
   // operand with the mask in VCC needs a v_mov per use (constant bus)
   asm volatile("" : "+v"(bg.x), "+v"(bg.y), "+v"(bg.z));
   const int mm = p->grid_m - 1, lg = p->log2_grid_m;
@@ -2488,8 +2483,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
   constexpr int V = 64 / LP;   // virtual lanes per lane
   constexpr int PPI = 64 / LP; // pixels per work item
   const int q = lane & (LP - 1);  // this lane's share of its pixel's virtual lanes
-  while (g < p->ngroups) {
-    const int gg = p->order[g * PPI + lane / LP];  // this lane's pixel (list entry; -1: padding)
+  while (g < ngroups) {
+    const int gg = order[g * PPI + lane / LP];  // this lane's pixel (list entry; -1: padding)
     qj = __builtin_amdgcn_readfirstlane(qj_next);
     if (lane == 0) qj_next = (int)atomicAdd(head, 1u);
     const unsigned long long vmask = bal(gg >= 0);
@@ -2588,11 +2583,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
     ws.v[STAT_SHADOW] += (unsigned)NL * nlit;
     ws.v[STAT_HITS] += nlit + nocc;
     if (++nflush >= p->stat_flush) {
-      flush_stats(ws, lds_tot[wib], lane);
+      flush_stats(ws, tot, lane);
       nflush = 0;
     }
-    g = qj * p->shards + shard;
+    g = qj * shards + shard;
   }
+}
+
+template <int NL, int LP>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k_render_lean1q(
+    const FastParams params_by_value) {
+  (void)params_by_value;
+  const KP p = params();
+  __shared__ unsigned long long lds_tot[4][kStatSlots];
+  const int wib = (int)(threadIdx.x >> 6);
+  const int lane = (int)__lane_id();
+  if (lane < kStatSlots) lds_tot[wib][lane] = 0ull;
+  Stats32 ws;
+#pragma unroll
+  for (int k = 0; k < kStatSlots; ++k) ws.v[k] = 0u;
+  int nflush = 0;
+  lean1q_loop<NL, LP>(p, p->order, p->ngroups, p->queue, p->shards, ws, lds_tot[wib], nflush);
   flush_stats(ws, lds_tot[wib], lane);
   const int wave = (int)(blockIdx.x * (blockDim.x >> 6) + threadIdx.x / 64u);
   if (lane < kStatSlots) p->partials[(size_t)wave * kStatSlots + lane] = lds_tot[wib][lane];
@@ -2697,20 +2708,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RTMI_GEN_WA
 #ifndef RTMI_GEN1_WAVES
 #define RTMI_GEN1_WAVES 7
 #endif
+// k_render_gen1's work loop over the primary list (p->order, p->ngroups,
+// the shard heads at p->queue); also the first phase of k_render_mix1.
 template <int NL>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RTMI_GEN1_WAVES))) void k_render_gen1(
-    const FastParams params_by_value) {
-  (void)params_by_value;
+__device__ __forceinline__ void gen1_loop(KP p, LdsF* ls, Stats32& ws, unsigned long long* tot, int& nflush) {
   constexpr unsigned F = F_PLANE | F_MESH;
-  KP p = params();
-  __shared__ float lds[4][kLdsSlots][64];  // shade_path's scratch (the fallback)
-  __shared__ unsigned long long lds_tot[4][kStatSlots];
-  const int wib = (int)(threadIdx.x >> 6);
-  LdsF* ls = (LdsF*)&lds[wib][0][__lane_id()];
-  if (__lane_id() < (unsigned)kStatSlots) lds_tot[wib][__lane_id()] = 0ull;
-  Stats32 ws;
-#pragma unroll
-  for (int k = 0; k < kStatSlots; ++k) ws.v[k] = 0u;
   const int shard = (int)(blockIdx.x % (unsigned int)p->shards);
   unsigned int* head = p->queue + shard * kQueueStride;
   int qj = 0;
@@ -2719,7 +2721,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RTMI_GEN1_W
   int qj_next = 0;
   if (__lane_id() == 0) qj_next = (int)atomicAdd(head, 1u);
   int g = qj * p->shards + shard;
-  int nflush = 0;
   while (g < p->ngroups) {
     p = params();
     const int iters = p->iters;
@@ -2758,13 +2759,62 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RTMI_GEN1_W
     finish_item(p, gp, acc.v, 64);
     const int lane = lane_id_fresh();
     if (++nflush >= p->stat_flush) {
-      flush_stats(ws, lds_tot[wib], lane);
+      flush_stats(ws, tot, lane);
       nflush = 0;
     }
     qj = __builtin_amdgcn_readfirstlane(qj_next);
     if (lane == 0) qj_next = (int)atomicAdd(head, 1u);
     g = qj * p->shards + shard;
   }
+}
+
+template <int NL>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RTMI_GEN1_WAVES))) void k_render_gen1(
+    const FastParams params_by_value) {
+  (void)params_by_value;
+  KP p = params();
+  __shared__ float lds[4][kLdsSlots][64];  // shade_path's scratch (the fallback)
+  __shared__ unsigned long long lds_tot[4][kStatSlots];
+  const int wib = (int)(threadIdx.x >> 6);
+  LdsF* ls = (LdsF*)&lds[wib][0][__lane_id()];
+  if (__lane_id() < (unsigned)kStatSlots) lds_tot[wib][__lane_id()] = 0ull;
+  Stats32 ws;
+#pragma unroll
+  for (int k = 0; k < kStatSlots; ++k) ws.v[k] = 0u;
+  int nflush = 0;
+  gen1_loop<NL>(p, ls, ws, lds_tot[wib], nflush);
+  p = params();
+  const int lane = (int)__lane_id();
+  flush_stats(ws, lds_tot[wib], lane);
+  const int wave = (int)(blockIdx.x * (blockDim.x >> 6) + threadIdx.x / 64u);
+  if (lane < kStatSlots) p->partials[(size_t)wave * kStatSlots + lane] = lds_tot[wib][lane];
+}
+
+// Both classes of a one-plane two-class launch in ONE kernel (short
+// launches, rtmi.cpp): every wave takes general pixels (k_render_gen1's
+// items, p->order / p->ngroups) until that list is exhausted, then lean
+// pixels (k_render_lean1q's items, p->order2 / p->ngroups2 from the second
+// set of queue heads) — one ramp and one tail per launch instead of two, the
+// expensive items first and the cheap ones filling the tail. Frames and
+// Stats those of the two kernels.
+template <int NL, int LP>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RTMI_GEN1_WAVES))) void k_render_mix1(
+    const FastParams params_by_value) {
+  (void)params_by_value;
+  KP p = params();
+  __shared__ float lds[4][kLdsSlots][64];
+  __shared__ unsigned long long lds_tot[4][kStatSlots];
+  const int wib = (int)(threadIdx.x >> 6);
+  LdsF* ls = (LdsF*)&lds[wib][0][__lane_id()];
+  if (__lane_id() < (unsigned)kStatSlots) lds_tot[wib][__lane_id()] = 0ull;
+  Stats32 ws;
+#pragma unroll
+  for (int k = 0; k < kStatSlots; ++k) ws.v[k] = 0u;
+  int nflush = 0;
+  gen1_loop<NL>(p, ls, ws, lds_tot[wib], nflush);
+  p = params();
+  lean1q_loop<NL, LP>(p, p->order2, p->ngroups2, p->queue + kQueueShards * kQueueStride, p->shards2, ws,
+                      lds_tot[wib], nflush);
   p = params();
   const int lane = (int)__lane_id();
   flush_stats(ws, lds_tot[wib], lane);

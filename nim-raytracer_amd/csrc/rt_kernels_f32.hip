@@ -65,6 +65,11 @@ template __global__ void fast::k_render_lean1q<2, 16>(const FastParams);
 // general pixels of the same scenes
 template __global__ void fast::k_render_gen1<1>(const FastParams);
 template __global__ void fast::k_render_gen1<2>(const FastParams);
+// both classes of a one-plane launch in one kernel
+template __global__ void fast::k_render_mix1<1, 4>(const FastParams);
+template __global__ void fast::k_render_mix1<2, 4>(const FastParams);
+template __global__ void fast::k_render_mix1<1, 16>(const FastParams);
+template __global__ void fast::k_render_mix1<2, 16>(const FastParams);
 
 }  // namespace rtmi
 
@@ -182,6 +187,30 @@ extern "C" int rtmi_launch_gen1_f32(const rtmi::FastParams* p, int nl, int block
   else
     return (int)hipErrorInvalidValue;
   return (int)hipGetLastError();
+}
+
+// The one-plane merged kernel (general items, then lean items with lp lanes per pixel).
+extern "C" int rtmi_launch_mix1_f32(const rtmi::FastParams* p, int nl, int lp, int blocks, void* stream) {
+  using namespace rtmi::fast;
+  if (nl == 1 && lp == 4)
+    hipLaunchKernelGGL((k_render_mix1<1, 4>), dim3(blocks), dim3(256), 0, (hipStream_t)stream, *p);
+  else if (nl == 2 && lp == 4)
+    hipLaunchKernelGGL((k_render_mix1<2, 4>), dim3(blocks), dim3(256), 0, (hipStream_t)stream, *p);
+  else if (nl == 1 && lp == 16)
+    hipLaunchKernelGGL((k_render_mix1<1, 16>), dim3(blocks), dim3(256), 0, (hipStream_t)stream, *p);
+  else if (nl == 2 && lp == 16)
+    hipLaunchKernelGGL((k_render_mix1<2, 16>), dim3(blocks), dim3(256), 0, (hipStream_t)stream, *p);
+  else
+    return (int)hipErrorInvalidValue;
+  return (int)hipGetLastError();
+}
+
+extern "C" int rtmi_mix1_f32_blocks_per_cu(int nl) {
+  int nb = 0;
+  const hipError_t e = nl == 1
+      ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, rtmi::fast::k_render_mix1<1, 4>, 256, 0)
+      : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, rtmi::fast::k_render_mix1<2, 4>, 256, 0);
+  return e == hipSuccess && nb > 0 ? nb : 1;
 }
 
 extern "C" int rtmi_gen1_f32_blocks_per_cu(int nl) {

@@ -1500,6 +1500,18 @@ rt_scene::Split* split_lists(rt_scene* s, const rt_options* o, const Mapping& mp
 // of every lane (spp a multiple of 256): every sample is valid and a lane's
 // samples share one column. Off with RT_FLAG_NO_LEAN1. The general pixels of
 // the same launches go to k_render_gen1 (off with RT_FLAG_NO_GEN1).
+// Whether a one-plane two-class launch runs as one merged kernel
+// (k_render_mix1). RTMI_MIX=0/1 forces it (diagnostic A/B); by default:
+// always.
+bool mix_policy(long long n_heavy, long long lean_items, const rt_scene* s) {
+  static const int force = std::getenv("RTMI_MIX") ? std::atoi(std::getenv("RTMI_MIX")) : -1;
+  (void)n_heavy;
+  (void)lean_items;
+  (void)s;
+  if (force >= 0) return force != 0;
+  return true;
+}
+
 bool lean1_ok(const rt_scene* s, const rt_options* o, const FastParams& p, unsigned sub) {
   return sub == SUB_MESH && p.nobj == 2 && p.shadow_mesh >= 0 &&
          (p.nlight == 1 || p.nlight == 2) && !p.has_point_light && p.aa_kind == RT_AA_GRID &&
@@ -1588,6 +1600,28 @@ int launch(rt_scene* s, const rt_options* o, const Mapping& mp, float* d_out, hi
       pl.shards = std::min(kQueueShards, lb);
       pl.queue = s->queue.p + (size_t)kQueueShards * kQueueStride;
       pl.partials = s->partials.p + (size_t)hb * 4 * kStatSlots;
+      // one-plane launches: both lists in one kernel (k_render_mix1: the
+      // general items first, then the lean ones) — one ramp and one tail
+      const bool mix = gen1 && lean1 && lp != 64 && !(o->flags & RT_FLAG_NO_MIX) && mix_policy(sp->n_heavy, lruns, s);
+      if (mix) {
+        FastParams pm = ph;
+        pm.order2 = pl.order;
+        pm.ngroups2 = pl.ngroups;
+        pm.stat_flush = std::min(ph.stat_flush, pl.stat_flush);
+        const long long mcap = (long long)rtmi_mix1_f32_blocks_per_cu(p.nlight) * s->num_cus;
+        const int mb = (int)std::max(1LL, std::min<long long>(std::min<long long>(mcap, blocks),
+                                                              ((long long)sp->n_heavy + lruns + 3) / 4));
+        pm.shards = std::min(kQueueShards, mb);
+        pm.shards2 = pm.shards;
+        const int e = rtmi_launch_mix1_f32(&pm, p.nlight, lp, mb, st);
+        if (e) return fail(RT_E_DEVICE, "render kernel launch failed: %s", hipGetErrorString((hipError_t)e));
+        blocks = mb;
+        s->last_lean = sp->n_lean;
+        s->last_lean_kind = 3 | (3 << 2);
+        s->last_general = sp->n_heavy;
+        s->last_batched = sp->n_heavy;
+        goto launched;
+      }
       // general kernel first on the caller's stream, the lean kernel on
       // the scene's aux stream (forked after the caller's earlier work,
       // joined before its later work)
@@ -1625,6 +1659,7 @@ int launch(rt_scene* s, const rt_options* o, const Mapping& mp, float* d_out, hi
       const int e = rtmi_launch_render_f32(&p, f32_subset(s, o), blocks, f32_table_lds(o), st);
       if (e) return fail(RT_E_DEVICE, "render kernel launch failed: %s", hipGetErrorString((hipError_t)e));
     }
+  launched:
     if (measuring) HIP_TRY(hipEventRecord(measuring->measured, st));
     if (dbg_cost.p) {
       std::vector<unsigned> c((size_t)p.ngroups);

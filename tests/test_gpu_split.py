@@ -17,7 +17,7 @@ import pytest
 
 from rtmi import Antialias, Options, Precision, akGrid, scenes
 from rtmi.abi import (RT_FLAG_BATCH_FALLBACK, RT_FLAG_NO_BATCH, RT_FLAG_NO_BINNING, RT_FLAG_NO_GEN1,
-                      RT_FLAG_NO_LEAN1, RT_FLAG_NO_REORDER, RT_FLAG_NO_SPLIT)
+                      RT_FLAG_NO_LEAN1, RT_FLAG_NO_MIX, RT_FLAG_NO_REORDER, RT_FLAG_NO_SPLIT)
 from rtmi.dist import band_rows
 from rtmi.glm import X_AXIS, degToRad, inverse, mat4, rotate, translate, vec3
 from rtmi.renderer import DeviceScene
@@ -25,7 +25,7 @@ from rtmi.scene import akCorrelatedMultiJittered, akJittered, akMultiJittered
 
 pytestmark = pytest.mark.gpu
 
-FLAG_SETS = (0, RT_FLAG_NO_LEAN1, RT_FLAG_NO_GEN1, RT_FLAG_NO_BATCH, RT_FLAG_BATCH_FALLBACK, RT_FLAG_NO_SPLIT, RT_FLAG_NO_BINNING)
+FLAG_SETS = (0, RT_FLAG_NO_MIX, RT_FLAG_NO_LEAN1, RT_FLAG_NO_GEN1, RT_FLAG_NO_BATCH, RT_FLAG_BATCH_FALLBACK, RT_FLAG_NO_SPLIT, RT_FLAG_NO_BINNING)
 
 
 def _opts(w, h, m, flags=0, aa=akGrid, bias=1e-4, seed=0):
@@ -147,6 +147,8 @@ def test_split_full_c3(gpu):
     assert lean + general == 1920 * 1080 and lean > 0.8 * 1920 * 1080, (lean, general)
     batched, fallback = ds.last_batch()
     assert batched == general and 0 <= fallback < 0.05 * general, (batched, fallback, general)
+    assert ds.last_lean_kernel() == 3 | 3 << 2  # the merged one-plane kernel
+    ds.render_device(_opts(1920, 1080, 16, RT_FLAG_NO_MIX), fb)
     assert ds.last_lean_kernel() == 2 | 2 << 2  # the one-plane lean and general kernels
     ds.render_device(_opts(1920, 1080, 16, RT_FLAG_NO_LEAN1), fb)
     assert ds.last_lean_kernel() == 1 | 2 << 2
@@ -168,7 +170,7 @@ def test_lean1_kernel_choice(gpu, m):
     for scene, want in ((scenes.mesh_bunny(), 2 | 2 << 2), (one, 2 | 2 << 2), (_reflective_ground(False), 0)):
         ds = DeviceScene(scene)
         fb = torch.zeros(256 * 144 * 3, dtype=torch.float32, device="cuda")
-        st = ds.render_device(_opts(256, 144, m), fb)
+        st = ds.render_device(_opts(256, 144, m, RT_FLAG_NO_MIX), fb)
         assert ds.last_lean_kernel() == want, (want, ds.last_lean_kernel())
         fb2 = torch.zeros_like(fb)
         st2 = ds.render_device(_opts(256, 144, m, RT_FLAG_NO_LEAN1 | RT_FLAG_NO_GEN1), fb2)
@@ -177,6 +179,8 @@ def test_lean1_kernel_choice(gpu, m):
     fb = torch.zeros(256 * 144 * 3, dtype=torch.float32, device="cuda")
     ds.render_device(_opts(256, 144, 8), fb)  # 64 spp: one iteration, no whole batch of 4
     assert ds.last_lean_kernel() == 1 | 1 << 2
+    ds.render_device(_opts(256, 144, 16), fb)  # the merged kernel by default
+    assert ds.last_lean_kernel() == 3 | 3 << 2
 
 
 def test_no_split_without_records(gpu):
