@@ -15,10 +15,11 @@ overlapping frame k+1's render from a second band buffer).
 
 Printed (rank 0, one JSON line): value = (primary + shadow rays of all ranks)
 x K / max-over-ranks wall time, plus
-  roofline     — the render call (two-class launches: the lean-pixel kernel
-                 k_render_lean + the batched general-pixel kernel
-                 k_render_gen, or k_render_fast where those do not apply), HIP
-                 events on the stream it runs on, against the 8 TB/s HBM peak.
+  roofline     — the render call (C3-C5, one mesh on one ground plane: the
+                 merged kernel k_render_mix1 — general pixels, then lean
+                 pixels; elsewhere the two-class launch k_render_gen +
+                 k_render_lean, or k_render_fast), HIP events on the stream it
+                 runs on, against the 8 TB/s HBM peak.
                  `achieved` = SURVEY 8(d)'s algorithmic bytes per ray — 32 B
                  per BVH box and 36 B per triangle the ray is tested against,
                  + 12 B per pixel — summed over the rays with the per-lane
@@ -292,6 +293,12 @@ def main():
         elapsed = float(e.item())
     kern_ms = sum(a.elapsed_time(b) for a, b in evs) / max(1, args.steps)
     lean_groups, general_groups = ds.last_split()
+    kinds = ds.last_lean_kernel()
+    lean_k = {0: None, 1: "k_render_lean", 2: "k_render_lean1q (one-plane lean pixels)", 3: None}[kinds & 3]
+    gen_k = {0: "k_render_fast<false>", 1: "k_render_gen", 2: "k_render_gen1 (one-plane general pixels)",
+             3: None}[kinds >> 2 & 3]
+    kernel_desc = ("k_render_mix1 (one-plane scene: general pixels, then lean pixels, one merged kernel)"
+                   if kinds == 15 else f"{gen_k} + {lean_k} (two-class launch)" if lean_k else gen_k)
     # outside the timed region: one more launch with Stats, for how many of
     # the batched general pixels fell back to the one-sample loop
     ds.render_bands_device(opts, local_bufs[0], BAND_H, rank, world, stream=stream, stats=True)
@@ -370,9 +377,7 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
-                "kernel": ("render call: " + ("k_render_lean + k_render_gen (two-class launch)" if batched_groups
-                                              else "k_render_lean + k_render_fast<false> (two-class launch)"
-                                              if lean_groups else "k_render_fast<false>")),
+                "kernel": "render call: " + kernel_desc,
                 "kernel_ms": round(kern_ms, 4),
                 "bytes_per_launch": int(bytes_launch),
                 "definition": ("SURVEY 8(d) per-ray bytes (32 B/BVH box + 36 B/triangle tested, 12 B/pixel) over "

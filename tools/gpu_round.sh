@@ -9,7 +9,7 @@ export TMPDIR=/tmp
 R=${ROUND:-r2}
 O=gpurun_out/round
 mkdir -p $O/pmc
-K='k_render_fast<false|k_render_lean<|k_render_gen<'
+K='k_render_fast<false|k_render_lean|k_render_gen|k_render_mix1'
 timeout -k 10 700 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread > $O/tests.log 2>&1 && \
 timeout -k 10 600 python bench.py > $O/bench_c3.json 2> $O/bench_c3.err && \
 timeout -k 10 300 python bench.py --config C2 > $O/bench_c2.json 2> $O/bench_c2.err && \

@@ -19,7 +19,7 @@ import re
 import sys
 
 # the render call's kernels (a regex on the kernel name)
-KERNEL = r"k_render_fast<false|k_render_lean<|k_render_gen<"
+KERNEL = r"k_render_fast<false|k_render_lean|k_render_gen|k_render_mix1"
 
 
 def means(path, kernel=None):
