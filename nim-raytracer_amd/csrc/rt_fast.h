@@ -177,6 +177,27 @@ __device__ __forceinline__ float plane(F3 o, F3 d) {
   return fabsf(d.y) > 1e-6f ? -o.y * rcp(d.y) : -finf();
 }
 
+// A TriFast record as ONE s_load_dwordx16 (the compiler otherwise splits the
+// record into per-field loads — up to eight SMEM instructions per face in
+// the batched list searches — since a face test reads 13 of its 16 dwords):
+// the pad dwords are marked live so the load stays whole.
+struct TriRegs {
+  float v0[3], e2[3], e1n[3], nn[3];
+  unsigned int id;
+};
+__device__ __forceinline__ TriRegs load_tri(const RT_CONST TriFast* t) {
+  using V16 = unsigned int __attribute__((ext_vector_type(16)));
+  const V16 r = *(const RT_CONST V16*)t;
+  asm volatile("" ::"s"(r[7]), "s"(r[11]), "s"(r[15]));
+  TriRegs T;
+  T.v0[0] = __uint_as_float(r[0]), T.v0[1] = __uint_as_float(r[1]), T.v0[2] = __uint_as_float(r[2]);
+  T.id = r[3];
+  T.e2[0] = __uint_as_float(r[4]), T.e2[1] = __uint_as_float(r[5]), T.e2[2] = __uint_as_float(r[6]);
+  T.e1n[0] = __uint_as_float(r[8]), T.e1n[1] = __uint_as_float(r[9]), T.e1n[2] = __uint_as_float(r[10]);
+  T.nn[0] = __uint_as_float(r[12]), T.nn[1] = __uint_as_float(r[13]), T.nn[2] = __uint_as_float(r[14]);
+  return T;
+}
+
 // Closest hit as ONE 64-bit key: float bits of t in the high word, the
 // triangle's face index in the low word. For t >= 0 the float bits order like
 // unsigned integers, so key order is the reference's "smaller t, then lower
@@ -194,8 +215,8 @@ __device__ __forceinline__ unsigned long long tkey(float t, unsigned int lo) {
 // (scalar triple-product identities of the reference's p = d x e2,
 // q = tvec x e1 form). The barycentric range is tested unscaled in one min:
 // u >= 0, v >= 0, u + v <= 1 (u <= 1 is implied), det >= 1e-6.
-__device__ __forceinline__ void tri_test(const RT_CONST TriFast& T, F3 o, F3 d, unsigned long long& key,
-                                         float& tc) {
+template <class TR>
+__device__ __forceinline__ void tri_test(const TR& T, F3 o, F3 d, unsigned long long& key, float& tc) {
   const float tx = o.x - T.v0[0], ty = o.y - T.v0[1], tz = o.z - T.v0[2];
   const float cx = __builtin_fmaf(ty, d.z, -tz * d.y);
   const float cy = __builtin_fmaf(tz, d.x, -tx * d.z);
@@ -226,11 +247,11 @@ __device__ __forceinline__ const RT_CONST T* rec(KP p, int off) {
 __device__ __forceinline__ void leaf(KP p, int first, int n, F3 o, F3 d, unsigned long long& key,
                                      float& tc) {
   const RT_CONST TriFast* t = rec<TriFast>(p, first);
-  tri_test(t[0], o, d, key, tc);
+  tri_test(load_tri(t), o, d, key, tc);
 #pragma unroll
   for (int k = 1; k < kLeafMax; ++k) {
     if (k >= n) break;
-    tri_test(t[k], o, d, key, tc);
+    tri_test(load_tri(t + k), o, d, key, tc);
   }
 }
 
@@ -369,7 +390,7 @@ __device__ __forceinline__ void list_search(KP p, const int32_t* ent, int b, int
   return;  // diagnostic build only: the binned searches' share of the frame
 #endif
   if (early && b < e) {  // a light cell's first face alone (the one covering most of the cell)
-    tri_test(*rec<TriFast>(p, cp(ent)[b]), o, d, key, tc);
+    tri_test(load_tri(rec<TriFast>(p, cp(ent)[b])), o, d, key, tc);
     tc = tc <= stop ? -1.0f : tc;
     if (bal(tc >= 0.0f) == 0ull) return;
     ++b;
@@ -377,10 +398,10 @@ __device__ __forceinline__ void list_search(KP p, const int32_t* ent, int b, int
   for (int k = b; k < e; k += 4) {
     const RT_CONST int32_t* q = cp(ent) + k;
     const int r0 = q[0], r1 = q[1], r2 = q[2], r3 = q[3];
-    tri_test(*rec<TriFast>(p, r0), o, d, key, tc);
-    if (k + 1 < e) tri_test(*rec<TriFast>(p, r1), o, d, key, tc);
-    if (k + 2 < e) tri_test(*rec<TriFast>(p, r2), o, d, key, tc);
-    if (k + 3 < e) tri_test(*rec<TriFast>(p, r3), o, d, key, tc);
+    tri_test(load_tri(rec<TriFast>(p, r0)), o, d, key, tc);
+    if (k + 1 < e) tri_test(load_tri(rec<TriFast>(p, r1)), o, d, key, tc);
+    if (k + 2 < e) tri_test(load_tri(rec<TriFast>(p, r2)), o, d, key, tc);
+    if (k + 3 < e) tri_test(load_tri(rec<TriFast>(p, r3)), o, d, key, tc);
     if (early) {
       tc = tc <= stop ? -1.0f : tc;
       if (bal(tc >= 0.0f) == 0ull) break;
@@ -1317,7 +1338,8 @@ __device__ __forceinline__ void lean_batch(KP p, const GroupPix& gp, int it0, co
 // t's float bits replace the (t, face) key — a tie never changes t, so t,
 // the culling limit tc and "found" follow tri_test's exactly. A lane that
 // takes no part holds best = +0.0 (nothing is below it).
-__device__ __forceinline__ void tri_test_t(const RT_CONST TriFast& T, F3 o, F3 d, float& best, float& tc) {
+template <class TR>
+__device__ __forceinline__ void tri_test_t(const TR& T, F3 o, F3 d, float& best, float& tc) {
   const float tx = o.x - T.v0[0], ty = o.y - T.v0[1], tz = o.z - T.v0[2];
   const float cx = __builtin_fmaf(ty, d.z, -tz * d.y);
   const float cy = __builtin_fmaf(tz, d.x, -tx * d.z);
@@ -1352,7 +1374,7 @@ __device__ __forceinline__ int list_search_batch(KP p, const int32_t* ent, int b
     // a cell's first face alone: it is the one covering most of the cell
     // (rt_bins.cpp), so lanes in the umbra retire after one test
     if (b < e) {
-      const RT_CONST TriFast& T = *rec<TriFast>(p, cp(ent)[b]);
+      const TriRegs T = load_tri(rec<TriFast>(p, cp(ent)[b]));
       unsigned long long left = 0ull;
 #pragma unroll
       for (int k = 0; k < S; ++k)
@@ -1371,7 +1393,7 @@ __device__ __forceinline__ int list_search_batch(KP p, const int32_t* ent, int b
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       if (j > 0 && k0 + j >= e) break;
-      const RT_CONST TriFast& T = *rec<TriFast>(p, r[j]);
+      const TriRegs T = load_tri(rec<TriFast>(p, r[j]));
 #pragma unroll
       for (int k = 0; k < S; ++k)
         if ((fl >> k) & 1u) {
@@ -1758,6 +1780,9 @@ __device__ __forceinline__ bool gen1_batch(KP p, const GroupPix& gp, int it0, un
   };
   auto camera_mesh = [&]() {
     if ((pinfo & kPixCount) == 0u || mob.root < 0) return;  // an empty pixel list: no camera ray can hit it
+#ifdef RTMI_DIAG_GEN_NOCAM
+    return;  // diagnostic build only (wrong images): the camera searches' share
+#endif
     F3 ro[S], rd[S];
     unsigned long long key[S], key0[S], anyp = 0ull, nomask[S];
     float tc[S], unused[S];
@@ -1870,6 +1895,9 @@ __device__ __forceinline__ bool gen1_batch(KP p, const GroupPix& gp, int it0, un
           anyp |= pm[k];
         }
         if (anyp == 0ull) return true;
+#ifdef RTMI_DIAG_GEN_NOSHADOWSEARCH
+        return true;  // diagnostic build only (wrong images): the gated shadow searches' share
+#endif
         const KP q = params();
         if (!q->grids || q->grids[li].gu <= 0) return false;
         // the exact early exit's stop: the plane after the mesh (if it is)
@@ -1921,6 +1949,9 @@ __device__ __forceinline__ bool gen1_batch(KP p, const GroupPix& gp, int it0, un
             wi.v[STAT_LANE_NODES] += pc(own[k]);  // diagnostic: rays in searched cells
 #endif
           }
+#ifdef RTMI_DIAG_GEN_NOTESTS
+          continue;  // diagnostic build only (wrong images): the cell loop without its face tests
+#endif
           const int nt = list_search_batch<S, false>(q, bent, cp(q->grid_off)[kb], cp(q->grid_off)[kb + 1], fl, ro, rd,
                                                      stop, own, unused, best, tc);
 #ifdef RTMI_DIAG_GEN_COUNT

@@ -159,8 +159,12 @@ struct rt_scene {
   PrecisionData<double> f64;
   DevBuf<BvhNode> nodes;
   DevBuf<unsigned long long> partials;
-  DevBuf<unsigned long long> acc;
-  DevBuf<unsigned int> queue;      // float32 work-queue heads (kQueueShards * kQueueStride)
+  // float32 work-queue heads (two sets of kQueueShards * kQueueStride: the
+  // general and the lean kernel), then the Stats accumulator: one buffer so
+  // a call clears both with one fill
+  DevBuf<unsigned int> queue;
+  static constexpr size_t kQueueWords = (size_t)2 * kQueueShards * kQueueStride;
+  unsigned long long* acc() const { return reinterpret_cast<unsigned long long*>(queue.p + kQueueWords); }
   DevBuf<double> f64_tables;       // float64 kernel per-lane stochastic sample tables
   struct Order {                   // one launch mapping's measured costs -> launch order
     std::array<int64_t, 17> key;
@@ -241,7 +245,6 @@ struct rt_scene {
     partials.release();
     queue.release();
     f64_tables.release();
-    acc.release();
     fb_scratch.release();
     grids.release();
     grid_off.release();
@@ -901,9 +904,8 @@ extern "C" int rt_scene_create(const rt_scene_desc* d, rt_scene** out_scene) {
   s->max_waves = s->num_cus * 8 * 4;  // 8 blocks of 4 waves per CU at most
   // two kernels per two-class launch: their waves' partial counters side by side
   if ((rc = s->partials.alloc((size_t)2 * s->max_waves * kStatSlots))) return rc;
-  if ((rc = s->acc.alloc(kStatSlots))) return rc;
-  if ((rc = s->queue.alloc((size_t)2 * kQueueShards * kQueueStride))) return rc;  // general + lean kernel
-  HIP_TRY(hipMemset(s->acc.p, 0, kStatSlots * sizeof(unsigned long long)));
+  if ((rc = s->queue.alloc(rt_scene::kQueueWords + 2 * (size_t)kStatSlots))) return rc;  // heads + Stats
+  HIP_TRY(hipMemset(s->queue.p, 0, s->queue.bytes()));
   HIP_TRY(hipDeviceSynchronize());
   mark("nodes + buffers");
   s->num_triangles = ntri;
@@ -934,8 +936,7 @@ extern "C" int rt_scene_get_info(const rt_scene* s, rt_scene_info* out) {
   out->max_bvh_depth = s->max_depth;
   out->device = s->device;
   out->device_bytes = (int64_t)(s->f32.bytes() + s->f64.bytes() + s->nodes.bytes() +
-                                s->partials.bytes() +
-                                s->acc.bytes());
+                                s->partials.bytes() + s->queue.bytes());
   out->build_ms = s->build_ms;
   return RT_OK;
 }
@@ -1673,14 +1674,14 @@ int launch(rt_scene* s, const rt_options* o, const Mapping& mp, float* d_out, hi
     }
   }
   if (!reduce) return RT_OK;  // nobody reads this call's Stats: no reduction launch
-  const int e = rtmi_launch_reduce_stats(s->partials.p, blocks * 4, s->acc.p, st);
+  const int e = rtmi_launch_reduce_stats(s->partials.p, blocks * 4, s->acc(), st);
   if (e) return fail(RT_E_DEVICE, "stats reduction launch failed: %s", hipGetErrorString((hipError_t)e));
   return RT_OK;
 }
 
 int read_stats(rt_scene* s, hipStream_t st, rt_stats* out) {
   unsigned long long h[kStatSlots];
-  HIP_TRY(hipMemcpyAsync(h, s->acc.p, sizeof h, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipMemcpyAsync(h, s->acc(), sizeof h, hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
   out->num_primary_rays = h[STAT_PRIMARY];
   // renderer.nim:54-56 counts one test per object per trace call, and every
@@ -1719,9 +1720,10 @@ int render_device(rt_scene* s, const rt_options* o, const Mapping& mp, float* d_
   const bool reduce = need_stats || out || !(o->flags & RT_FLAG_NO_STATS) || (o->flags & RT_FLAG_COUNT_TRAVERSAL);
   s->stats_kept = reduce;
   HIP_TRY(hipStreamWaitEvent(st, s->done, 0));
-  if (reduce) HIP_TRY(hipMemsetAsync(s->acc.p, 0, kStatSlots * sizeof(unsigned long long), st));
-  if (o->precision == RT_FP32)
-    HIP_TRY(hipMemsetAsync(s->queue.p, 0, (size_t)2 * kQueueShards * kQueueStride * sizeof(unsigned int), st));
+  // one fill: the queue heads (float32) and / or the Stats accumulator behind them
+  const size_t q0 = o->precision == RT_FP32 ? 0 : rt_scene::kQueueWords;
+  const size_t q1 = rt_scene::kQueueWords + (reduce ? 2 * (size_t)kStatSlots : 0);
+  if (q1 > q0) HIP_TRY(hipMemsetAsync(s->queue.p + q0, 0, (q1 - q0) * sizeof(unsigned int), st));
   int rc = launch(s, o, mp, d_out, st, reduce);
   if (rc) return rc;
   HIP_TRY(hipEventRecord(s->done, st));
@@ -1894,7 +1896,7 @@ extern "C" int rt_scene_last_counters(rt_scene* s, rt_traversal_counters* out) {
   DeviceGuard g(s->device);
   unsigned long long h[kStatSlots];
   HIP_TRY(hipEventSynchronize(s->done));
-  HIP_TRY(hipMemcpy(h, s->acc.p, sizeof h, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(h, s->acc(), sizeof h, hipMemcpyDeviceToHost));
   out->wave_node_fetches = h[STAT_NODE_FETCH];
   out->wave_tri_fetches = h[STAT_TRI_FETCH];
   out->lane_node_visits = h[STAT_LANE_NODES];
