@@ -2522,30 +2522,40 @@ __device__ __forceinline__ void lean1q_loop(KP p, const int32_t* order, int ngro
     const GroupPix gp = lane_pixel(p, gg >= 0 ? gg : 0);
     const float pxb = (float)gp.x, pyb = (float)gp.y;
     unsigned nlit = 0u, nocc = 0u;
-    // the binary-counter stack of the V virtual lanes' partial sums
-    F3 s0 = f3(0.0f, 0.0f, 0.0f), s1 = s0, s2 = s0, s3 = s0;
+    // the binary-counter stack of the V virtual lanes' partial sums, two
+    // virtual lanes at a time (two independent sample chains per step; their
+    // sum is the tree's first level)
+    F3 s1 = f3(0.0f, 0.0f, 0.0f), s2 = s1, s3 = s1, sum = s1;
+    static_assert(V % 2 == 0, "virtual lanes in pairs");
 #pragma unroll 1
-    for (int j = 0; j < V; ++j) {
-      const int jv = q * V + j;  // the virtual lane (k_render_lean1's lane)
-      const float px = pxb + __builtin_fmaf((float)(jv & mm), st, of);
-      const float cx = (px - p->cam_b) * p->cam_a;
-      const float q0 = __builtin_fmaf(cx, cx, 1.0f);
-      const float ay = __builtin_fmaf(cx, p->cam[4], -p->cam[10]);
-      // the sample row (it * 64 + jv) >> lg == it * (64 >> lg) + (jv >> lg)
-      // (m | 64), as a float stepped by 64 >> lg: exact small integers
-      float sjf = (float)(jv >> lg);
+    for (int j = 0; j < V; j += 2) {
+      float q0[2], ay[2], sjf[2];
+      F3 acc[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int jv = q * V + j + h;  // the virtual lane (k_render_lean1's lane)
+        const float px = pxb + __builtin_fmaf((float)(jv & mm), st, of);
+        const float cx = (px - p->cam_b) * p->cam_a;
+        q0[h] = __builtin_fmaf(cx, cx, 1.0f);
+        ay[h] = __builtin_fmaf(cx, p->cam[4], -p->cam[10]);
+        // the sample row (it * 64 + jv) >> lg == it * (64 >> lg) + (jv >> lg)
+        // (m | 64), as a float stepped by 64 >> lg: exact small integers
+        sjf[h] = (float)(jv >> lg);
+        acc[h] = f3(0.0f, 0.0f, 0.0f);
+      }
       const float rows = (float)(64 >> lg);
-      F3 acc = f3(0.0f, 0.0f, 0.0f);
       // iters is a multiple of 4 (rtmi.cpp lean1_ok): four samples per step
 #pragma unroll 1
       for (int it0 = 0; it0 < iters; it0 += 4)
 #pragma unroll
-      for (int it = it0; it < it0 + 4; ++it) {
-        const float py = pyb + __builtin_fmaf(sjf, st, of);
-        sjf += rows;
+      for (int it = it0; it < it0 + 4; ++it)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const float py = pyb + __builtin_fmaf(sjf[h], st, of);
+        sjf[h] += rows;
         const float cy = (p->cam_d - py) * p->cam_c;
-        const float rl = rsq(__builtin_fmaf(cy, cy, q0));
-        const float dy = __builtin_fmaf(cy, p->cam[7], ay) * rl;
+        const float rl = rsq(__builtin_fmaf(cy, cy, q0[h]));
+        const float dy = __builtin_fmaf(cy, p->cam[7], ay[h]) * rl;
         const float t = fabsf(dy) > 1e-6f ? nroy * rcp(dy) : -finf();
         const unsigned long long litm = m_hit0(t) & vmask;
         nlit += pc(litm);
@@ -2561,32 +2571,29 @@ __device__ __forceinline__ void lean1q_loop(KP p, const int32_t* order, int ngro
           E = f3(__builtin_fmaf(ci[l][0], x, E.x), __builtin_fmaf(ci[l][1], x, E.y), __builtin_fmaf(ci[l][2], x, E.z));
         }
         const F3 a = mul3(alb, E);
-        acc = f3(acc.x + (lit ? a.x : bg.x), acc.y + (lit ? a.y : bg.y), acc.z + (lit ? a.z : bg.z));
+        acc[h] = f3(acc[h].x + (lit ? a.x : bg.x), acc[h].y + (lit ? a.y : bg.y), acc[h].z + (lit ? a.z : bg.z));
       }
-      // push: pair with the stack while j has trailing ones (uniform branches)
-      F3 t = acc;
-      if (j & 1) {
-        t = f3(s0.x + t.x, s0.y + t.y, s0.z + t.z);
-        if (j & 2) {
-          t = f3(s1.x + t.x, s1.y + t.y, s1.z + t.z);
-          if (j & 4) {
-            t = f3(s2.x + t.x, s2.y + t.y, s2.z + t.z);
-            if (j & 8) t = f3(s3.x + t.x, s3.y + t.y, s3.z + t.z);
-            else s3 = t;
-          } else {
-            s2 = t;
-          }
+      // push the pair's sum: pair index P = j / 2 pairs with the stack while
+      // it has trailing ones (uniform branches)
+      const int P = j >> 1;
+      F3 t = f3(acc[0].x + acc[1].x, acc[0].y + acc[1].y, acc[0].z + acc[1].z);
+      if (P & 1) {
+        t = f3(s1.x + t.x, s1.y + t.y, s1.z + t.z);
+        if (P & 2) {
+          t = f3(s2.x + t.x, s2.y + t.y, s2.z + t.z);
+          if (P & 4) t = f3(s3.x + t.x, s3.y + t.y, s3.z + t.z);
+          else s3 = t;
         } else {
-          s1 = t;
+          s2 = t;
         }
       } else {
-        s0 = t;
+        s1 = t;
       }
-      if (j == V - 1) s0 = t;  // the lane's sum
+      if (j + 2 == V) sum = t;  // the lane's sum
     }
     // the pixel's lanes pairwise: xor 1 and 2 by quad permutes (DPP), then
     // xor 4, 8, ... by shuffles
-    F3 r = s0;
+    F3 r = sum;
     r = f3(r.x + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(r.x), 0xB1, 0xf, 0xf, false)),
            r.y + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(r.y), 0xB1, 0xf, 0xf, false)),
            r.z + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(r.z), 0xB1, 0xf, 0xf, false)));
