@@ -357,6 +357,8 @@ bool build_light_grid(const std::vector<BinTri>& tris, const double w2o[16], con
       }
   };
   if (!fill_bins((size_t)gu * (size_t)gv, tris.size(), emit, out->off, out->ent, why)) return false;
+  out->box = box;
+  out->rec0 = tris.empty() ? 0 : tris[0].rec;
   // each cell's faces ordered by the share of the cell their projection
   // covers, largest first: a shadow ray in the umbra meets the covering face
   // first, and the kernels' early exit (checked after a cell's first face)
@@ -410,7 +412,7 @@ void grid_occupancy(const LightGridHost& lg, GridOcc* out) {
 bool build_shadow_skips(const std::vector<int32_t>& pix_off, const std::vector<SkipPlane>& planes,
                         const double mesh_w2o[16], const std::vector<GridOcc>& grids, const double c2w[16],
                         double fov_deg, int width, int height, double bias, std::vector<uint32_t>* out,
-                        const char** why) {
+                        const char** why, std::vector<int32_t>* sl, std::vector<int32_t>* sl_ent, int sl_nl) {
   *why = "";
   const size_t npx = (size_t)width * (size_t)height;
   if (width <= 0 || height <= 0 || pix_off.size() != npx + 1) {
@@ -419,6 +421,10 @@ bool build_shadow_skips(const std::vector<int32_t>& pix_off, const std::vector<S
   }
   out->assign((npx + 3) / 4, 0u);
   const int nl = std::min<int>(8, (int)grids.size());
+  if (sl) {
+    sl->assign(npx * (size_t)sl_nl * 2, -1);
+    sl_ent->clear();
+  }
   unsigned have = 0;
   for (int l = 0; l < nl; ++l) have |= grids[(size_t)l].g.gu > 0 ? 1u << l : 0u;
   if (have == 0) return true;
@@ -450,9 +456,16 @@ bool build_shadow_skips(const std::vector<int32_t>& pix_off, const std::vector<S
       return true;  // no pixel qualifies
     }
   }
-  // rows in parallel (host threads), one byte per pixel, packed below
+  // rows in parallel (host threads), one byte per pixel, packed below; the
+  // shadow lists per thread, merged after
   std::vector<uint8_t> bytes(npx, 0);
-  auto rows = [&](int ya, int yb) {
+  struct ListPart {
+    std::vector<int32_t> ent;
+    std::vector<std::array<int64_t, 3>> at;  // (pix * sl_nl + l, start in ent, count)
+  };
+  const bool want_lists = sl != nullptr && sl_nl > 0;
+  auto rows = [&](int ya, int yb, ListPart* part) {
+  std::vector<std::pair<double, int32_t>> cand[8];
   for (int y = ya; y < yb; ++y) {
     for (int x = 0; x < width; ++x) {
       const size_t pix = (size_t)y * width + x;
@@ -465,7 +478,9 @@ bool build_shadow_skips(const std::vector<int32_t>& pix_off, const std::vector<S
         const double len = norm3(dw[c]);
         for (int k = 0; k < 3; ++k) dw[c][k] /= len;
       }
-      unsigned bits = have;
+      unsigned bits = have, bad = 0u;
+      bool qualified = true;
+      for (int l = 0; l < nl; ++l) cand[l].clear();
       for (size_t k = 0; k < planes.size() && bits; ++k) {
         const PlaneC& P = pc[k];
         int hit = 0, miss = 0;
@@ -484,11 +499,13 @@ bool build_shadow_skips(const std::vector<int32_t>& pix_off, const std::vector<S
         if (miss == 4) continue;  // no ray of the pixel reaches this plane
         if (hit != 4) {           // a horizon inside the pixel: unbounded footprint
           bits = 0;
+          qualified = false;
           break;
         }
         for (int l = 0; l < nl; ++l) {
-          if (!(bits >> l & 1u)) continue;
+          if (!(bits >> l & 1u) && !want_lists) continue;
           const LightGrid& g = grids[(size_t)l].g;
+          if (g.gu <= 0) continue;
           const double e1[3] = {g.e1[0], g.e1[1], g.e1[2]}, e2[3] = {g.e2[0], g.e2[1], g.e2[2]};
           double umin = INFINITY, umax = -INFINITY, vmin = INFINITY, vmax = -INFINITY, qmax = 0.0;
           for (int c = 0; c < 4; ++c) {
@@ -513,32 +530,91 @@ bool build_shadow_skips(const std::vector<int32_t>& pix_off, const std::vector<S
           if (!(fu1 >= 0.0 && fv1 >= 0.0 && fu0 < g.gu && fv0 < g.gv)) continue;  // off the grid
           if (!std::isfinite(fu0 + fu1 + fv0 + fv1)) {
             bits &= ~(1u << l);
+            bad |= 1u << l;
             continue;
           }
+          // a list stands in for the kernel's float32-safe-radius check
+          // (origins beyond rmax take the BVH): keep well inside it
+          const bool far = !(qmax <= 0.5 * (double)g.rmax);
           const int u0 = (int)std::max(0.0, std::floor(fu0)), u1 = (int)std::min((double)g.gu - 1, std::floor(fu1));
           const int v0 = (int)std::max(0.0, std::floor(fv0)), v1 = (int)std::min((double)g.gv - 1, std::floor(fv1));
           const std::vector<int32_t>& S = grids[(size_t)l].sat;
           const size_t W1 = (size_t)g.gu + 1;
           const int32_t n = S[(size_t)(v1 + 1) * W1 + u1 + 1] - S[(size_t)v0 * W1 + u1 + 1] -
                             S[(size_t)(v1 + 1) * W1 + u0] + S[(size_t)v0 * W1 + u0];
-          if (n != 0) bits &= ~(1u << l);
+          if (n == 0) continue;
+          bits &= ~(1u << l);
+          // the shadow list: faces of those cells whose grown projected box
+          // meets the footprint grown by mw (a hit face's box must)
+          const LightGridHost* L = grids[(size_t)l].lists;
+          if (!want_lists || l >= sl_nl || !L || far) {
+            bad |= 1u << l;
+            continue;
+          }
+          const double ru0 = umin - mw, ru1 = umax + mw, rv0 = vmin - mw, rv1 = vmax + mw;
+          for (int cv = v0; cv <= v1; ++cv)
+            for (int cu = u0; cu <= u1; ++cu) {
+              const size_t cell = (size_t)cv * (size_t)g.gu + (size_t)cu;
+              for (int32_t e = L->off[cell]; e < L->off[cell + 1]; ++e) {
+                const int32_t rec = L->ent[(size_t)e];
+                const size_t fi = (size_t)((rec - L->rec0) / (int32_t)sizeof(TriFast));
+                const double* fb = &L->box[4 * fi];
+                const double ou = std::min(fb[1], ru1) - std::max(fb[0], ru0);
+                const double ov = std::min(fb[3], rv1) - std::max(fb[2], rv0);
+                if (ou >= 0.0 && ov >= 0.0) cand[l].emplace_back(-ou * ov, rec);
+              }
+            }
+          if (cand[l].size() > 16 * (size_t)kShadowListMax) bad |= 1u << l;
         }
       }
       bytes[pix] = (uint8_t)bits;
+      if (!want_lists || !qualified) continue;
+      for (int l = 0; l < std::min(nl, sl_nl); ++l) {
+        if ((bits >> l & 1u) || (bad >> l & 1u) || grids[(size_t)l].g.gu <= 0) continue;
+        auto& c = cand[l];
+        // deduplicate (one entry per face, its largest overlap), then the
+        // faces covering most of the footprint first (early exit)
+        std::sort(c.begin(), c.end(), [](const std::pair<double, int32_t>& a, const std::pair<double, int32_t>& b) {
+          return a.second != b.second ? a.second < b.second : a.first < b.first;
+        });
+        c.erase(std::unique(c.begin(), c.end(),
+                            [](const std::pair<double, int32_t>& a, const std::pair<double, int32_t>& b) {
+                              return a.second == b.second;
+                            }),
+                c.end());
+        if (c.size() > (size_t)kShadowListMax) continue;
+        std::stable_sort(c.begin(), c.end(), [](const std::pair<double, int32_t>& a,
+                                                const std::pair<double, int32_t>& b) { return a.first < b.first; });
+        part->at.push_back({(int64_t)(pix * (size_t)sl_nl + (size_t)l), (int64_t)part->ent.size(), (int64_t)c.size()});
+        for (const auto& e : c) part->ent.push_back(e.second);
+      }
     }
   }
   };
   const int nt = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  std::vector<ListPart> parts((size_t)std::max(1, nt));
   if (nt == 1 || npx < 65536) {
-    rows(0, height);
+    rows(0, height, &parts[0]);
   } else {
     std::vector<std::thread> th;
     const int chunk = (height + nt - 1) / nt;
     for (int t = 0; t < nt; ++t) {
       const int ya = t * chunk, yb = std::min(height, ya + chunk);
-      if (ya < yb) th.emplace_back(rows, ya, yb);
+      if (ya < yb) th.emplace_back(rows, ya, yb, &parts[(size_t)t]);
     }
     for (auto& t : th) t.join();
+  }
+  if (want_lists) {
+    for (const ListPart& pt : parts) {
+      const int64_t base = (int64_t)sl_ent->size();
+      if (base + (int64_t)pt.ent.size() > INT32_MAX) break;
+      for (const auto& a : pt.at) {
+        (*sl)[2 * (size_t)a[0]] = (int32_t)(base + a[1]);
+        (*sl)[2 * (size_t)a[0] + 1] = (int32_t)a[2];
+      }
+      sl_ent->insert(sl_ent->end(), pt.ent.begin(), pt.ent.end());
+    }
+    for (int k = 0; k < kBinPad; ++k) sl_ent->push_back(sl_ent->empty() ? 0 : sl_ent->back());  // read-ahead pad
   }
   for (size_t pix = 0; pix < npx; ++pix) (*out)[pix >> 2] |= (uint32_t)bytes[pix] << (8 * (pix & 3));
   return true;

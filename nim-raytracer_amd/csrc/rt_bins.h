@@ -59,6 +59,10 @@ bool build_pixel_bins(const std::vector<BinTri>& tris, const double o2w[16], con
 struct LightGridHost {
   LightGrid g;
   std::vector<int32_t> off, ent;  // off: gu * gv + 1 (entry indices local to ent)
+  // per face (leaf order, record rec0 + 64 i): its projection's bounding box
+  // grown by the lists' margin (u0, u1, v0, v1), NaN for faces never listed
+  std::vector<double> box;
+  int32_t rec0 = 0;
 };
 // dir: the light's travel direction (world); shadow rays go along -dir.
 bool build_light_grid(const std::vector<BinTri>& tris, const double w2o[16], const double dir[3],
@@ -78,6 +82,7 @@ bool build_light_grid(const std::vector<BinTri>& tris, const double w2o[16], con
 struct GridOcc {
   LightGrid g{};                 // g.gu == 0: no grid for this light
   std::vector<int32_t> sat;      // (gu + 1) x (gv + 1) prefix counts of non-empty cells
+  const LightGridHost* lists = nullptr;  // the grid's cell lists and face boxes (shadow lists)
 };
 void grid_occupancy(const LightGridHost& lg, GridOcc* out);
 struct SkipPlane {
@@ -85,10 +90,20 @@ struct SkipPlane {
 };
 // pix_off: the pixel lists' offsets (w * h + 1); out: one byte per pixel,
 // packed four to a dword (pixel 4i + k in byte k of out[i]).
+//
+// Per-pixel shadow lists (sl != nullptr, the grids' `lists` set): for a
+// qualifying pixel and a light l whose skip bit stays clear, the faces whose
+// grown projected box meets the grown footprint of the pixel's shadow-ray
+// origins on the planes it reaches — every face any such shadow ray can hit —
+// deduplicated, those covering most of the footprint first, at most
+// kShadowListMax. sl[2 (pix * nl + l)] = start in *sl_ent, sl[.. + 1] =
+// count, -1: no list (the kernel searches the light's grid cells).
+constexpr int kShadowListMax = 48;
 bool build_shadow_skips(const std::vector<int32_t>& pix_off, const std::vector<SkipPlane>& planes,
                         const double mesh_w2o[16], const std::vector<GridOcc>& grids, const double c2w[16],
                         double fov_deg, int width, int height, double bias, std::vector<uint32_t>* out,
-                        const char** why);
+                        const char** why, std::vector<int32_t>* sl = nullptr, std::vector<int32_t>* sl_ent = nullptr,
+                        int sl_nl = 0);
 
 }  // namespace rtmi
 

@@ -1908,6 +1908,44 @@ __device__ __forceinline__ bool gen1_batch(KP p, const GroupPix& gp, int it0, un
           stop[k] = finf();
           if (mesh == 0) stop[k] = tpl[k] >= 0.0f ? fminf(stop[k], tpl[k]) : stop[k];
         }
+        // the pixel's shadow list for this light (rt_bins.h: built for pixels
+        // whose camera rays only reach planes; every face a shadow ray from
+        // the pixel's footprint can hit, deduplicated): one search for all
+        // the batch's rays instead of the light-grid cells
+        if (q->pix_sl && li < q->pix_sl_nl) {
+          const int pu = __builtin_amdgcn_readfirstlane(gp.y * q->width + gp.x);
+          const int32_t* e = cp(q->pix_sl) + 2 * (pu * q->pix_sl_nl + li);
+          const int lb = e[0], lc = e[1];
+          if (lc >= 0) {
+            unsigned fl = 0u;
+            unsigned long long own[S];
+#pragma unroll
+            for (int k = 0; k < S; ++k) {
+              const bool part = lane_in(pm[k]);
+              stop[k] = fminf(stop[k], __uint_as_float(__float_as_uint(ts[k]) - 1u));
+              tc[k] = part ? ts[k] : -1.0f;
+              best[k] = part ? ts[k] : 0.0f;
+              unused[k] = 0ull;
+              own[k] = pm[k];
+              fl |= pm[k] != 0ull ? (1u << k) : 0u;
+            }
+            const int nt = list_search_batch<S, false>(q, q->pix_sl_ent, lb, lb + lc, fl, ro, rd, stop, own, unused,
+                                                       best, tc);
+#ifdef RTMI_DIAG_GEN_COUNT
+            wi.v[STAT_NODE_FETCH] += 1u;
+            wi.v[STAT_TRI_FETCH] += (unsigned)nt * (unsigned)__builtin_popcount(fl);
+#else
+            (void)nt;
+#endif
+#pragma unroll
+            for (int k = 0; k < S; ++k) {  // found => 0 <= t < ts: the hit counts
+              const bool c = lane_in(pm[k]) && __float_as_uint(best[k]) != __float_as_uint(ts[k]);
+              ts[k] = c ? best[k] : ts[k];
+              hitl += c ? 1u : 0u;
+            }
+            return true;
+          }
+        }
         const RT_CONST LightGrid& G = cp(q->grids)[li];
         int cell[S];
         unsigned long long todo[S], left = 0ull, unsafe = 0ull;

@@ -198,6 +198,7 @@ struct rt_scene {
   bool has_grids = false;
   // shadow skips (rt_bins.h): scenes of the one mesh and planes
   std::vector<GridOcc> grid_occ;   // per light (g.gu == 0: none)
+  std::vector<LightGridHost> grid_host;  // per light: the cell lists + face boxes the shadow lists gather from
   std::vector<SkipPlane> skip_planes;
   bool skippable = false;
   struct PixelBins {               // camera-ray lists of one image size
@@ -214,7 +215,13 @@ struct rt_scene {
       double bias = 0.0;
       DevBuf<uint32_t> info;
       std::vector<uint32_t> host;  // the records (two-class launches list lean pixels from them)
-      ~Records() { info.release(); }
+      DevBuf<int32_t> sl, sl_ent;  // per-pixel shadow lists (rt_bins.h), or empty
+      int sl_nl = 0;
+      ~Records() {
+        info.release();
+        sl.release();
+        sl_ent.release();
+      }
     };
     std::vector<std::unique_ptr<Records>> records;
     ~PixelBins() {
@@ -816,6 +823,7 @@ extern "C" int rt_scene_create(const rt_scene_desc* d, rt_scene** out_scene) {
     // light grids of the distant lights
     std::vector<LightGrid> gh((size_t)std::max(1, d->num_lights), LightGrid{});
     s->grid_occ.assign((size_t)d->num_lights, GridOcc{});
+    s->grid_host.assign((size_t)d->num_lights, LightGridHost{});
     std::vector<int32_t> goff, gent;
     bool any = false;
     for (int li = 0; s->binnable && li < d->num_lights; ++li) {
@@ -832,6 +840,8 @@ extern "C" int rt_scene_create(const rt_scene_desc* d, rt_scene** out_scene) {
       gent.insert(gent.end(), lg.ent.begin(), lg.ent.end());
       gh[(size_t)li] = lg.g;
       grid_occupancy(lg, &s->grid_occ[(size_t)li]);
+      s->grid_host[(size_t)li] = std::move(lg);
+      s->grid_occ[(size_t)li].lists = &s->grid_host[(size_t)li];
       any = true;
     }
     if (any) {
@@ -1187,12 +1197,22 @@ const rt_scene::PixelBins::Records* pixel_records(rt_scene* s, rt_scene::PixelBi
   }
   const size_t npx = (size_t)o->width * (size_t)o->height;
   std::vector<uint32_t> sk;
+  std::vector<int32_t> sl, sl_ent;
   const char* why = "";
+  const int sl_nl = std::min(s->nlight, 8);
+  const bool lists = sl_nl > 0 && !std::getenv("RTMI_NO_SHADOW_LISTS");  // diagnostic A/B
   if (!(s->skippable && build_shadow_skips(pb->host_off, s->skip_planes, s->mesh_w2o, s->grid_occ, s->c2w, s->fov,
-                                           o->width, o->height, o->bias, &sk, &why)))
+                                           o->width, o->height, o->bias, &sk, &why, lists ? &sl : nullptr,
+                                           lists ? &sl_ent : nullptr, sl_nl))) {
     sk.assign((npx + 3) / 4, 0u);
+    sl.clear();
+  }
   std::unique_ptr<rt_scene::PixelBins::Records> r(new rt_scene::PixelBins::Records());
   r->bias = o->bias;
+  if (!sl.empty() && sl_ent.size() > (size_t)kBinPad) {
+    if (r->sl.upload(sl) != RT_OK || r->sl_ent.upload(sl_ent) != RT_OK) return nullptr;
+    r->sl_nl = sl_nl;
+  }
   r->host.resize(npx);
   for (size_t k = 0; k < npx; ++k) {
     const uint32_t n = (uint32_t)(pb->host_off[k + 1] - pb->host_off[k]);
@@ -1316,6 +1336,11 @@ void fill_fast(rt_scene* s, const rt_options* o, const Mapping& mp, float* fb, F
       // this bias, rt_bins.h), one set per bias (cached)
       const rt_scene::PixelBins::Records* rec = (pb->ok && pl.L == 64) ? pixel_records(s, pb, o) : nullptr;
       if (rec) p.pix_info = rec->info.p;
+      if (rec && rec->sl_nl > 0) {
+        p.pix_sl = rec->sl.p;
+        p.pix_sl_ent = rec->sl_ent.p;
+        p.pix_sl_nl = rec->sl_nl;
+      }
       if (pb->obj_ok) p.obj_pix = pb->omask.p;
     }
     if (s->has_grids) {
