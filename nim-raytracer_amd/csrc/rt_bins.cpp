@@ -813,6 +813,43 @@ extern "C" int64_t rtmi_test_light_grid(const double* v9, int64_t nf, const doub
   return (int64_t)lg.off.back();
 }
 
+// Per-pixel shadow lists of a one-mesh + planes scene (the arguments of
+// rtmi_test_shadow_skips): sl_out = w * h * nl * 2 (start, count; -1: none),
+// ent_out (cap entries) = face record offsets (64 x leaf-order index; the
+// test's faces in input order). Returns the number of lists, -1 on failure,
+// -2 if ent_cap is too small.
+extern "C" int64_t rtmi_test_shadow_lists(const double* v9, int64_t nf, const double o2w[16], const double w2o[16],
+                                          const double c2w[16], double fov, int32_t w, int32_t h, const double* planes,
+                                          int32_t nplanes, const double* dirs, int32_t nl, double bias, int32_t* sl_out,
+                                          int32_t* ent_out, int64_t ent_cap) {
+  const std::vector<rtmi::BinTri> tris = test_tris(v9, nf);
+  rtmi::PixelBinsHost hb;
+  const char* why = "";
+  if (!rtmi::build_pixel_bins(tris, o2w, w2o, c2w, fov, w, h, &hb, &why)) return -1;
+  std::vector<rtmi::GridOcc> occ((size_t)nl);
+  std::vector<rtmi::LightGridHost> hosts((size_t)nl);
+  for (int l = 0; l < nl; ++l) {
+    if (rtmi::build_light_grid(tris, w2o, dirs + 3 * l, &hosts[(size_t)l], &why)) {
+      rtmi::grid_occupancy(hosts[(size_t)l], &occ[(size_t)l]);
+      occ[(size_t)l].lists = &hosts[(size_t)l];
+    }
+  }
+  std::vector<rtmi::SkipPlane> pl((size_t)nplanes);
+  for (int k = 0; k < nplanes; ++k) {
+    std::copy(planes + 32 * k, planes + 32 * k + 16, pl[(size_t)k].o2w);
+    std::copy(planes + 32 * k + 16, planes + 32 * k + 32, pl[(size_t)k].w2o);
+  }
+  std::vector<uint32_t> sk;
+  std::vector<int32_t> sl, ent;
+  if (!rtmi::build_shadow_skips(hb.off, pl, w2o, occ, c2w, fov, w, h, bias, &sk, &why, &sl, &ent, nl)) return -1;
+  if ((int64_t)ent.size() > ent_cap) return -2;
+  std::copy(sl.begin(), sl.end(), sl_out);
+  std::copy(ent.begin(), ent.end(), ent_out);
+  int64_t n = 0;
+  for (size_t i = 1; i < sl.size(); i += 2) n += sl[i] >= 0;
+  return n;
+}
+
 // Shadow skips of a one-mesh + planes scene: planes[k] = o2w[16], w2o[16];
 // dirs: nl distant-light directions. out: (w * h + 3) / 4 dwords. Returns the
 // number of pixels with any skip bit, or -1.

@@ -240,3 +240,65 @@ def test_shadow_skips_are_conservative(name, tilted):
             assert len(hit) == 0, (name, li, x, y, hit[:5])
             near += k < len(edge)
     assert near > 100
+
+
+@pytest.mark.parametrize("name,tilted", [("bunny", False), ("rotated_torus", True)])
+def test_shadow_lists_hold_every_hit_face(name, tilted):
+    """A pixel's shadow list for a light (rt_bins.h build_shadow_skips, sl)
+    promises every face a shadow ray to that light from a camera hit in the
+    pixel can meet: checked for random samples (and the pixel corners) of
+    pixels with a list, against every face in float64."""
+    L = lib()
+    f = L.rtmi_test_shadow_lists
+    f.restype = C.c_int64
+    mesh = MESHES[name]()
+    v9 = _faces(mesh)
+    nf = len(v9)
+    o2w, w2o = _m(mesh.objectToWorld), _m(mesh.worldToObject)
+    sc = scenes.mesh_bunny()
+    c2w = _m(sc.cameraToWorld)
+    po2w, pw2o = _tilted_plane() if tilted else (mat4(1.0), mat4(1.0))
+    planes = np.concatenate([_m(po2w), _m(pw2o)])
+    dirs = np.ascontiguousarray(np.concatenate([np.asarray(l.dir[:3], np.float64) for l in sc.lights]))
+    nl = len(sc.lights)
+    W, H, fov, bias = 480, 270, 50.0, 1e-4
+    sl = np.zeros(W * H * nl * 2, np.int32)
+    cap = 1 << 22
+    ent = np.zeros(cap, np.int32)
+    n = f(v9.ctypes.data_as(C.c_void_p), C.c_int64(nf), o2w.ctypes.data_as(C.c_void_p),
+          w2o.ctypes.data_as(C.c_void_p), c2w.ctypes.data_as(C.c_void_p), C.c_double(fov), W, H,
+          planes.ctypes.data_as(C.c_void_p), 1, dirs.ctypes.data_as(C.c_void_p), nl, C.c_double(bias),
+          sl.ctypes.data_as(C.c_void_p), ent.ctypes.data_as(C.c_void_p), C.c_int64(cap))
+    assert n > 100, n
+    sl = sl.reshape(W * H, nl, 2)
+    C2W, W2O, P2W, W2P = _cols(c2w), _cols(w2o), _cols(_m(po2w)), _cols(_m(pw2o))
+    N = P2W[:3, 1]
+    fo = math.tan(math.radians(fov) / 2)
+    ca, cc = 2 * (W / H) * fo / W, 2 * fo / H
+    org = C2W[:3, 3]
+    rng = np.random.default_rng(11)
+    hits_seen = 0
+    for li, light in enumerate(sc.lights):
+        rd = W2O[:3, :3] @ -np.asarray(light.dir[:3], np.float64)
+        have = np.nonzero(sl[:, li, 1] >= 0)[0]
+        assert len(have) > 0
+        for k, pix in enumerate(have[rng.permutation(len(have))[:500]]):
+            x, y = int(pix % W), int(pix // W)
+            lst = set((ent[sl[pix, li, 0]:sl[pix, li, 0] + sl[pix, li, 1]] // 64).tolist())
+            for j in range(3):
+                sx, sy = (rng.random(), rng.random()) if j else (float(rng.integers(0, 2)), float(rng.integers(0, 2)))
+                px, py = x + min(sx, 0.999999), y + min(sy, 0.999999)
+                dc = np.array([(px - W / 2) * ca, (H / 2 - py) * cc, -1.0])
+                d = C2W[:3, :3] @ (dc / np.linalg.norm(dc))
+                oy = (W2P[:3, :3] @ org + W2P[:3, 3])[1]
+                dy = (W2P[:3, :3] @ d)[1]
+                t = -oy / dy
+                if not (t >= 0):
+                    continue
+                so = org + d * t + N * bias
+                ro = W2O[:3, :3] @ so + W2O[:3, 3]
+                hit = _hits(v9, ro, rd)
+                hits_seen += len(hit)
+                missing = set(hit.tolist()) - lst
+                assert not missing, (name, li, x, y, sorted(missing)[:5])
+    assert hits_seen > 50, hits_seen
