@@ -466,6 +466,9 @@ bool build_shadow_skips(const std::vector<int32_t>& pix_off, const std::vector<S
   const bool want_lists = sl != nullptr && sl_nl > 0;
   auto rows = [&](int ya, int yb, ListPart* part) {
   std::vector<std::pair<double, int32_t>> cand[8];
+  // per light, the last (pixel + 1) that listed a face: duplicates from
+  // neighbouring cells are dropped as they are gathered (no sort / unique)
+  std::vector<uint32_t> seen[8];
   for (int y = ya; y < yb; ++y) {
     for (int x = 0; x < width; ++x) {
       const size_t pix = (size_t)y * width + x;
@@ -547,42 +550,43 @@ bool build_shadow_skips(const std::vector<int32_t>& pix_off, const std::vector<S
           // the shadow list: faces of those cells whose grown projected box
           // meets the footprint grown by mw (a hit face's box must)
           const LightGridHost* L = grids[(size_t)l].lists;
-          if (!want_lists || l >= sl_nl || !L || far) {
+          // a footprint over many cells (towards the horizon) would list more
+          // faces than the cells the kernel would search: no list
+          const bool wide = (int64_t)(u1 - u0 + 1) * (int64_t)(v1 - v0 + 1) > 36;
+          if (!want_lists || l >= sl_nl || !L || far || wide) {
             bad |= 1u << l;
             continue;
           }
           const double ru0 = umin - mw, ru1 = umax + mw, rv0 = vmin - mw, rv1 = vmax + mw;
+          std::vector<uint32_t>& sn = seen[l];
+          if (sn.size() < L->box.size() / 4) sn.assign(L->box.size() / 4, 0u);
+          const uint32_t stamp = (uint32_t)pix + 1u;
           for (int cv = v0; cv <= v1; ++cv)
             for (int cu = u0; cu <= u1; ++cu) {
               const size_t cell = (size_t)cv * (size_t)g.gu + (size_t)cu;
               for (int32_t e = L->off[cell]; e < L->off[cell + 1]; ++e) {
                 const int32_t rec = L->ent[(size_t)e];
                 const size_t fi = (size_t)((rec - L->rec0) / (int32_t)sizeof(TriFast));
+                if (sn[fi] == stamp) continue;
                 const double* fb = &L->box[4 * fi];
                 const double ou = std::min(fb[1], ru1) - std::max(fb[0], ru0);
                 const double ov = std::min(fb[3], rv1) - std::max(fb[2], rv0);
-                if (ou >= 0.0 && ov >= 0.0) cand[l].emplace_back(-ou * ov, rec);
+                if (ou >= 0.0 && ov >= 0.0) {
+                  sn[fi] = stamp;
+                  cand[l].emplace_back(-ou * ov, rec);
+                }
               }
             }
-          if (cand[l].size() > 16 * (size_t)kShadowListMax) bad |= 1u << l;
+          if (cand[l].size() > 4 * (size_t)kShadowListMax) bad |= 1u << l;
         }
       }
       bytes[pix] = (uint8_t)bits;
       if (!want_lists || !qualified) continue;
       for (int l = 0; l < std::min(nl, sl_nl); ++l) {
         if ((bits >> l & 1u) || (bad >> l & 1u) || grids[(size_t)l].g.gu <= 0) continue;
-        auto& c = cand[l];
-        // deduplicate (one entry per face, its largest overlap), then the
-        // faces covering most of the footprint first (early exit)
-        std::sort(c.begin(), c.end(), [](const std::pair<double, int32_t>& a, const std::pair<double, int32_t>& b) {
-          return a.second != b.second ? a.second < b.second : a.first < b.first;
-        });
-        c.erase(std::unique(c.begin(), c.end(),
-                            [](const std::pair<double, int32_t>& a, const std::pair<double, int32_t>& b) {
-                              return a.second == b.second;
-                            }),
-                c.end());
+        auto& c = cand[l];  // one entry per face (the stamps), every plane's footprint
         if (c.size() > (size_t)kShadowListMax) continue;
+        // the faces covering most of the footprint first (early exit)
         std::stable_sort(c.begin(), c.end(), [](const std::pair<double, int32_t>& a,
                                                 const std::pair<double, int32_t>& b) { return a.first < b.first; });
         part->at.push_back({(int64_t)(pix * (size_t)sl_nl + (size_t)l), (int64_t)part->ent.size(), (int64_t)c.size()});
