@@ -256,6 +256,11 @@ struct FastParams {
   // k_render_mix1's second list (lean pixels, k_render_lean1q items) and its shard count
   const int32_t* order2;
   int32_t ngroups2, shards2;
+  // every distant light's direction on the same side of the plane y = const
+  // (|dir.y| > 1e-6, one sign), or none off it: k_render_lean1q / _mix1
+  // test a lit sample's shadow rays with one plane test (host-side choice
+  // of the kernel instantiation, rtmi.cpp)
+  int32_t lights_one_side;
 };
 
 enum : int32_t {

@@ -2511,7 +2511,7 @@ __device__ __forceinline__ GroupPix lane_pixel(KP p, int g) {
 // k_render_lean1q's work loop over one list (order: 64 / LP entries per
 // item, ngroups items, dequeued from the shard heads at `queue`); also the
 // second phase of k_render_mix1.
-template <int NL, int LP>
+template <int NL, int LP, bool ONE>
 __device__ __forceinline__ void lean1q_loop(KP p, const int32_t* order, int ngroups, unsigned int* queue, int shards,
                                             Stats32& ws, unsigned long long* tot, int& nflush) {
   const int lane = (int)__lane_id();
@@ -2552,6 +2552,28 @@ __device__ __forceinline__ void lean1q_loop(KP p, const int32_t* order, int ngro
   constexpr int V = 64 / LP;   // virtual lanes per lane
   constexpr int PPI = 64 / LP; // pixels per work item
   const int q = lane & (LP - 1);  // this lane's share of its pixel's virtual lanes
+  // ONE (rtmi.cpp lights_one_side): every light on the same side of the
+  // plane (finite plane reciprocals of one sign), or none with one. A lit
+  // sample's shadow rays then all hit the plane or all miss it — ts_l =
+  // -(s) * m_l with s finite for a lit sample (|s| is about the bias) has
+  // the sign of -s times that of m_l, rounding never changes a sign, and a
+  // NaN m_l never hits — so one test decides them, and the sample's colour
+  // is one of three wave-uniform values: albedo x E over all lights (formed
+  // in the order of the per-light loop below), albedo x E with every light
+  // occluded, the background.
+  F3 av = f3(0.0f, 0.0f, 0.0f), a0 = av;
+  {
+    F3 ev = f3(0.0f, 0.0f, 0.0f), e0 = ev;
+#pragma unroll
+    for (int l = 0; l < NL; ++l) {
+      ev = f3(__builtin_fmaf(ci[l][0], ndl[l], ev.x), __builtin_fmaf(ci[l][1], ndl[l], ev.y),
+              __builtin_fmaf(ci[l][2], ndl[l], ev.z));
+      e0 = f3(__builtin_fmaf(ci[l][0], 0.0f, e0.x), __builtin_fmaf(ci[l][1], 0.0f, e0.y),
+              __builtin_fmaf(ci[l][2], 0.0f, e0.z));
+    }
+    av = mul3(alb, ev);
+    a0 = mul3(alb, e0);
+  }
   while (g < ngroups) {
     const int gg = order[g * PPI + lane / LP];  // this lane's pixel (list entry; -1: padding)
     qj = __builtin_amdgcn_readfirstlane(qj_next);
@@ -2599,17 +2621,26 @@ __device__ __forceinline__ void lean1q_loop(KP p, const int32_t* order, int ngro
         nlit += pc(litm);
         const bool lit = lane_in(litm);
         const float soy = __builtin_fmaf(1.0f, bias, __builtin_fmaf(dy, t, oy));
-        F3 E = f3(0.0f, 0.0f, 0.0f);
+        if constexpr (ONE) {
+          const float ts = -(soy + ty) * mulp[0];
+          const unsigned long long occ = m_hit0(ts) & litm;  // every light's shadow ray alike
+          nocc += (unsigned)NL * pc(occ);
+          const bool vis = lane_in(litm & ~occ);
+          acc[h] = f3(acc[h].x + (lit ? (vis ? av.x : a0.x) : bg.x), acc[h].y + (lit ? (vis ? av.y : a0.y) : bg.y),
+                      acc[h].z + (lit ? (vis ? av.z : a0.z) : bg.z));
+        } else {
+          F3 E = f3(0.0f, 0.0f, 0.0f);
 #pragma unroll
-        for (int l = 0; l < NL; ++l) {
-          const float ts = -(soy + ty) * mulp[l];
-          const unsigned long long occ = m_hit0(ts) & litm;
-          nocc += pc(occ);
-          const float x = lane_in(litm & ~occ) ? ndl[l] : 0.0f;
-          E = f3(__builtin_fmaf(ci[l][0], x, E.x), __builtin_fmaf(ci[l][1], x, E.y), __builtin_fmaf(ci[l][2], x, E.z));
+          for (int l = 0; l < NL; ++l) {
+            const float ts = -(soy + ty) * mulp[l];
+            const unsigned long long occ = m_hit0(ts) & litm;
+            nocc += pc(occ);
+            const float x = lane_in(litm & ~occ) ? ndl[l] : 0.0f;
+            E = f3(__builtin_fmaf(ci[l][0], x, E.x), __builtin_fmaf(ci[l][1], x, E.y), __builtin_fmaf(ci[l][2], x, E.z));
+          }
+          const F3 a = mul3(alb, E);
+          acc[h] = f3(acc[h].x + (lit ? a.x : bg.x), acc[h].y + (lit ? a.y : bg.y), acc[h].z + (lit ? a.z : bg.z));
         }
-        const F3 a = mul3(alb, E);
-        acc[h] = f3(acc[h].x + (lit ? a.x : bg.x), acc[h].y + (lit ? a.y : bg.y), acc[h].z + (lit ? a.z : bg.z));
       }
       // push the pair's sum: pair index P = j / 2 pairs with the stack while
       // it has trailing ones (uniform branches)
@@ -2666,7 +2697,7 @@ __device__ __forceinline__ void lean1q_loop(KP p, const int32_t* order, int ngro
   }
 }
 
-template <int NL, int LP>
+template <int NL, int LP, bool ONE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k_render_lean1q(
     const FastParams params_by_value) {
   (void)params_by_value;
@@ -2679,7 +2710,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
 #pragma unroll
   for (int k = 0; k < kStatSlots; ++k) ws.v[k] = 0u;
   int nflush = 0;
-  lean1q_loop<NL, LP>(p, p->order, p->ngroups, p->queue, p->shards, ws, lds_tot[wib], nflush);
+  lean1q_loop<NL, LP, ONE>(p, p->order, p->ngroups, p->queue, p->shards, ws, lds_tot[wib], nflush);
   flush_stats(ws, lds_tot[wib], lane);
   const int wave = (int)(blockIdx.x * (blockDim.x >> 6) + threadIdx.x / 64u);
   if (lane < kStatSlots) p->partials[(size_t)wave * kStatSlots + lane] = lds_tot[wib][lane];
@@ -2873,7 +2904,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RTMI_GEN1_W
 // set of queue heads) — one ramp and one tail per launch instead of two, the
 // expensive items first and the cheap ones filling the tail. Frames and
 // Stats those of the two kernels.
-template <int NL, int LP>
+template <int NL, int LP, bool ONE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RTMI_GEN1_WAVES))) void k_render_mix1(
     const FastParams params_by_value) {
   (void)params_by_value;
@@ -2889,7 +2920,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RTMI_GEN1_W
   int nflush = 0;
   gen1_loop<NL>(p, ls, ws, lds_tot[wib], nflush);
   p = params();
-  lean1q_loop<NL, LP>(p, p->order2, p->ngroups2, p->queue + kQueueShards * kQueueStride, p->shards2, ws,
+  lean1q_loop<NL, LP, ONE>(p, p->order2, p->ngroups2, p->queue + kQueueShards * kQueueStride, p->shards2, ws,
                       lds_tot[wib], nflush);
   p = params();
   const int lane = (int)__lane_id();

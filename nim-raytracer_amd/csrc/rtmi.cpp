@@ -150,6 +150,7 @@ struct rt_scene {
   int32_t nobj = 0, nlight = 0, nmesh = 0;
   int32_t shadow_mesh = -1;  // the only mesh object, or -1 (FastParams.shadow_mesh)
   int32_t has_point_light = 0;
+  int32_t lights_one_side = 0;  // FastParams.lights_one_side
   unsigned f32_subset = 0;   // SUB_* feature bits of the scene (kernel specialisation)
   bool any_reflective = false;
   double fov = 50.0;
@@ -741,6 +742,16 @@ extern "C" int rt_scene_create(const rt_scene_desc* d, rt_scene** out_scene) {
     std::vector<FMesh> fm;
     std::vector<FLight> fl;
     fill_fast_records(d, m, fo, fx, fm, fl);
+    {  // the kernels' shadow-ray y components are -dir.y (rt_fast.h lean1q_loop)
+      int up = 0, down = 0, flat = 0;
+      for (const FLight& L : fl) {
+        const float sy = -L.v[1];
+        if (L.type != LIGHT_DISTANT) continue;
+        if (fabsf(sy) > 1e-6f) (sy > 0.0f ? up : down) += 1;
+        else flat += 1;
+      }
+      s->lights_one_side = (up == 0 || down == 0) && (flat == 0 || up + down == 0);
+    }
     int rc;
     if ((rc = s->f32.objs.upload(fo)) || (rc = s->f32.objx.upload(fx)) || (rc = s->f32.meshes.upload(fm)) ||
         (rc = s->f32.lights.upload(fl)) || (rc = s->f32.normals.upload(n)))
@@ -1278,6 +1289,7 @@ void fill_fast(rt_scene* s, const rt_options* o, const Mapping& mp, float* fb, F
     if (m == (1 << k)) p.log2_grid_m = k;
   p.nobj = s->nobj;
   p.nlight = s->nlight;
+  p.lights_one_side = s->lights_one_side;
   p.has_point_light = s->has_point_light;
   p.seed = o->seed;
   p.width = o->width;

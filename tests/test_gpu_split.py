@@ -183,6 +183,34 @@ def test_lean1_kernel_choice(gpu, m):
     assert ds.last_lean_kernel() == 3 | 3 << 2
 
 
+@pytest.mark.parametrize("dirs", [
+    ((-2.0, -0.8, -0.3), (2.0, 0.8, -1.3)),   # opposite sides of the plane: one test per light
+    ((-2.0, -0.8, -0.3), (2.0, 0.0, -1.3)),   # one parallel to it (no plane hit): per light
+    ((-2.0, 0.0, -0.3), (2.0, 0.0, -1.3)),    # both parallel: the shared test
+    ((-2.0, 0.0, -0.3),),                     # one light, parallel
+    ((2.0, 0.8, -1.3),),                      # one light from below
+])
+def test_lean1_light_sides(gpu, dirs):
+    """k_render_lean1q / _mix1 test a lit sample's shadow rays against the
+    plane once when every light is on the same side of it (or none off it,
+    rtmi.cpp lights_one_side), per light otherwise: both equal the general
+    kernels, frames and Stats."""
+    import torch
+    from rtmi.glm import normalize, vec
+    from rtmi.scene import DistantLight
+    s = scenes.mesh_bunny()
+    s.lights = [DistantLight(color=vec3(1.0, 0.9, 0.8), intensity=3.0 - k, dir=normalize(vec(*d)))
+                for k, d in enumerate(dirs)]
+    ds = DeviceScene(s)
+    ref = torch.zeros(256 * 144 * 3, dtype=torch.float32, device="cuda")
+    st_ref = ds.render_device(_opts(256, 144, 16, RT_FLAG_NO_LEAN1 | RT_FLAG_NO_GEN1), ref)
+    for flags, kind in ((0, 3 | 3 << 2), (RT_FLAG_NO_MIX, 2 | 2 << 2)):
+        fb = torch.zeros_like(ref)
+        st = ds.render_device(_opts(256, 144, 16, flags), fb)
+        assert ds.last_lean_kernel() == kind, (flags, ds.last_lean_kernel())
+        assert st == st_ref and torch.equal(fb, ref), (dirs, flags, float((fb - ref).abs().max()))
+
+
 def test_no_split_without_records(gpu):
     """No lean kernel where no pixel can be lean: a point light (no skip
     bit), two meshes (no pixel records), fewer than 64 samples per pixel."""
