@@ -257,9 +257,10 @@ struct FastParams {
   const int32_t* order2;
   int32_t ngroups2, shards2;
   // every distant light's direction on the same side of the plane y = const
-  // (|dir.y| > 1e-6, one sign), or none off it: k_render_lean1q / _mix1
-  // test a lit sample's shadow rays with one plane test (host-side choice
-  // of the kernel instantiation, rtmi.cpp)
+  // (1e-6 < |dir.y| <= 1, one sign), or none off it, with finite colours,
+  // albedos and coordinates: k_render_lean1q / _mix1 test a lit sample's
+  // shadow rays with one class test (host-side choice of the kernel
+  // instantiation, rtmi.cpp; conditions in rt_fast.h lean1q_loop)
   int32_t lights_one_side;
 };
 

@@ -2349,6 +2349,36 @@ __device__ __forceinline__ unsigned long long m_hit0(float t) {
   asm("v_cmp_class_f32_e64 %0, %1, %2" : "=s"(m) : "v"(t), "v"(0x1E0));
   return m;
 }
+// v_cmp_class with a run-time class mask (bits: 3 -normal, 4 -denormal,
+// 5 -0, 6 +0, 7 +denormal, 8 +normal; 0: never)
+__device__ __forceinline__ unsigned long long m_class(float x, int classes) {
+  unsigned long long m;
+  asm("v_cmp_class_f32_e64 %0, %1, %2" : "=s"(m) : "v"(x), "v"(classes));
+  return m;
+}
+// acc += av on the lanes of `vis`, += bg on the lanes off `lit`, unchanged
+// elsewhere (the occluded samples, whose colour is +-0: see lean1q_loop):
+// two runs of three adds under EXEC instead of two selects per channel.
+// EXEC is restored before the block ends.
+__device__ __forceinline__ void acc_vis_bg(F3& acc, unsigned long long vis, unsigned long long lit, const F3& av,
+                                           const F3& bg) {
+  unsigned long long save;
+  asm volatile(
+      "s_mov_b64 %[sv], exec\n\t"
+      "s_and_b64 exec, %[sv], %[vis]\n\t"
+      "v_add_f32 %[x], %[ax], %[x]\n\t"
+      "v_add_f32 %[y], %[ay], %[y]\n\t"
+      "v_add_f32 %[z], %[az], %[z]\n\t"
+      "s_andn2_b64 exec, %[sv], %[lit]\n\t"
+      "v_add_f32 %[x], %[bx], %[x]\n\t"
+      "v_add_f32 %[y], %[by], %[y]\n\t"
+      "v_add_f32 %[z], %[bz], %[z]\n\t"
+      "s_mov_b64 exec, %[sv]"
+      : [x] "+v"(acc.x), [y] "+v"(acc.y), [z] "+v"(acc.z), [sv] "=&s"(save)
+      : [vis] "s"(vis), [lit] "s"(lit), [ax] "v"(av.x), [ay] "v"(av.y), [az] "v"(av.z), [bx] "v"(bg.x),
+        [by] "v"(bg.y), [bz] "v"(bg.z)
+      : "scc");
+}
 template <int NL>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k_render_lean1(
     const FastParams params_by_value) {
@@ -2553,26 +2583,27 @@ __device__ __forceinline__ void lean1q_loop(KP p, const int32_t* order, int ngro
   constexpr int PPI = 64 / LP; // pixels per work item
   const int q = lane & (LP - 1);  // this lane's share of its pixel's virtual lanes
   // ONE (rtmi.cpp lights_one_side): every light on the same side of the
-  // plane (finite plane reciprocals of one sign), or none with one. A lit
-  // sample's shadow rays then all hit the plane or all miss it — ts_l =
-  // -(s) * m_l with s finite for a lit sample (|s| is about the bias) has
-  // the sign of -s times that of m_l, rounding never changes a sign, and a
-  // NaN m_l never hits — so one test decides them, and the sample's colour
-  // is one of three wave-uniform values: albedo x E over all lights (formed
-  // in the order of the per-light loop below), albedo x E with every light
-  // occluded, the background.
-  F3 av = f3(0.0f, 0.0f, 0.0f), a0 = av;
+  // plane (plane reciprocals m_l finite, of one sign, |m_l| >= 1), or none
+  // with one (all NaN). A lit sample's shadow rays then all hit the plane or
+  // all miss it — ts_l = -(X) * m_l, X = soy + ty finite and far from
+  // overflow for a lit sample (the host bounds the camera, plane and bias),
+  // is >= 0 exactly when X <= 0 (m > 0) or X >= 0 (m < 0), zeros of either
+  // sign counting (no product underflows to a zero with |m| >= 1), and a NaN
+  // m_l never hits — so one class test of X decides them all, and the
+  // sample's colour is one of three wave-uniform values: albedo x E over all
+  // lights (formed in the order of the per-light loop below), albedo x E
+  // with every light occluded — +-0 for finite albedo and light colours,
+  // which leaves the running sum unchanged (it starts at +0 and is never
+  // -0) — and the background.
+  const int occ_classes = __builtin_isnan(mulp[0]) ? 0 : (mulp[0] > 0.0f ? 0x78 : 0x1E0);
+  F3 av = f3(0.0f, 0.0f, 0.0f);
   {
-    F3 ev = f3(0.0f, 0.0f, 0.0f), e0 = ev;
+    F3 ev = av;
 #pragma unroll
-    for (int l = 0; l < NL; ++l) {
+    for (int l = 0; l < NL; ++l)
       ev = f3(__builtin_fmaf(ci[l][0], ndl[l], ev.x), __builtin_fmaf(ci[l][1], ndl[l], ev.y),
               __builtin_fmaf(ci[l][2], ndl[l], ev.z));
-      e0 = f3(__builtin_fmaf(ci[l][0], 0.0f, e0.x), __builtin_fmaf(ci[l][1], 0.0f, e0.y),
-              __builtin_fmaf(ci[l][2], 0.0f, e0.z));
-    }
     av = mul3(alb, ev);
-    a0 = mul3(alb, e0);
   }
   while (g < ngroups) {
     const int gg = order[g * PPI + lane / LP];  // this lane's pixel (list entry; -1: padding)
@@ -2616,18 +2647,17 @@ __device__ __forceinline__ void lean1q_loop(KP p, const int32_t* order, int ngro
         const float cy = (p->cam_d - py) * p->cam_c;
         const float rl = rsq(__builtin_fmaf(cy, cy, q0[h]));
         const float dy = __builtin_fmaf(cy, p->cam[7], ay[h]) * rl;
-        const float t = fabsf(dy) > 1e-6f ? nroy * rcp(dy) : -finf();
-        const unsigned long long litm = m_hit0(t) & vmask;
+        // (|dy| <= 1e-6: no hit; t is only read on lit lanes)
+        const float t = nroy * rcp(dy);
+        const unsigned long long litm = m_hit0(t) & bal(fabsf(dy) > 1e-6f) & vmask;
         nlit += pc(litm);
         const bool lit = lane_in(litm);
         const float soy = __builtin_fmaf(1.0f, bias, __builtin_fmaf(dy, t, oy));
         if constexpr (ONE) {
-          const float ts = -(soy + ty) * mulp[0];
-          const unsigned long long occ = m_hit0(ts) & litm;  // every light's shadow ray alike
+          (void)lit;
+          const unsigned long long occ = m_class(soy + ty, occ_classes) & litm;  // every light's shadow ray alike
           nocc += (unsigned)NL * pc(occ);
-          const bool vis = lane_in(litm & ~occ);
-          acc[h] = f3(acc[h].x + (lit ? (vis ? av.x : a0.x) : bg.x), acc[h].y + (lit ? (vis ? av.y : a0.y) : bg.y),
-                      acc[h].z + (lit ? (vis ? av.z : a0.z) : bg.z));
+          acc_vis_bg(acc[h], litm & ~occ, litm, av, bg);
         } else {
           F3 E = f3(0.0f, 0.0f, 0.0f);
 #pragma unroll

@@ -58,12 +58,13 @@ template __global__ void fast::k_render_fast<true, fast::F_ALL>(const FastParams
 // lean pixels of one-plane scenes (rtmi.cpp lean1_ok), one or two lights
 template __global__ void fast::k_render_lean1<1>(const FastParams);
 template __global__ void fast::k_render_lean1<2>(const FastParams);
-// (ONE: the lights' shadow rays share one plane test, rt_fast.h
-// lean1q_loop; always so for one light)
+// (ONE: the lights' shadow rays share one plane test, rt_fast.h lean1q_loop)
 template __global__ void fast::k_render_lean1q<1, 4, true>(const FastParams);
+template __global__ void fast::k_render_lean1q<1, 4, false>(const FastParams);
 template __global__ void fast::k_render_lean1q<2, 4, true>(const FastParams);
 template __global__ void fast::k_render_lean1q<2, 4, false>(const FastParams);
 template __global__ void fast::k_render_lean1q<1, 16, true>(const FastParams);
+template __global__ void fast::k_render_lean1q<1, 16, false>(const FastParams);
 template __global__ void fast::k_render_lean1q<2, 16, true>(const FastParams);
 template __global__ void fast::k_render_lean1q<2, 16, false>(const FastParams);
 // general pixels of the same scenes
@@ -71,9 +72,11 @@ template __global__ void fast::k_render_gen1<1>(const FastParams);
 template __global__ void fast::k_render_gen1<2>(const FastParams);
 // both classes of a one-plane launch in one kernel
 template __global__ void fast::k_render_mix1<1, 4, true>(const FastParams);
+template __global__ void fast::k_render_mix1<1, 4, false>(const FastParams);
 template __global__ void fast::k_render_mix1<2, 4, true>(const FastParams);
 template __global__ void fast::k_render_mix1<2, 4, false>(const FastParams);
 template __global__ void fast::k_render_mix1<1, 16, true>(const FastParams);
+template __global__ void fast::k_render_mix1<1, 16, false>(const FastParams);
 template __global__ void fast::k_render_mix1<2, 16, true>(const FastParams);
 template __global__ void fast::k_render_mix1<2, 16, false>(const FastParams);
 
@@ -156,11 +159,12 @@ extern "C" int rtmi_lean1_quads() {
 extern "C" int rtmi_launch_lean1_f32(const rtmi::FastParams* p, int nl, int lp, int blocks, void* stream) {
   if (lp == 4 || lp == 16) {
     using namespace rtmi::fast;
-    const bool one = nl == 1 || p->lights_one_side;
+    const bool one = p->lights_one_side != 0;
     const int k = (nl == 2 ? 2 : 0) + (one ? 0 : 1) + (lp == 16 ? 4 : 0);
     switch (nl == 1 || nl == 2 ? k : -1) {
       case 0: hipLaunchKernelGGL((k_render_lean1q<1, 4, true>), dim3(blocks), dim3(256), 0, (hipStream_t)stream, *p); break;
-      case 1: case 5: return (int)hipErrorInvalidValue;  // one light: always shared
+      case 1: hipLaunchKernelGGL((k_render_lean1q<1, 4, false>), dim3(blocks), dim3(256), 0, (hipStream_t)stream, *p); break;
+      case 5: hipLaunchKernelGGL((k_render_lean1q<1, 16, false>), dim3(blocks), dim3(256), 0, (hipStream_t)stream, *p); break;
       case 2: hipLaunchKernelGGL((k_render_lean1q<2, 4, true>), dim3(blocks), dim3(256), 0, (hipStream_t)stream, *p); break;
       case 3: hipLaunchKernelGGL((k_render_lean1q<2, 4, false>), dim3(blocks), dim3(256), 0, (hipStream_t)stream, *p); break;
       case 4: hipLaunchKernelGGL((k_render_lean1q<1, 16, true>), dim3(blocks), dim3(256), 0, (hipStream_t)stream, *p); break;
@@ -200,13 +204,15 @@ extern "C" int rtmi_launch_gen1_f32(const rtmi::FastParams* p, int nl, int block
 // The one-plane merged kernel (general items, then lean items with lp lanes per pixel).
 extern "C" int rtmi_launch_mix1_f32(const rtmi::FastParams* p, int nl, int lp, int blocks, void* stream) {
   using namespace rtmi::fast;
-  const bool one = nl == 1 || p->lights_one_side;
+  const bool one = p->lights_one_side != 0;
   const int k = (nl == 2 ? 2 : 0) + (one ? 0 : 1) + (lp == 16 ? 4 : 0);
   switch ((nl == 1 || nl == 2) && (lp == 4 || lp == 16) ? k : -1) {
     case 0: hipLaunchKernelGGL((k_render_mix1<1, 4, true>), dim3(blocks), dim3(256), 0, (hipStream_t)stream, *p); break;
+    case 1: hipLaunchKernelGGL((k_render_mix1<1, 4, false>), dim3(blocks), dim3(256), 0, (hipStream_t)stream, *p); break;
     case 2: hipLaunchKernelGGL((k_render_mix1<2, 4, true>), dim3(blocks), dim3(256), 0, (hipStream_t)stream, *p); break;
     case 3: hipLaunchKernelGGL((k_render_mix1<2, 4, false>), dim3(blocks), dim3(256), 0, (hipStream_t)stream, *p); break;
     case 4: hipLaunchKernelGGL((k_render_mix1<1, 16, true>), dim3(blocks), dim3(256), 0, (hipStream_t)stream, *p); break;
+    case 5: hipLaunchKernelGGL((k_render_mix1<1, 16, false>), dim3(blocks), dim3(256), 0, (hipStream_t)stream, *p); break;
     case 6: hipLaunchKernelGGL((k_render_mix1<2, 16, true>), dim3(blocks), dim3(256), 0, (hipStream_t)stream, *p); break;
     case 7: hipLaunchKernelGGL((k_render_mix1<2, 16, false>), dim3(blocks), dim3(256), 0, (hipStream_t)stream, *p); break;
     default: return (int)hipErrorInvalidValue;

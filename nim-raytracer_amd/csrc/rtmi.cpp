@@ -150,7 +150,8 @@ struct rt_scene {
   int32_t nobj = 0, nlight = 0, nmesh = 0;
   int32_t shadow_mesh = -1;  // the only mesh object, or -1 (FastParams.shadow_mesh)
   int32_t has_point_light = 0;
-  int32_t lights_one_side = 0;  // FastParams.lights_one_side
+  int32_t lights_one_side = 0;  // FastParams.lights_one_side (with the per-call bounds of fill_fast)
+  float max_abs_ty = 0.0f;      // max |world_to_object y translation| over the objects
   unsigned f32_subset = 0;   // SUB_* feature bits of the scene (kernel specialisation)
   bool any_reflective = false;
   double fov = 50.0;
@@ -742,15 +743,25 @@ extern "C" int rt_scene_create(const rt_scene_desc* d, rt_scene** out_scene) {
     std::vector<FMesh> fm;
     std::vector<FLight> fl;
     fill_fast_records(d, m, fo, fx, fm, fl);
-    {  // the kernels' shadow-ray y components are -dir.y (rt_fast.h lean1q_loop)
+    {  // rt_fast.h lean1q_loop ONE: the shadow-ray y components (-dir.y) all
+       // of one sign with |.| in (1e-6, 1], or all within 1e-6 of 0; finite
+       // light colours and albedos (an occluded sample's colour is +-0)
       int up = 0, down = 0, flat = 0;
+      bool ok = true;
       for (const FLight& L : fl) {
         const float sy = -L.v[1];
         if (L.type != LIGHT_DISTANT) continue;
         if (fabsf(sy) > 1e-6f) (sy > 0.0f ? up : down) += 1;
         else flat += 1;
+        ok = ok && fabsf(sy) <= 1.0f && std::isfinite(L.ci[0]) && std::isfinite(L.ci[1]) && std::isfinite(L.ci[2]);
       }
-      s->lights_one_side = (up == 0 || down == 0) && (flat == 0 || up + down == 0);
+      float ty = 0.0f;
+      for (size_t i = 0; i < fo.size(); ++i) {
+        ty = std::max(ty, fabsf(fo[i].t[1]));
+        for (int k = 0; k < 3; ++k) ok = ok && std::isfinite(fx[i].albedo_pi[k]);
+      }
+      s->lights_one_side = ok && std::isfinite(ty) && (up == 0 || down == 0) && (flat == 0 || up + down == 0);
+      s->max_abs_ty = ty;
     }
     int rc;
     if ((rc = s->f32.objs.upload(fo)) || (rc = s->f32.objx.upload(fx)) || (rc = s->f32.meshes.upload(fm)) ||
@@ -1289,7 +1300,10 @@ void fill_fast(rt_scene* s, const rt_options* o, const Mapping& mp, float* fb, F
     if (m == (1 << k)) p.log2_grid_m = k;
   p.nobj = s->nobj;
   p.nlight = s->nlight;
-  p.lights_one_side = s->lights_one_side;
+  // the lean kernels' one-test occlusion needs |soy + ty| far from overflow
+  // (rt_fast.h lean1q_loop): it is about |cam y + ty| rounding plus the bias
+  p.lights_one_side = s->lights_one_side && std::isfinite(p.bias) && std::isfinite(p.cam[1]) &&
+                      3.0f * (fabsf(p.cam[1]) + s->max_abs_ty) + fabsf(p.bias) < 1e30f;
   p.has_point_light = s->has_point_light;
   p.seed = o->seed;
   p.width = o->width;

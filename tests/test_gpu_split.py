@@ -189,6 +189,7 @@ def test_lean1_kernel_choice(gpu, m):
     ((-2.0, 0.0, -0.3), (2.0, 0.0, -1.3)),    # both parallel: the shared test
     ((-2.0, 0.0, -0.3),),                     # one light, parallel
     ((2.0, 0.8, -1.3),),                      # one light from below
+    ("raw", (-2.0, -1.5, -0.3)),              # not normalised, |dir.y| > 1: per light
 ])
 def test_lean1_light_sides(gpu, dirs):
     """k_render_lean1q / _mix1 test a lit sample's shadow rays against the
@@ -199,8 +200,9 @@ def test_lean1_light_sides(gpu, dirs):
     from rtmi.glm import normalize, vec
     from rtmi.scene import DistantLight
     s = scenes.mesh_bunny()
-    s.lights = [DistantLight(color=vec3(1.0, 0.9, 0.8), intensity=3.0 - k, dir=normalize(vec(*d)))
-                for k, d in enumerate(dirs)]
+    raw = dirs[0] == "raw"
+    s.lights = [DistantLight(color=vec3(1.0, 0.9, 0.8), intensity=3.0 - k, dir=vec(*d) if raw else normalize(vec(*d)))
+                for k, d in enumerate(dirs[1:] if raw else dirs)]
     ds = DeviceScene(s)
     ref = torch.zeros(256 * 144 * 3, dtype=torch.float32, device="cuda")
     st_ref = ds.render_device(_opts(256, 144, 16, RT_FLAG_NO_LEAN1 | RT_FLAG_NO_GEN1), ref)
