@@ -2366,13 +2366,17 @@ __device__ __forceinline__ void acc_vis_bg(F3& acc, unsigned long long vis, unsi
   asm volatile(
       "s_mov_b64 %[sv], exec\n\t"
       "s_and_b64 exec, %[sv], %[vis]\n\t"
+      "s_cbranch_execz .Lacc_vis_%=\n\t"
       "v_add_f32 %[x], %[ax], %[x]\n\t"
       "v_add_f32 %[y], %[ay], %[y]\n\t"
-      "v_add_f32 %[z], %[az], %[z]\n\t"
+      "v_add_f32 %[z], %[az], %[z]\n"
+      ".Lacc_vis_%=:\n\t"
       "s_andn2_b64 exec, %[sv], %[lit]\n\t"
+      "s_cbranch_execz .Lacc_bg_%=\n\t"
       "v_add_f32 %[x], %[bx], %[x]\n\t"
       "v_add_f32 %[y], %[by], %[y]\n\t"
-      "v_add_f32 %[z], %[bz], %[z]\n\t"
+      "v_add_f32 %[z], %[bz], %[z]\n"
+      ".Lacc_bg_%=:\n\t"
       "s_mov_b64 exec, %[sv]"
       : [x] "+v"(acc.x), [y] "+v"(acc.y), [z] "+v"(acc.z), [sv] "=&s"(save)
       : [vis] "s"(vis), [lit] "s"(lit), [ax] "v"(av.x), [ay] "v"(av.y), [az] "v"(av.z), [bx] "v"(bg.x),
@@ -2618,9 +2622,24 @@ __device__ __forceinline__ void lean1q_loop(KP p, const int32_t* order, int ngro
     // sum is the tree's first level)
     F3 s1 = f3(0.0f, 0.0f, 0.0f), s2 = s1, s3 = s1, sum = s1;
     static_assert(V % 2 == 0, "virtual lanes in pairs");
+    // the sample row of virtual lane jv in iteration it: (it * 64 + jv) >> lg
+    // == it * (64 >> lg) + (jv >> lg) (m | 64), and jv >> lg == (q V) >> lg
+    // for all of this lane's virtual lanes (m >= 16, rtmi.cpp lean1_ok, so V
+    // divides 2^lg): one camera y per iteration for the whole lane, formed
+    // from exact small-integer floats as k_render_lean1 steps them
+    const float rows = (float)(64 >> lg), sj0 = (float)((q * V) >> lg);
+    float cyc[4];  // the camera y of four consecutive iterations from it0
+    auto cy_rows = [&](int it0) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float py = pyb + __builtin_fmaf(__builtin_fmaf((float)(it0 + k), rows, sj0), st, of);
+        cyc[k] = (p->cam_d - py) * p->cam_c;
+      }
+    };
+    if (iters == 4) cy_rows(0);  // one chunk (m = 16): once per item
 #pragma unroll 1
     for (int j = 0; j < V; j += 2) {
-      float q0[2], ay[2], sjf[2];
+      float q0[2], ay[2];
       F3 acc[2];
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
@@ -2629,22 +2648,17 @@ __device__ __forceinline__ void lean1q_loop(KP p, const int32_t* order, int ngro
         const float cx = (px - p->cam_b) * p->cam_a;
         q0[h] = __builtin_fmaf(cx, cx, 1.0f);
         ay[h] = __builtin_fmaf(cx, p->cam[4], -p->cam[10]);
-        // the sample row (it * 64 + jv) >> lg == it * (64 >> lg) + (jv >> lg)
-        // (m | 64), as a float stepped by 64 >> lg: exact small integers
-        sjf[h] = (float)(jv >> lg);
         acc[h] = f3(0.0f, 0.0f, 0.0f);
       }
-      const float rows = (float)(64 >> lg);
       // iters is a multiple of 4 (rtmi.cpp lean1_ok): four samples per step
 #pragma unroll 1
-      for (int it0 = 0; it0 < iters; it0 += 4)
+      for (int it0 = 0; it0 < iters; it0 += 4) {
+      if (iters != 4) cy_rows(it0);
 #pragma unroll
-      for (int it = it0; it < it0 + 4; ++it)
+      for (int it = 0; it < 4; ++it)
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        const float py = pyb + __builtin_fmaf(sjf[h], st, of);
-        sjf[h] += rows;
-        const float cy = (p->cam_d - py) * p->cam_c;
+        const float cy = cyc[it];
         const float rl = rsq(__builtin_fmaf(cy, cy, q0[h]));
         const float dy = __builtin_fmaf(cy, p->cam[7], ay[h]) * rl;
         // (|dy| <= 1e-6: no hit; t is only read on lit lanes)
@@ -2671,6 +2685,7 @@ __device__ __forceinline__ void lean1q_loop(KP p, const int32_t* order, int ngro
           const F3 a = mul3(alb, E);
           acc[h] = f3(acc[h].x + (lit ? a.x : bg.x), acc[h].y + (lit ? a.y : bg.y), acc[h].z + (lit ? a.z : bg.z));
         }
+      }
       }
       // push the pair's sum: pair index P = j / 2 pairs with the stack while
       // it has trailing ones (uniform branches)
