@@ -262,6 +262,10 @@ struct FastParams {
   // shadow rays with one class test (host-side choice of the kernel
   // instantiation, rtmi.cpp; conditions in rt_fast.h lean1q_loop)
   int32_t lights_one_side;
+  // lights_one_side with every light above the plane and a bias the
+  // rounding of the shadow origin cannot cancel: no lit lean sample is
+  // occluded (rt_fast.h lean1q_loop MODE 2; conditions in rtmi.cpp fill_fast)
+  int32_t lean_no_occ;
 };
 
 enum : int32_t {

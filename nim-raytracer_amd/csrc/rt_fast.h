@@ -2545,7 +2545,7 @@ __device__ __forceinline__ GroupPix lane_pixel(KP p, int g) {
 // k_render_lean1q's work loop over one list (order: 64 / LP entries per
 // item, ngroups items, dequeued from the shard heads at `queue`); also the
 // second phase of k_render_mix1.
-template <int NL, int LP, bool ONE>
+template <int NL, int LP, int MODE>
 __device__ __forceinline__ void lean1q_loop(KP p, const int32_t* order, int ngroups, unsigned int* queue, int shards,
                                             Stats32& ws, unsigned long long* tot, int& nflush) {
   const int lane = (int)__lane_id();
@@ -2586,7 +2586,8 @@ __device__ __forceinline__ void lean1q_loop(KP p, const int32_t* order, int ngro
   constexpr int V = 64 / LP;   // virtual lanes per lane
   constexpr int PPI = 64 / LP; // pixels per work item
   const int q = lane & (LP - 1);  // this lane's share of its pixel's virtual lanes
-  // ONE (rtmi.cpp lights_one_side): every light on the same side of the
+  // MODE 0: each light's shadow ray tested against the plane. MODE 1
+  // (rtmi.cpp lights_one_side): every light on the same side of the
   // plane (plane reciprocals m_l finite, of one sign, |m_l| >= 1), or none
   // with one (all NaN). A lit sample's shadow rays then all hit the plane or
   // all miss it — ts_l = -(X) * m_l, X = soy + ty finite and far from
@@ -2599,7 +2600,17 @@ __device__ __forceinline__ void lean1q_loop(KP p, const int32_t* order, int ngro
   // with every light occluded — +-0 for finite albedo and light colours,
   // which leaves the running sum unchanged (it starts at +0 and is never
   // -0) — and the background.
+  // MODE 2 (rtmi.cpp lean_no_occ): as MODE 1 with every light above the
+  // plane (m > 0) and a bias the host proved larger than the rounding of
+  // X = soy + ty (bias > 1e-6 (|cam y| + 2 |ty|): X > 0 for every lit
+  // sample), so no lit sample is occluded and its colour is albedo x E; with
+  // 1e-20 <= |nroy| <= 1e30 and a bounded camera, t = nroy rcp(dy) is
+  // finite and nonzero for |dy| > 1e-6, so the lit test "t in [-0, +inf),
+  // |dy| > 1e-6" is sg dy > 1e-6 (sg = the sign of nroy) — formed as
+  // fma(cy, sg c7, sg ay) rl, which is sg dy exactly (negation commutes with
+  // rounding): no t, no shadow origin.
   const int occ_classes = __builtin_isnan(mulp[0]) ? 0 : (mulp[0] > 0.0f ? 0x78 : 0x1E0);
+  const float sg = nroy > 0.0f ? 1.0f : -1.0f, c7s = p->cam[7] * sg;
   F3 av = f3(0.0f, 0.0f, 0.0f);
   {
     F3 ev = av;
@@ -2648,6 +2659,7 @@ __device__ __forceinline__ void lean1q_loop(KP p, const int32_t* order, int ngro
         const float cx = (px - p->cam_b) * p->cam_a;
         q0[h] = __builtin_fmaf(cx, cx, 1.0f);
         ay[h] = __builtin_fmaf(cx, p->cam[4], -p->cam[10]);
+        if constexpr (MODE == 2) ay[h] = ay[h] * sg;
         acc[h] = f3(0.0f, 0.0f, 0.0f);
       }
       // iters is a multiple of 4 (rtmi.cpp lean1_ok): four samples per step
@@ -2660,6 +2672,18 @@ __device__ __forceinline__ void lean1q_loop(KP p, const int32_t* order, int ngro
       for (int h = 0; h < 2; ++h) {
         const float cy = cyc[it];
         const float rl = rsq(__builtin_fmaf(cy, cy, q0[h]));
+        if constexpr (MODE == 2) {
+          const float dys = __builtin_fmaf(cy, c7s, ay[h]) * rl;  // sg dy
+          const unsigned long long litm = bal(dys > 1e-6f) & vmask;
+          nlit += pc(litm);
+#ifdef RTMI_LEAN2_SELECT
+          const bool lit = lane_in(litm);
+          acc[h] = f3(acc[h].x + (lit ? av.x : bg.x), acc[h].y + (lit ? av.y : bg.y), acc[h].z + (lit ? av.z : bg.z));
+#else
+          acc_vis_bg(acc[h], litm, litm, av, bg);
+#endif
+          continue;
+        }
         const float dy = __builtin_fmaf(cy, p->cam[7], ay[h]) * rl;
         // (|dy| <= 1e-6: no hit; t is only read on lit lanes)
         const float t = nroy * rcp(dy);
@@ -2667,7 +2691,7 @@ __device__ __forceinline__ void lean1q_loop(KP p, const int32_t* order, int ngro
         nlit += pc(litm);
         const bool lit = lane_in(litm);
         const float soy = __builtin_fmaf(1.0f, bias, __builtin_fmaf(dy, t, oy));
-        if constexpr (ONE) {
+        if constexpr (MODE == 1) {
           (void)lit;
           const unsigned long long occ = m_class(soy + ty, occ_classes) & litm;  // every light's shadow ray alike
           nocc += (unsigned)NL * pc(occ);
@@ -2742,7 +2766,7 @@ __device__ __forceinline__ void lean1q_loop(KP p, const int32_t* order, int ngro
   }
 }
 
-template <int NL, int LP, bool ONE>
+template <int NL, int LP, int MODE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k_render_lean1q(
     const FastParams params_by_value) {
   (void)params_by_value;
@@ -2755,7 +2779,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
 #pragma unroll
   for (int k = 0; k < kStatSlots; ++k) ws.v[k] = 0u;
   int nflush = 0;
-  lean1q_loop<NL, LP, ONE>(p, p->order, p->ngroups, p->queue, p->shards, ws, lds_tot[wib], nflush);
+  lean1q_loop<NL, LP, MODE>(p, p->order, p->ngroups, p->queue, p->shards, ws, lds_tot[wib], nflush);
   flush_stats(ws, lds_tot[wib], lane);
   const int wave = (int)(blockIdx.x * (blockDim.x >> 6) + threadIdx.x / 64u);
   if (lane < kStatSlots) p->partials[(size_t)wave * kStatSlots + lane] = lds_tot[wib][lane];
@@ -2949,7 +2973,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RTMI_GEN1_W
 // set of queue heads) — one ramp and one tail per launch instead of two, the
 // expensive items first and the cheap ones filling the tail. Frames and
 // Stats those of the two kernels.
-template <int NL, int LP, bool ONE>
+template <int NL, int LP, int MODE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RTMI_GEN1_WAVES))) void k_render_mix1(
     const FastParams params_by_value) {
   (void)params_by_value;
@@ -2965,7 +2989,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RTMI_GEN1_W
   int nflush = 0;
   gen1_loop<NL>(p, ls, ws, lds_tot[wib], nflush);
   p = params();
-  lean1q_loop<NL, LP, ONE>(p, p->order2, p->ngroups2, p->queue + kQueueShards * kQueueStride, p->shards2, ws,
+  lean1q_loop<NL, LP, MODE>(p, p->order2, p->ngroups2, p->queue + kQueueShards * kQueueStride, p->shards2, ws,
                       lds_tot[wib], nflush);
   p = params();
   const int lane = (int)__lane_id();

@@ -58,27 +58,35 @@ template __global__ void fast::k_render_fast<true, fast::F_ALL>(const FastParams
 // lean pixels of one-plane scenes (rtmi.cpp lean1_ok), one or two lights
 template __global__ void fast::k_render_lean1<1>(const FastParams);
 template __global__ void fast::k_render_lean1<2>(const FastParams);
-// (ONE: the lights' shadow rays share one plane test, rt_fast.h lean1q_loop)
-template __global__ void fast::k_render_lean1q<1, 4, true>(const FastParams);
-template __global__ void fast::k_render_lean1q<1, 4, false>(const FastParams);
-template __global__ void fast::k_render_lean1q<2, 4, true>(const FastParams);
-template __global__ void fast::k_render_lean1q<2, 4, false>(const FastParams);
-template __global__ void fast::k_render_lean1q<1, 16, true>(const FastParams);
-template __global__ void fast::k_render_lean1q<1, 16, false>(const FastParams);
-template __global__ void fast::k_render_lean1q<2, 16, true>(const FastParams);
-template __global__ void fast::k_render_lean1q<2, 16, false>(const FastParams);
+// (MODE 0: a plane test per light, 1: one for all, 2: none needed — rt_fast.h lean1q_loop)
+template __global__ void fast::k_render_lean1q<1, 4, 0>(const FastParams);
+template __global__ void fast::k_render_lean1q<1, 4, 1>(const FastParams);
+template __global__ void fast::k_render_lean1q<1, 4, 2>(const FastParams);
+template __global__ void fast::k_render_lean1q<2, 4, 0>(const FastParams);
+template __global__ void fast::k_render_lean1q<2, 4, 1>(const FastParams);
+template __global__ void fast::k_render_lean1q<2, 4, 2>(const FastParams);
+template __global__ void fast::k_render_lean1q<1, 16, 0>(const FastParams);
+template __global__ void fast::k_render_lean1q<1, 16, 1>(const FastParams);
+template __global__ void fast::k_render_lean1q<1, 16, 2>(const FastParams);
+template __global__ void fast::k_render_lean1q<2, 16, 0>(const FastParams);
+template __global__ void fast::k_render_lean1q<2, 16, 1>(const FastParams);
+template __global__ void fast::k_render_lean1q<2, 16, 2>(const FastParams);
 // general pixels of the same scenes
 template __global__ void fast::k_render_gen1<1>(const FastParams);
 template __global__ void fast::k_render_gen1<2>(const FastParams);
 // both classes of a one-plane launch in one kernel
-template __global__ void fast::k_render_mix1<1, 4, true>(const FastParams);
-template __global__ void fast::k_render_mix1<1, 4, false>(const FastParams);
-template __global__ void fast::k_render_mix1<2, 4, true>(const FastParams);
-template __global__ void fast::k_render_mix1<2, 4, false>(const FastParams);
-template __global__ void fast::k_render_mix1<1, 16, true>(const FastParams);
-template __global__ void fast::k_render_mix1<1, 16, false>(const FastParams);
-template __global__ void fast::k_render_mix1<2, 16, true>(const FastParams);
-template __global__ void fast::k_render_mix1<2, 16, false>(const FastParams);
+template __global__ void fast::k_render_mix1<1, 4, 0>(const FastParams);
+template __global__ void fast::k_render_mix1<1, 4, 1>(const FastParams);
+template __global__ void fast::k_render_mix1<1, 4, 2>(const FastParams);
+template __global__ void fast::k_render_mix1<2, 4, 0>(const FastParams);
+template __global__ void fast::k_render_mix1<2, 4, 1>(const FastParams);
+template __global__ void fast::k_render_mix1<2, 4, 2>(const FastParams);
+template __global__ void fast::k_render_mix1<1, 16, 0>(const FastParams);
+template __global__ void fast::k_render_mix1<1, 16, 1>(const FastParams);
+template __global__ void fast::k_render_mix1<1, 16, 2>(const FastParams);
+template __global__ void fast::k_render_mix1<2, 16, 0>(const FastParams);
+template __global__ void fast::k_render_mix1<2, 16, 1>(const FastParams);
+template __global__ void fast::k_render_mix1<2, 16, 2>(const FastParams);
 
 }  // namespace rtmi
 
@@ -159,20 +167,16 @@ extern "C" int rtmi_lean1_quads() {
 extern "C" int rtmi_launch_lean1_f32(const rtmi::FastParams* p, int nl, int lp, int blocks, void* stream) {
   if (lp == 4 || lp == 16) {
     using namespace rtmi::fast;
-    const bool one = p->lights_one_side != 0;
-    const int k = (nl == 2 ? 2 : 0) + (one ? 0 : 1) + (lp == 16 ? 4 : 0);
-    switch (nl == 1 || nl == 2 ? k : -1) {
-      case 0: hipLaunchKernelGGL((k_render_lean1q<1, 4, true>), dim3(blocks), dim3(256), 0, (hipStream_t)stream, *p); break;
-      case 1: hipLaunchKernelGGL((k_render_lean1q<1, 4, false>), dim3(blocks), dim3(256), 0, (hipStream_t)stream, *p); break;
-      case 5: hipLaunchKernelGGL((k_render_lean1q<1, 16, false>), dim3(blocks), dim3(256), 0, (hipStream_t)stream, *p); break;
-      case 2: hipLaunchKernelGGL((k_render_lean1q<2, 4, true>), dim3(blocks), dim3(256), 0, (hipStream_t)stream, *p); break;
-      case 3: hipLaunchKernelGGL((k_render_lean1q<2, 4, false>), dim3(blocks), dim3(256), 0, (hipStream_t)stream, *p); break;
-      case 4: hipLaunchKernelGGL((k_render_lean1q<1, 16, true>), dim3(blocks), dim3(256), 0, (hipStream_t)stream, *p); break;
-      case 6: hipLaunchKernelGGL((k_render_lean1q<2, 16, true>), dim3(blocks), dim3(256), 0, (hipStream_t)stream, *p); break;
-      case 7: hipLaunchKernelGGL((k_render_lean1q<2, 16, false>), dim3(blocks), dim3(256), 0, (hipStream_t)stream, *p); break;
-      default: return (int)hipErrorInvalidValue;
-    }
-    return (int)hipGetLastError();
+    const int mode = p->lean_no_occ ? 2 : p->lights_one_side ? 1 : 0;
+#define RTMI_LQ(nl_, lp_, m_) \
+  if (nl == nl_ && lp == lp_ && mode == m_) { \
+    hipLaunchKernelGGL((k_render_lean1q<nl_, lp_, m_>), dim3(blocks), dim3(256), 0, (hipStream_t)stream, *p); \
+    return (int)hipGetLastError(); \
+  }
+    RTMI_LQ(1, 4, 0) RTMI_LQ(1, 4, 1) RTMI_LQ(1, 4, 2) RTMI_LQ(2, 4, 0) RTMI_LQ(2, 4, 1) RTMI_LQ(2, 4, 2)
+    RTMI_LQ(1, 16, 0) RTMI_LQ(1, 16, 1) RTMI_LQ(1, 16, 2) RTMI_LQ(2, 16, 0) RTMI_LQ(2, 16, 1) RTMI_LQ(2, 16, 2)
+#undef RTMI_LQ
+    return (int)hipErrorInvalidValue;
   }
   if (nl == 1)
     hipLaunchKernelGGL(rtmi::fast::k_render_lean1<1>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, *p);
@@ -204,27 +208,23 @@ extern "C" int rtmi_launch_gen1_f32(const rtmi::FastParams* p, int nl, int block
 // The one-plane merged kernel (general items, then lean items with lp lanes per pixel).
 extern "C" int rtmi_launch_mix1_f32(const rtmi::FastParams* p, int nl, int lp, int blocks, void* stream) {
   using namespace rtmi::fast;
-  const bool one = p->lights_one_side != 0;
-  const int k = (nl == 2 ? 2 : 0) + (one ? 0 : 1) + (lp == 16 ? 4 : 0);
-  switch ((nl == 1 || nl == 2) && (lp == 4 || lp == 16) ? k : -1) {
-    case 0: hipLaunchKernelGGL((k_render_mix1<1, 4, true>), dim3(blocks), dim3(256), 0, (hipStream_t)stream, *p); break;
-    case 1: hipLaunchKernelGGL((k_render_mix1<1, 4, false>), dim3(blocks), dim3(256), 0, (hipStream_t)stream, *p); break;
-    case 2: hipLaunchKernelGGL((k_render_mix1<2, 4, true>), dim3(blocks), dim3(256), 0, (hipStream_t)stream, *p); break;
-    case 3: hipLaunchKernelGGL((k_render_mix1<2, 4, false>), dim3(blocks), dim3(256), 0, (hipStream_t)stream, *p); break;
-    case 4: hipLaunchKernelGGL((k_render_mix1<1, 16, true>), dim3(blocks), dim3(256), 0, (hipStream_t)stream, *p); break;
-    case 5: hipLaunchKernelGGL((k_render_mix1<1, 16, false>), dim3(blocks), dim3(256), 0, (hipStream_t)stream, *p); break;
-    case 6: hipLaunchKernelGGL((k_render_mix1<2, 16, true>), dim3(blocks), dim3(256), 0, (hipStream_t)stream, *p); break;
-    case 7: hipLaunchKernelGGL((k_render_mix1<2, 16, false>), dim3(blocks), dim3(256), 0, (hipStream_t)stream, *p); break;
-    default: return (int)hipErrorInvalidValue;
+  const int mode = p->lean_no_occ ? 2 : p->lights_one_side ? 1 : 0;
+#define RTMI_MX(nl_, lp_, m_) \
+  if (nl == nl_ && lp == lp_ && mode == m_) { \
+    hipLaunchKernelGGL((k_render_mix1<nl_, lp_, m_>), dim3(blocks), dim3(256), 0, (hipStream_t)stream, *p); \
+    return (int)hipGetLastError(); \
   }
-  return (int)hipGetLastError();
+  RTMI_MX(1, 4, 0) RTMI_MX(1, 4, 1) RTMI_MX(1, 4, 2) RTMI_MX(2, 4, 0) RTMI_MX(2, 4, 1) RTMI_MX(2, 4, 2)
+  RTMI_MX(1, 16, 0) RTMI_MX(1, 16, 1) RTMI_MX(1, 16, 2) RTMI_MX(2, 16, 0) RTMI_MX(2, 16, 1) RTMI_MX(2, 16, 2)
+#undef RTMI_MX
+  return (int)hipErrorInvalidValue;
 }
 
 extern "C" int rtmi_mix1_f32_blocks_per_cu(int nl) {
   int nb = 0;
   const hipError_t e = nl == 1
-      ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, rtmi::fast::k_render_mix1<1, 4, true>, 256, 0)
-      : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, rtmi::fast::k_render_mix1<2, 4, false>, 256, 0);
+      ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, rtmi::fast::k_render_mix1<1, 4, 1>, 256, 0)
+      : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, rtmi::fast::k_render_mix1<2, 4, 0>, 256, 0);
   return e == hipSuccess && nb > 0 ? nb : 1;
 }
 

@@ -152,6 +152,8 @@ struct rt_scene {
   int32_t has_point_light = 0;
   int32_t lights_one_side = 0;  // FastParams.lights_one_side (with the per-call bounds of fill_fast)
   float max_abs_ty = 0.0f;      // max |world_to_object y translation| over the objects
+  bool lights_all_above = false;  // lights_one_side, every shadow ray going up (-dir.y > 1e-6)
+  float plane_ty = 0.0f;          // the non-mesh object's y translation (two-object scenes)
   unsigned f32_subset = 0;   // SUB_* feature bits of the scene (kernel specialisation)
   bool any_reflective = false;
   double fov = 50.0;
@@ -761,7 +763,10 @@ extern "C" int rt_scene_create(const rt_scene_desc* d, rt_scene** out_scene) {
         for (int k = 0; k < 3; ++k) ok = ok && std::isfinite(fx[i].albedo_pi[k]);
       }
       s->lights_one_side = ok && std::isfinite(ty) && (up == 0 || down == 0) && (flat == 0 || up + down == 0);
+      s->lights_all_above = s->lights_one_side && up > 0 && down == 0 && flat == 0;
       s->max_abs_ty = ty;
+      // the plane of a mesh + plane scene (FastParams.shadow_mesh's partner)
+      s->plane_ty = fo.size() == 2 ? fo[fo[0].type == RT_MESH ? 1 : 0].t[1] : 0.0f;
     }
     int rc;
     if ((rc = s->f32.objs.upload(fo)) || (rc = s->f32.objx.upload(fx)) || (rc = s->f32.meshes.upload(fm)) ||
@@ -1304,6 +1309,14 @@ void fill_fast(rt_scene* s, const rt_options* o, const Mapping& mp, float* fb, F
   // (rt_fast.h lean1q_loop): it is about |cam y + ty| rounding plus the bias
   p.lights_one_side = s->lights_one_side && std::isfinite(p.bias) && std::isfinite(p.cam[1]) &&
                       3.0f * (fabsf(p.cam[1]) + s->max_abs_ty) + fabsf(p.bias) < 1e30f;
+  {  // rt_fast.h lean1q_loop MODE 2: the plane's nroy as the kernel forms it,
+     // nonzero and bounded; a bias above the shadow origin's rounding
+    const float nroy = -(p.cam[1] + s->plane_ty);
+    bool cam_ok = true;
+    for (int k = 3; k < 12; ++k) cam_ok = cam_ok && fabsf(p.cam[k]) <= 1e6f;
+    p.lean_no_occ = p.lights_one_side && s->lights_all_above && cam_ok && fabsf(nroy) >= 1e-20f &&
+                    fabsf(nroy) <= 1e30f && p.bias > 1e-6f * (fabsf(p.cam[1]) + 2.0f * fabsf(s->plane_ty));
+  }
   p.has_point_light = s->has_point_light;
   p.seed = o->seed;
   p.width = o->width;

@@ -213,6 +213,25 @@ def test_lean1_light_sides(gpu, dirs):
         assert st == st_ref and torch.equal(fb, ref), (dirs, flags, float((fb - ref).abs().max()))
 
 
+@pytest.mark.parametrize("cam_y,bias", [(5.5, 1e-4), (5.5, 1e-7), (5.5, 0.0), (-3.0, 1e-4), (0.5, 1e-4)])
+def test_lean1_camera_side_and_bias(gpu, cam_y, bias):
+    """Lights above the plane: with a bias the shadow origin's rounding
+    cannot cancel the lean kernels skip the occlusion test (rtmi.cpp
+    lean_no_occ, rt_fast.h lean1q_loop MODE 2; its lit test is sg dy > 1e-6
+    with sg the side of the camera), otherwise they keep it (bias 1e-7, 0):
+    equal to the general kernels either way, camera above or below the plane."""
+    import torch
+    s = scenes.mesh_bunny()
+    s.cameraToWorld = scenes._std_camera(0.0, cam_y, 1.5)
+    ds = DeviceScene(s)
+    ref = torch.zeros(256 * 144 * 3, dtype=torch.float32, device="cuda")
+    st_ref = ds.render_device(_opts(256, 144, 16, RT_FLAG_NO_LEAN1 | RT_FLAG_NO_GEN1, bias=bias), ref)
+    for flags in (0, RT_FLAG_NO_MIX):
+        fb = torch.zeros_like(ref)
+        st = ds.render_device(_opts(256, 144, 16, flags, bias=bias), fb)
+        assert st == st_ref and torch.equal(fb, ref), (cam_y, bias, flags, float((fb - ref).abs().max()))
+
+
 def test_no_split_without_records(gpu):
     """No lean kernel where no pixel can be lean: a point light (no skip
     bit), two meshes (no pixel records), fewer than 64 samples per pixel."""
