@@ -2660,6 +2660,7 @@ __device__ __forceinline__ void lean1q_loop(KP p, const int32_t* order, int ngro
         q0[h] = __builtin_fmaf(cx, cx, 1.0f);
         ay[h] = __builtin_fmaf(cx, p->cam[4], -p->cam[10]);
         if constexpr (MODE == 2) ay[h] = ay[h] * sg;
+        if constexpr (MODE == 2) q0[h] = gg >= 0 ? q0[h] : __builtin_nanf("");  // padding: rl NaN, never lit
         acc[h] = f3(0.0f, 0.0f, 0.0f);
       }
       // iters is a multiple of 4 (rtmi.cpp lean1_ok): four samples per step
@@ -2674,7 +2675,7 @@ __device__ __forceinline__ void lean1q_loop(KP p, const int32_t* order, int ngro
         const float rl = rsq(__builtin_fmaf(cy, cy, q0[h]));
         if constexpr (MODE == 2) {
           const float dys = __builtin_fmaf(cy, c7s, ay[h]) * rl;  // sg dy
-          const unsigned long long litm = bal(dys > 1e-6f) & vmask;
+          const unsigned long long litm = bal(dys > 1e-6f);  // (padding lanes: NaN)
           nlit += pc(litm);
 #ifdef RTMI_LEAN2_SELECT
           const bool lit = lane_in(litm);
