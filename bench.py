@@ -7,32 +7,31 @@
 One step = one full frame of BASELINE config C3 (mesh-bunny layout: baked
 bunny.geom 69,451 triangles + ground plane, 2 distant lights, akGrid 16x16 =
 256 samples per pixel, fp32 performance mode) rendered from a scene resident
-in HBM into a device framebuffer. With N GPUs the SAME frame is cut into
-4-row bands dealt round-robin to the ranks, each rank renders its bands and
-one RCCL gather + an on-GPU un-interleave assembles the frame on rank 0
-(strong scaling; every gather is inside the timed region, frame k's
+in HBM into a device framebuffer. Every step does the whole frame's work:
+the render call builds its camera-dependent data on the device (camera-ray
+face lists, pixel records with the shadow skip bits, the lean / general
+lists — rt_frame.h) and then traces every ray it counts; nothing that
+depends on the camera is kept between steps. What is built once per scene
+(BVH, light grids) depends on the geometry and the lights only.
+
+N = 1: one whole-frame call per step. N > 1 (torchrun): the same frame cut
+into 4-row bands dealt round-robin to the ranks; each rank builds and renders
+its own bands, one RCCL gather + an on-GPU un-interleave assembles the frame
+on rank 0 (strong scaling; every gather inside the timed region, frame k's
 overlapping frame k+1's render from a second band buffer).
 
 Printed (rank 0, one JSON line): value = (primary + shadow rays of all ranks)
 x K / max-over-ranks wall time, plus
-  roofline     — the render call (C3-C5, one mesh on one ground plane: the
-                 merged kernel k_render_mix1 — general pixels, then lean
-                 pixels; elsewhere the two-class launch k_render_gen +
-                 k_render_lean, or k_render_fast), HIP events on the stream it
-                 runs on, against the 8 TB/s HBM peak.
-                 `achieved` = SURVEY 8(d)'s algorithmic bytes per ray — 32 B
-                 per BVH box and 36 B per triangle the ray is tested against,
-                 + 12 B per pixel — summed over the rays with the per-lane
-                 counts of the algorithm the kernels execute (binned face
-                 lists, pixel records, BVH only for left-over lanes; from one
-                 instrumented launch), / the call's duration. `traffic` = the
-                 PMC-measured HBM bytes per launch (profiles/, or null); the
-                 kernels are not HBM-bound (one scalar record fetch serves 64
-                 lanes, the working set lives in the caches): `issue` holds
-                 the VALU / SALU issue utilisation from the committed PMC
-                 instruction counts, the actual limiter. The per-ray BVH model
-                 of round 1 (every ray traverses the scene BVH) is kept as
-                 `survey_bvh_model_gbs` for comparison only;
+  roofline     — the render kernels of the call (C3-C5: the merged kernel
+                 k_render_mix1), timed with HIP events inside the library
+                 (RT_FLAG_TIMING, the call's stream) in a pass after the
+                 timed region. The kernels are instruction-issue bound
+                 (wave-uniform scalar record fetches serve 64 lanes; the
+                 records live in the caches): bound "issue", achieved = wave64
+                 VALU instructions per second (PMC SQ_INSTS_VALU of the same
+                 kernels, profiles/pmc_summary.json, used only when its source
+                 hash matches these sources) against 1024 SIMDs x 2.4 GHz / 2
+                 cycles; HBM bytes per call from the same summary beside it;
   cpu_baseline — the fp64 oracle (the reference algorithm: linear objects,
                  brute-force mesh, scanline thread pool) on this host, 1 spp on
                  a bounded row subsample of the same frame (rank 0, N = 1 only).
@@ -53,8 +52,6 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md "Chip-level para
 SURVEY_BOX_BYTES = 32
 SURVEY_TRI_BYTES = 36
 PIXEL_BYTES = 12
-NODE_BYTES = 64        # what the kernel fetches: one BvhNode record (two child boxes + refs)
-TRI_BYTES = 64         # one TriFast record (v0, e2, -e1, -n, face id)
 BAND_H = 4             # rows per band (round-robin over ranks)
 
 
@@ -142,19 +139,27 @@ def cpu_baseline(scene, width, height, target_s, bvh=False):
 
 
 SIMDS = 1024           # MI355X: 256 CUs x 4 SIMDs (MI355X_MICROARCH.md)
+CUS = 256
 CLOCK_GHZ = 2.4        # peak engine clock
-VALU_CYCLES = 2        # a wave64 fp32 VALU instruction per SIMD (tools/micro/issue_rate.hip)
+VALU_CYCLES = 2        # a wave64 VALU instruction issues over 2 cycles per SIMD (MI355X_MICROARCH.md)
+VALU_PEAK_GINST = SIMDS * CLOCK_GHZ / VALU_CYCLES   # 1228.8 G wave64 VALU instructions / s
+SALU_PEAK_GINST = CUS * CLOCK_GHZ                   # one scalar unit per CU, one instruction per cycle
 
 
 def load_pmc(workload_key):
-    """Per-launch PMC figures of the render call from the committed summary
-    (profiles/pmc_summary.json, tools/pmc_summary.py), or None."""
+    """Per-call PMC figures of the render kernels from the committed summary
+    (profiles/pmc_summary.json, tools/pmc_summary.py) when it was measured on
+    these native sources (never mix two builds), else None."""
+    from rtmi._lib import kernel_source_hash
     p = os.path.join(REPO, "profiles", "pmc_summary.json")
     try:
         with open(p) as f:
-            return json.load(f).get(workload_key)
+            e = json.load(f).get(workload_key)
     except (OSError, ValueError):
         return None
+    if e is None or e.get("source_hash") != kernel_source_hash():
+        return None
+    return e
 
 
 def main():
@@ -197,9 +202,9 @@ def main():
     opts = Options(width=W, height=H, antialias=Antialias(akGrid, m), bias=1e-4,
                    precision=Precision.fp32, flags=args.flags)
     stream = torch.cuda.current_stream()
-    # the first frame of this camera and image size also builds its
-    # camera-dependent bins (pixel face lists, pixel records, lean/general
-    # lists): timed on its own, reported beside the steady-state frame
+    # the first frame of this scene and image size also allocates the
+    # per-call buffers and reads the camera-ray list size once (every frame
+    # builds the lists themselves): timed on its own, beside the steps
     if not distributed:
         fb0 = torch.zeros(H * W * 3, dtype=torch.float32, device="cuda")
         torch.cuda.synchronize()
@@ -249,18 +254,16 @@ def main():
             pending[0] = gather_bands(buf, gathered if rank == 0 else None, rows * W * 3, async_op=True)
 
     # warmup (+ the deterministic per-frame ray counts)
-    # two instrumented launches (RT_FLAG_COUNT_TRAVERSAL): the per-ray BVH
-    # visit / test counts of SURVEY 8(d)'s algorithmic bytes (BVH for every
-    # ray: RT_FLAG_NO_BINNING), and the records the kernel really fetches
-    # (camera / shadow rays searching their pixel lists and light grids)
-    from rtmi.abi import RT_FLAG_COUNT_TRAVERSAL, RT_FLAG_NO_BINNING
+    from rtmi.abi import RT_FLAG_COUNT_TRAVERSAL, RT_FLAG_NO_BINNING, RT_FLAG_TIMING
     import dataclasses
+    st = ds.render_bands_device(opts, local_buf, BAND_H, rank, world, stream=stream, stats=True)
+    # SURVEY 8(d)'s per-ray BVH model (every ray traverses the scene BVH):
+    # node visits / triangle tests of one instrumented launch of the BVH path
+    # (k_render_fast<true>, RT_FLAG_COUNT_TRAVERSAL | RT_FLAG_NO_BINNING) —
+    # a model of what a per-ray BVH tracer would read, not the timed kernels
     copts = dataclasses.replace(opts, flags=opts.flags | RT_FLAG_COUNT_TRAVERSAL | RT_FLAG_NO_BINNING)
-    st = ds.render_bands_device(copts, local_buf, BAND_H, rank, world, stream=stream, stats=True)
+    ds.render_bands_device(copts, local_buf, BAND_H, rank, world, stream=stream, stats=True)
     counters = ds.last_counters()
-    kopts = dataclasses.replace(opts, flags=opts.flags | RT_FLAG_COUNT_TRAVERSAL)
-    ds.render_bands_device(kopts, local_buf, BAND_H, rank, world, stream=stream, stats=False)
-    kcounters = ds.last_counters()
     for _ in range(max(0, args.warmup)):
         step()
     finish_frame()
@@ -291,7 +294,7 @@ def main():
         e = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
-    kern_ms = sum(a.elapsed_time(b) for a, b in evs) / max(1, args.steps)
+    call_ms = sum(a.elapsed_time(b) for a, b in evs) / max(1, args.steps)
     lean_groups, general_groups = ds.last_split()
     kinds = ds.last_lean_kernel()
     lean_k = {0: None, 1: "k_render_lean", 2: "k_render_lean1q (one-plane lean pixels)", 3: None}[kinds & 3]
@@ -299,6 +302,18 @@ def main():
              3: None}[kinds >> 2 & 3]
     kernel_desc = ("k_render_mix1 (one-plane scene: general pixels, then lean pixels, one merged kernel)"
                    if kinds == 15 else f"{gen_k} + {lean_k} (two-class launch)" if lean_k else gen_k)
+    # after the timed region, the same steps once more with RT_FLAG_TIMING:
+    # HIP events inside the library split each call into its per-call
+    # camera-dependent build and its render kernels (each call waited for)
+    topts = dataclasses.replace(opts, flags=opts.flags | RT_FLAG_TIMING)
+    setup_ms, render_ms = [], []
+    for _ in range(args.steps):
+        ds.render_bands_device(topts, local_bufs[0], BAND_H, rank, world, stream=stream, stats=False)
+        a_ms, b_ms = ds.last_timing()
+        setup_ms.append(a_ms)
+        render_ms.append(b_ms)
+    setup_ms = sum(setup_ms) / len(setup_ms)
+    render_ms = sum(render_ms) / len(render_ms)
     # outside the timed region: one more launch with Stats, for how many of
     # the batched general pixels fell back to the one-sample loop
     ds.render_bands_device(opts, local_bufs[0], BAND_H, rank, world, stream=stream, stats=True)
@@ -313,33 +328,49 @@ def main():
         frame_check = {"bit_identical_to_single_call_frame": bool(torch.equal(ref, fb))}
 
     value = rays_frame * args.steps / elapsed / 1e6
-    # algorithmic bytes of one launch on this rank, SURVEY.md 8(d): per ray
-    # 32 B x boxes tested + 36 B x triangles tested + 12/spp B, summed over
-    # the launch's rays with the per-lane counts of the executed algorithm
-    # (binned lists, pixel records, BVH for left-over lanes only)
-    bytes_launch = (kcounters["lane_node_visits"] * 2 * SURVEY_BOX_BYTES
-                    + kcounters["lane_tri_tests"] * SURVEY_TRI_BYTES + rows * W * PIXEL_BYTES)
-    achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
-    # round 1's model: every ray traverses the scene BVH (what a per-ray
-    # BVH tracer would need; the kernels skip most of it)
+    # SURVEY 8(d)'s per-ray BVH byte model over this launch's rays (what a
+    # per-ray BVH tracer would read; these kernels skip most of it)
     bvh_model_bytes = (counters["lane_node_visits"] * 2 * SURVEY_BOX_BYTES
                        + counters["lane_tri_tests"] * SURVEY_TRI_BYTES + rows * W * PIXEL_BYTES)
-    # what the wave-coherent kernels request: one record fetch serves all 64
-    # lanes of a wave (binned searches: + a 4-B list entry per face)
-    fetch_bytes = (kcounters["wave_node_fetches"] * NODE_BYTES + kcounters["wave_tri_fetches"] * (TRI_BYTES + 4)
-                   + rows * W * PIXEL_BYTES)
     workload_key = f"{args.config.lower()}_{W}x{H}_m{m}_world{world}"
     pmc = load_pmc(workload_key)
-    traffic = None if pmc is None or "hbm_bytes_per_launch" not in pmc else float(pmc["hbm_bytes_per_launch"])
-    issue = None
-    if pmc is not None and "SQ_INSTS_VALU" in pmc.get("counters_mean_per_dispatch", {}):
+    roof = {"bound": "issue", "achieved": None, "peak": VALU_PEAK_GINST, "unit": "G wave64 VALU inst/s",
+            "frac": None, "traffic": None}
+    if pmc is not None:
         c = pmc["counters_mean_per_dispatch"]
-        cyc = kern_ms * 1e-3 * CLOCK_GHZ * 1e9
-        issue = {"valu_busy": round(c["SQ_INSTS_VALU"] * VALU_CYCLES / SIMDS / cyc, 3),
-                 "salu_busy": round(c["SQ_INSTS_SALU"] / (SIMDS // 4) / cyc, 3),
-                 "note": ("PMC instruction counts per call (committed summary) over this run's call time at "
-                          f"{CLOCK_GHZ} GHz: VALU {VALU_CYCLES} cycles per wave64 instruction per SIMD, SALU one "
-                          "instruction per cycle per CU (shared by its 4 SIMDs)")}
+        sec = render_ms * 1e-3
+        if "SQ_INSTS_VALU" in c:
+            ach = c["SQ_INSTS_VALU"] / sec / 1e9
+            roof["achieved"] = round(ach, 1)
+            roof["frac"] = round(ach / VALU_PEAK_GINST, 4)
+        if "SQ_INSTS_SALU" in c:
+            roof["salu_frac"] = round(c["SQ_INSTS_SALU"] / sec / 1e9 / SALU_PEAK_GINST, 4)
+        if "hbm_bytes_per_launch" in pmc:
+            roof["traffic"] = int(pmc["hbm_bytes_per_launch"])
+            roof["hbm_gbs"] = round(pmc["hbm_bytes_per_launch"] / sec / 1e9, 1)
+            roof["hbm_frac"] = round(pmc["hbm_bytes_per_launch"] / sec / 1e9 / HBM_PEAK_GBS, 4)
+        roof["pmc"] = f"profiles/pmc_summary.json[{workload_key}] (sources {pmc['source_hash']}): {pmc.get('note', '')}"
+    else:
+        roof["pmc"] = "no PMC summary for these native sources (profiles/pmc_summary.json): achieved / frac null"
+    roof.update({
+        "kernel": "render kernels: " + kernel_desc,
+        "kernel_ms": round(render_ms, 4),
+        "setup_ms": round(setup_ms, 4),
+        "call_ms": round(call_ms, 4),
+        "definition": ("achieved = PMC SQ_INSTS_VALU of the render kernels per call / their duration (HIP events "
+                       "inside the library, RT_FLAG_TIMING pass after the timed region); peak = 1024 SIMDs x "
+                       f"{CLOCK_GHZ} GHz / {VALU_CYCLES} cycles per wave64 VALU instruction; salu_frac likewise "
+                       "against one scalar instruction per CU per cycle; traffic = PMC HBM bytes per call "
+                       "(2 x FETCH_SIZE + WRITE_SIZE, MI355X_MICROARCH.md)"),
+        "setup": ("per-call camera-dependent build on the device (rt_frame.hip: face-list count / scan / fill, "
+                  "pixel records + lean/general lists), inside every timed step"),
+        "survey_bvh_model_gbs": round(bvh_model_bytes / (render_ms * 1e-3) / 1e9, 1),
+        "survey_bvh_model_note": ("SURVEY 8(d) bytes of a per-ray BVH tracer (32 B/box, 36 B/triangle, 12 B/pixel) "
+                                  "from one instrumented BVH-only launch, over the render kernels' time: a model, "
+                                  "not traffic (the kernels share each record fetch across 64 lanes)"),
+        "bvh_model_lane_node_visits": counters["lane_node_visits"],
+        "bvh_model_lane_tri_tests": counters["lane_tri_tests"],
+    })
 
     if rank == 0:
         out = {
@@ -359,43 +390,20 @@ def main():
                      "boxes2": "synthetic rays over the reference's boxes2.nim scene",
                      "torus": "synthetic rays over a deterministic procedural 1M-triangle torus"}[scene_name],
             "config": {
-                "workload": (f"{desc}, {W}x{H}, akGrid {m}x{m} = {m * m} spp, fp32, {BAND_H}-row bands "
-                             f"round-robin over {world} GPU(s) + RCCL gather to rank 0"),
+                "workload": (f"{desc}, {W}x{H}, akGrid {m}x{m} = {m * m} spp, fp32, "
+                             + (f"{BAND_H}-row bands round-robin over {world} ranks (one GPU each) + RCCL gather "
+                                "to rank 0" if distributed else "one whole-frame call per step on one GPU")
+                             + "; every step builds its camera-dependent data on the device"),
                 "width": W, "height": H, "spp": m * m, "triangles": info["num_triangles"],
                 "bvh_nodes": info["num_bvh_nodes"], "primary_rays_per_frame": prim_frame,
                 "shadow_rays_per_frame": shadow_frame, "parallelism": f"bands{world}",
                 "scene_setup_s": round(setup_s, 3), "scene_setup_ms_lib": round(info["build_ms"], 1),
-                "first_frame_ms": None if first_frame_ms is None else round(first_frame_ms, 1),
+                "first_frame_ms": None if first_frame_ms is None else round(first_frame_ms, 3),
                 "lean_pixel_groups": lean_groups, "general_pixel_groups": general_groups,
                 "batched_general_groups": batched_groups, "batch_fallback_groups": batch_fallback,
                 "bvh_builder": {"sah": "host binned SAH", "ploc": "device PLOC"}[args.bvh],
             },
-            "roofline": {
-                "bound": "hbm",
-                "achieved": round(achieved, 1),
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": traffic,
-                "kernel": "render call: " + kernel_desc,
-                "kernel_ms": round(kern_ms, 4),
-                "bytes_per_launch": int(bytes_launch),
-                "definition": ("SURVEY 8(d) per-ray bytes (32 B/BVH box + 36 B/triangle tested, 12 B/pixel) over "
-                               "the per-lane tests the kernels execute (binned face lists, pixel records, BVH for "
-                               "left-over lanes)"),
-                "limiter": ("instruction issue (SALU + VALU), not HBM: one scalar record fetch serves 64 lanes and "
-                            "the records live in the caches (traffic << achieved)"),
-                "issue": issue,
-                "record_fetch_bytes_per_launch": int(fetch_bytes),
-                "record_fetch_gbs": round(fetch_bytes / (kern_ms * 1e-3) / 1e9, 1),
-                "survey_bvh_model_gbs": round(bvh_model_bytes / (kern_ms * 1e-3) / 1e9, 1),
-                "kernel_lane_node_visits": kcounters["lane_node_visits"],
-                "kernel_lane_tri_tests": kcounters["lane_tri_tests"],
-                "kernel_wave_node_fetches": kcounters["wave_node_fetches"],
-                "kernel_wave_tri_fetches": kcounters["wave_tri_fetches"],
-                "bvh_model_lane_node_visits": counters["lane_node_visits"],
-                "bvh_model_lane_tri_tests": counters["lane_tri_tests"],
-            },
+            "roofline": roof,
             "cpu_baseline": None,
         }
         if frame_check is not None:

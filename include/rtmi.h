@@ -201,6 +201,11 @@ typedef struct rt_options {
  * lean pixels' kernels separately. By default both lists run in one merged
  * kernel (general items first, then lean ones). Same image and Stats. */
 #define RT_FLAG_NO_MIX 0x400u
+/* Record HIP events (on the call's stream) around the call's two parts: the
+ * camera-dependent data it builds on the device (camera-ray face lists, pixel
+ * records, lean / general lists, object masks) and its render kernels;
+ * rt_scene_last_timing reads them. Same image and Stats. */
+#define RT_FLAG_TIMING 0x800u
 
 /* Stats (src/renderer/stats.nim:4-13) plus ray counts for Mray/s. */
 typedef struct rt_stats {
@@ -255,6 +260,16 @@ int rt_scene_create(const rt_scene_desc *desc, rt_scene **out_scene);
 int rt_scene_destroy(rt_scene *scene);
 int rt_scene_get_info(const rt_scene *scene, rt_scene_info *out);
 
+/* Replace the scene's camera: Scene.cameraToWorld (column-major, glm) and
+ * Scene.fov in degrees (scene.nim:14-16), which renderLine re-reads on every
+ * call (renderer.nim:135-136, 150-153 via castPrimaryRay :31-44). Takes
+ * effect from the next render call; the geometry, BVH and light grids are
+ * kept (every camera-dependent structure is rebuilt by each render call
+ * anyway). Waits for the scene's earlier calls. RT_E_INVALID for a non-finite
+ * matrix or a fov outside (0, 180). */
+int rt_scene_set_camera(rt_scene *scene, const double camera_to_world[16],
+                        double fov_deg);
+
 /* ---- rendering ----------------------------------------------------------
  * All render calls implement renderLine (renderer.nim:162-211) for every row
  * y in countup(y0, y1 - 1, step):
@@ -308,6 +323,11 @@ int rt_band_rows(int32_t height, int32_t band_h, int32_t world,
  * call set RT_FLAG_NO_STATS). */
 int rt_scene_last_stats(rt_scene *scene, rt_stats *out);
 
+/* Durations of the last call made with RT_FLAG_TIMING (waits for it): its
+ * per-call camera-dependent build and its render kernels (incl. the Stats
+ * reduction), in milliseconds. RT_E_INVALID if that call did not set the flag. */
+int rt_scene_last_timing(rt_scene *scene, double *setup_ms, double *render_ms);
+
 /* ---- one process, several GPUs (SURVEY.md 8(b) rt_render_frame_multi) ---- */
 
 /* The scene replicated on every listed device (a device may repeat: several
@@ -327,6 +347,9 @@ int rt_render_frame_multi_device(rt_multi *m, const rt_options *opts,
 /* Whole frame into the caller's host framebuffer (fb_w*fb_h*3 floats). */
 int rt_render_frame_multi(rt_multi *m, const rt_options *opts, float *fb,
                           int32_t fb_w, int32_t fb_h, rt_stats *out);
+/* rt_scene_set_camera on every rank's scene. */
+int rt_multi_set_camera(rt_multi *m, const double camera_to_world[16],
+                        double fov_deg);
 int rt_multi_destroy(rt_multi *m);
 
 /* ---- render queue (workerpool.nim WorkerPool[WorkMsg, ResponseMsg]) ---- */

@@ -8,6 +8,7 @@
 #include <cmath>
 #include <cstdint>
 #include <cstdlib>
+#include <cstring>
 #include <limits>
 #include <thread>
 #include <unordered_map>
@@ -163,6 +164,57 @@ bool fill_bins(size_t nbins, size_t ntri, Emit emit, std::vector<int32_t>& off, 
 
 }  // namespace
 
+bool pixel_camera(const double o2w[16], const double w2o[16], const double c2w[16], double fov_deg, int width,
+                  int height, bg::PixCam* out) {
+  if (!invert4(c2w, out->w2c)) return false;
+  std::memcpy(out->o2w, o2w, sizeof out->o2w);
+  // camera constants of the float32 kernel (rtmi.cpp fill_fast): a camera-space
+  // direction (cx, cy, -1) is the sample at px = w/2 + cx/a, py = h/2 - cy/c
+  const double f = std::tan(fov_deg * (3.14159265358979323846 / 180.0) / 2);
+  const double r = (double)width / (double)height;
+  out->cam_a = 2.0 * r * f / (double)width;
+  out->cam_c = 2.0 * f / (double)height;
+  const double cw[3] = {c2w[12], c2w[13], c2w[14]};
+  xform_point(w2o, cw, out->co);  // camera origin in object space
+  // |rd| of a unit world direction lies in [1/|o2w|, |w2o|]
+  out->rd_max = frob3(w2o);
+  out->rd_min = 1.0 / frob3(o2w);
+  out->margin = kPixelMargin;
+  out->width = width;
+  out->height = height;
+  return true;
+}
+
+bool skip_camera(const std::vector<SkipPlane>& planes, const double mesh_w2o[16], const double c2w[16],
+                 double fov_deg, int width, int height, double bias, bg::SkipCam* cam,
+                 std::vector<bg::SkipPlaneC>* pc) {
+  std::memcpy(cam->c2w, c2w, sizeof cam->c2w);
+  std::memcpy(cam->mesh_w2o, mesh_w2o, sizeof cam->mesh_w2o);
+  for (int k = 0; k < 3; ++k) cam->cw[k] = c2w[12 + k];
+  const double f = std::tan(fov_deg * (3.14159265358979323846 / 180.0) / 2);
+  const double r = (double)width / (double)height;
+  cam->cam_a = 2.0 * r * f / (double)width;
+  cam->cam_c = 2.0 * f / (double)height;
+  cam->margin = kPixelMargin;
+  cam->bias = bias;
+  cam->width = width;
+  cam->height = height;
+  pc->assign(planes.size(), bg::SkipPlaneC{});
+  for (size_t k = 0; k < planes.size(); ++k) {
+    double o[3];
+    xform_point(planes[k].w2o, cam->cw, o);
+    bg::SkipPlaneC& P = (*pc)[k];
+    P.oy = o[1];
+    for (int c = 0; c < 3; ++c) {
+      P.row[c] = planes[k].w2o[c * 4 + 1];
+      P.n[c] = planes[k].o2w[1 * 4 + c];
+    }
+    P.tol = 1e-5 * frob3(planes[k].w2o);
+    if (!(std::fabs(o[1]) > 1e-9)) return false;  // the camera lies on a plane: no pixel qualifies
+  }
+  return true;
+}
+
 bool build_pixel_bins(const std::vector<BinTri>& tris, const double o2w[16], const double w2o[16],
                       const double c2w[16], double fov_deg, int width, int height, PixelBinsHost* out,
                       const char** why) {
@@ -171,74 +223,28 @@ bool build_pixel_bins(const std::vector<BinTri>& tris, const double o2w[16], con
     *why = "empty image";
     return false;
   }
-  double w2c[16];
-  if (!invert4(c2w, w2c)) {
+  bg::PixCam pc;
+  if (!pixel_camera(o2w, w2o, c2w, fov_deg, width, height, &pc)) {
     *why = "singular camera";
     return false;
   }
-  // camera constants of the float32 kernel (rtmi.cpp fill_fast): a camera-space
-  // direction (cx, cy, -1) is the sample at px = w/2 + cx/a, py = h/2 - cy/c
-  const double f = std::tan(fov_deg * (3.14159265358979323846 / 180.0) / 2);
-  const double r = (double)width / (double)height;
-  const double cam_a = 2.0 * r * f / (double)width, cam_c = 2.0 * f / (double)height;
-  const double cw[3] = {c2w[12], c2w[13], c2w[14]};
-  double co[3];
-  xform_point(w2o, cw, co);  // camera origin in object space
-  // |rd| of a unit world direction lies in [1/|o2w|, |w2o|]
-  const double rd_max = frob3(w2o), rd_min = 1.0 / frob3(o2w);
   const double margin = kPixelMargin;
   // per face: pixel rectangle (or empty) and projected vertices
+  // (rt_bins_geom.h face_pixel_rect, shared with the per-frame device builder)
   std::vector<int32_t> rect(tris.size() * 4, -1);
   std::vector<double> proj(tris.size() * 6, 0.0);
   for (size_t i = 0; i < tris.size(); ++i) {
-    const BinTri& t = tris[i];
-    double e1[3], e2[3], c[3], nn[3], dc[3];
-    for (int k = 0; k < 3; ++k) {
-      e1[k] = t.v[1][k] - t.v[0][k];
-      e2[k] = t.v[2][k] - t.v[0][k];
-      dc[k] = t.v[0][k] - co[k];
+    if (!bg::face_pixel_rect(pc, tris[i].v, &proj[6 * i], &rect[4 * i])) {
+      *why = "a mesh vertex lies at or behind the camera plane";
+      return false;
     }
-    cross3(e1, e2, c);
-    for (int k = 0; k < 3; ++k) nn[k] = -c[k];
-    const double nlen = norm3(nn);
-    // every camera ray reaching the face's plane has det = |rd| (v0 - C).nn / |P - C|
-    const double s = dot3(dc, nn);
-    double maxd = 0.0;
-    for (int v = 0; v < 3; ++v) {
-      double dv[3] = {t.v[v][0] - co[0], t.v[v][1] - co[1], t.v[v][2] - co[2]};
-      maxd = std::max(maxd, norm3(dv));
-    }
-    if (s <= 0.0 && maxd > 0.0 && never_passes(rd_min * s / maxd, rd_max, nlen)) continue;  // back face
-    double xmin = INFINITY, xmax = -INFINITY, ymin = INFINITY, ymax = -INFINITY;
-    for (int v = 0; v < 3; ++v) {
-      double pw[3], pc[3];
-      xform_point(o2w, t.v[v], pw);
-      xform_point(w2c, pw, pc);
-      if (!(pc[2] < -1e-9 * (1.0 + std::fabs(pc[0]) + std::fabs(pc[1])))) {
-        *why = "a mesh vertex lies at or behind the camera plane";
-        return false;
-      }
-      const double px = 0.5 * width + (pc[0] / -pc[2]) / cam_a;
-      const double py = 0.5 * height - (pc[1] / -pc[2]) / cam_c;
-      proj[6 * i + 2 * v] = px;
-      proj[6 * i + 2 * v + 1] = py;
-      xmin = std::min(xmin, px);
-      xmax = std::max(xmax, px);
-      ymin = std::min(ymin, py);
-      ymax = std::max(ymax, py);
-    }
-    if (!(xmax + margin >= 0.0 && ymax + margin >= 0.0 && xmin - margin < width && ymin - margin < height)) continue;
-    rect[4 * i + 0] = (int32_t)std::max(0.0, std::floor(xmin - margin));
-    rect[4 * i + 1] = (int32_t)std::min((double)width - 1, std::floor(xmax + margin));
-    rect[4 * i + 2] = (int32_t)std::max(0.0, std::floor(ymin - margin));
-    rect[4 * i + 3] = (int32_t)std::min((double)height - 1, std::floor(ymax + margin));
   }
   auto emit = [&](size_t i, auto&& put) {
     if (rect[4 * i] < 0) return;
     const double* q = &proj[6 * i];
     for (int32_t y = rect[4 * i + 2]; y <= rect[4 * i + 3]; ++y)
       for (int32_t x = rect[4 * i + 0]; x <= rect[4 * i + 1]; ++x)
-        if (tri_meets_box(q, x - margin, y - margin, x + 1 + margin, y + 1 + margin))
+        if (bg::tri_meets_box(q, x - margin, y - margin, x + 1 + margin, y + 1 + margin))
           put((size_t)y * (size_t)width + (size_t)x, tris[i].rec);
   };
   return fill_bins((size_t)width * (size_t)height, tris.size(), emit, out->off, out->ent, why);
@@ -390,6 +396,20 @@ bool build_light_grid(const std::vector<BinTri>& tris, const double w2o[16], con
   return true;
 }
 
+void skip_grid(const GridOcc& go, bg::SkipGrid* out) {
+  const LightGrid& g = go.g;
+  for (int k = 0; k < 3; ++k) {
+    out->e1[k] = g.e1[k];
+    out->e2[k] = g.e2[k];
+  }
+  out->u0 = g.u0;
+  out->v0 = g.v0;
+  out->inv_h = g.inv_h;
+  out->gu = g.gu;
+  out->gv = g.gv;
+  out->sat = go.sat.empty() ? nullptr : go.sat.data();
+}
+
 void grid_occupancy(const LightGridHost& lg, GridOcc* out) {
   out->g = lg.g;
   out->sat.clear();
@@ -428,6 +448,39 @@ bool build_shadow_skips(const std::vector<int32_t>& pix_off, const std::vector<S
   unsigned have = 0;
   for (int l = 0; l < nl; ++l) have |= grids[(size_t)l].g.gu > 0 ? 1u << l : 0u;
   if (have == 0) return true;
+  if (!sl || sl_nl <= 0) {  // the bits alone: rt_bins_geom.h pixel_skip_bits, as the device builder forms them
+    bg::SkipCam cam;
+    std::vector<bg::SkipPlaneC> pcs;
+    if (!skip_camera(planes, mesh_w2o, c2w, fov_deg, width, height, bias, &cam, &pcs)) {
+      *why = "the camera lies on a plane";
+      return true;  // no pixel qualifies
+    }
+    std::vector<bg::SkipGrid> sg((size_t)nl);
+    for (int l = 0; l < nl; ++l) skip_grid(grids[(size_t)l], &sg[(size_t)l]);
+    std::vector<uint8_t> bytes(npx, 0);
+    auto rows = [&](int64_t ya, int64_t yb) {
+      for (int64_t y = ya; y < yb; ++y)
+        for (int x = 0; x < width; ++x) {
+          const size_t pix = (size_t)y * width + x;
+          if (pix_off[pix + 1] != pix_off[pix]) continue;  // camera rays may hit the mesh
+          bytes[pix] = (uint8_t)bg::pixel_skip_bits(cam, pcs.data(), (int)pcs.size(), sg.data(), nl, have, x, (int)y);
+        }
+    };
+    const int nt = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    if (nt == 1 || npx < 65536) {
+      rows(0, height);
+    } else {
+      std::vector<std::thread> th;
+      const int chunk = (height + nt - 1) / nt;
+      for (int t = 0; t < nt; ++t) {
+        const int ya = t * chunk, yb = std::min(height, ya + chunk);
+        if (ya < yb) th.emplace_back(rows, ya, yb);
+      }
+      for (auto& t : th) t.join();
+    }
+    for (size_t pix = 0; pix < npx; ++pix) (*out)[pix >> 2] |= (uint32_t)bytes[pix] << (8 * (pix & 3));
+    return true;
+  }
   // the kernel's camera constants (as in build_pixel_bins); a corner ray of
   // pixel (x, y) passes through (x +- margin, y +- margin)
   const double f = std::tan(fov_deg * (3.14159265358979323846 / 180.0) / 2);

@@ -21,6 +21,7 @@
 
 #include <vector>
 
+#include "rt_bins_geom.h"
 #include "rt_common.h"
 
 namespace rtmi {
@@ -85,9 +86,19 @@ struct GridOcc {
   const LightGridHost* lists = nullptr;  // the grid's cell lists and face boxes (shadow lists)
 };
 void grid_occupancy(const LightGridHost& lg, GridOcc* out);
+void skip_grid(const GridOcc& go, bg::SkipGrid* out);  // the skip test's view (sat points into go)
 struct SkipPlane {
   double o2w[16], w2o[16];       // a plane object's transforms (y = 0 in object space)
 };
+// Per-camera constants of the camera-ray bins (rt_bins_geom.h PixCam) and of
+// the shadow skips (SkipCam + one SkipPlaneC per plane); false: a singular
+// camera (pixel_camera) or a camera on a plane (skip_camera: no pixel
+// qualifies).
+bool pixel_camera(const double o2w[16], const double w2o[16], const double c2w[16], double fov_deg, int width,
+                  int height, bg::PixCam* out);
+bool skip_camera(const std::vector<SkipPlane>& planes, const double mesh_w2o[16], const double c2w[16],
+                 double fov_deg, int width, int height, double bias, bg::SkipCam* cam,
+                 std::vector<bg::SkipPlaneC>* pc);
 // pix_off: the pixel lists' offsets (w * h + 1); out: one byte per pixel,
 // packed four to a dword (pixel 4i + k in byte k of out[i]).
 //

@@ -256,16 +256,11 @@ struct FastParams {
   // k_render_mix1's second list (lean pixels, k_render_lean1q items) and its shard count
   const int32_t* order2;
   int32_t ngroups2, shards2;
-  // every distant light's direction on the same side of the plane y = const
-  // (1e-6 < |dir.y| <= 1, one sign), or none off it, with finite colours,
-  // albedos and coordinates: k_render_lean1q / _mix1 test a lit sample's
-  // shadow rays with one class test (host-side choice of the kernel
-  // instantiation, rtmi.cpp; conditions in rt_fast.h lean1q_loop)
-  int32_t lights_one_side;
-  // lights_one_side with every light above the plane and a bias the
-  // rounding of the shadow origin cannot cancel: no lit lean sample is
-  // occluded (rt_fast.h lean1q_loop MODE 2; conditions in rtmi.cpp fill_fast)
-  int32_t lean_no_occ;
+  // two-class launches: the entry counts of the lists at order / order2,
+  // counted on the device by this call's k_frame_records (rt_frame.h), or
+  // nullptr (the lists' lengths are ngroups / ngroups2, items of the kernel)
+  const int32_t* list_n;
+  const int32_t* list_n2;
 };
 
 enum : int32_t {
@@ -296,12 +291,12 @@ int rtmi_render_f32_blocks_per_cu(int count, unsigned subset, size_t shmem);
 int rtmi_launch_lean_f32(const rtmi::FastParams* p, unsigned subset, int blocks, size_t shmem, void* stream);
 int rtmi_lean_f32_blocks_per_cu(unsigned subset, size_t shmem);
 int rtmi_launch_lean1_f32(const rtmi::FastParams* p, int nl, int lp, int blocks, void* stream);
-int rtmi_lean1_f32_blocks_per_cu(int nl);
+int rtmi_lean1_f32_blocks_per_cu(int nl, int lp);
 int rtmi_lean1_quads();
 int rtmi_launch_gen1_f32(const rtmi::FastParams* p, int nl, int blocks, void* stream);
 int rtmi_gen1_f32_blocks_per_cu(int nl);
 int rtmi_launch_mix1_f32(const rtmi::FastParams* p, int nl, int lp, int blocks, void* stream);
-int rtmi_mix1_f32_blocks_per_cu(int nl);
+int rtmi_mix1_f32_blocks_per_cu(int nl, int lp);
 int rtmi_launch_gen_f32(const rtmi::FastParams* p, unsigned subset, int blocks, size_t shmem, void* stream);
 int rtmi_gen_f32_blocks_per_cu(unsigned subset, size_t shmem);
 int rtmi_launch_ppm_encode(const float* fb, long long n, int bits, int srgb, void* out, void* stream);

@@ -59,6 +59,13 @@ __device__ __forceinline__ const RT_CONST T& at(const T* base, int i) {
   return *(const RT_CONST T*)((const RT_CONST char*)base + (unsigned)i * (unsigned)sizeof(T));
 }
 
+// Work items of a two-class launch's list: its entry count as this call's
+// k_frame_records counted it on the device (n, rt_frame.h; per_item entries
+// per item), or the host's item count when the list is not counted.
+__device__ __forceinline__ int list_items(const int32_t* n, int host_items, int per_item) {
+  return n ? (cp(n)[0] + per_item - 1) / per_item : host_items;
+}
+
 __device__ __forceinline__ unsigned long long bal(bool p) { return __builtin_amdgcn_ballot_w64(p); }
 // Lane masks straight from a v_cmp (llvm.amdgcn.fcmp: ordered >= / <) and a
 // mask back to a per-lane predicate (llvm.amdgcn.inverse.ballot): a ballot of
@@ -2153,7 +2160,8 @@ __global__ __launch_bounds__(256) RTMI_OCC void k_render_fast(const FastParams p
 #endif
   int g = qj * p->shards + shard;
   int nflush = 0;
-  while (g < p->ngroups) {
+  const int ngroups = list_items(p->list_n, p->ngroups, 1);
+  while (g < ngroups) {
     p = params();
     const int L = p->lanes_per_px;
     const int iters = p->iters;
@@ -2288,12 +2296,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RTMI_LEAN_W
   static_assert(kLeanRun == 4, "a run is one s_load_dwordx4");
   using Run = int32_t __attribute__((ext_vector_type(4)));
   const RT_CONST Run* runs = (const RT_CONST Run*)cp(p->order);
-  Run ent = g < p->ngroups ? runs[g] : Run{-1, -1, -1, -1};
-  while (g < p->ngroups) {
+  const int nruns = list_items(p->list_n, p->ngroups, kLeanRun);
+  Run ent = g < nruns ? runs[g] : Run{-1, -1, -1, -1};
+  while (g < nruns) {
     qj = __builtin_amdgcn_readfirstlane(qj_next);
     if (lane == 0) qj_next = (int)atomicAdd(head, 1u);
     const int gn = qj * p->shards + shard;
-    const Run ent_next = gn < p->ngroups ? runs[gn] : Run{-1, -1, -1, -1};
+    const Run ent_next = gn < nruns ? runs[gn] : Run{-1, -1, -1, -1};
 #pragma unroll 1
     for (int r = 0; r < kLeanRun; ++r) {
       const int gg = ent.x;  // the entries shift down (static swizzles, no indexed SGPR access)
@@ -2349,40 +2358,6 @@ __device__ __forceinline__ unsigned long long m_hit0(float t) {
   asm("v_cmp_class_f32_e64 %0, %1, %2" : "=s"(m) : "v"(t), "v"(0x1E0));
   return m;
 }
-// v_cmp_class with a run-time class mask (bits: 3 -normal, 4 -denormal,
-// 5 -0, 6 +0, 7 +denormal, 8 +normal; 0: never)
-__device__ __forceinline__ unsigned long long m_class(float x, int classes) {
-  unsigned long long m;
-  asm("v_cmp_class_f32_e64 %0, %1, %2" : "=s"(m) : "v"(x), "v"(classes));
-  return m;
-}
-// acc += av on the lanes of `vis`, += bg on the lanes off `lit`, unchanged
-// elsewhere (the occluded samples, whose colour is +-0: see lean1q_loop):
-// two runs of three adds under EXEC instead of two selects per channel.
-// EXEC is restored before the block ends.
-__device__ __forceinline__ void acc_vis_bg(F3& acc, unsigned long long vis, unsigned long long lit, const F3& av,
-                                           const F3& bg) {
-  unsigned long long save;
-  asm volatile(
-      "s_mov_b64 %[sv], exec\n\t"
-      "s_and_b64 exec, %[sv], %[vis]\n\t"
-      "s_cbranch_execz .Lacc_vis_%=\n\t"
-      "v_add_f32 %[x], %[ax], %[x]\n\t"
-      "v_add_f32 %[y], %[ay], %[y]\n\t"
-      "v_add_f32 %[z], %[az], %[z]\n"
-      ".Lacc_vis_%=:\n\t"
-      "s_andn2_b64 exec, %[sv], %[lit]\n\t"
-      "s_cbranch_execz .Lacc_bg_%=\n\t"
-      "v_add_f32 %[x], %[bx], %[x]\n\t"
-      "v_add_f32 %[y], %[by], %[y]\n\t"
-      "v_add_f32 %[z], %[bz], %[z]\n"
-      ".Lacc_bg_%=:\n\t"
-      "s_mov_b64 exec, %[sv]"
-      : [x] "+v"(acc.x), [y] "+v"(acc.y), [z] "+v"(acc.z), [sv] "=&s"(save)
-      : [vis] "s"(vis), [lit] "s"(lit), [ax] "v"(av.x), [ay] "v"(av.y), [az] "v"(av.z), [bx] "v"(bg.x),
-        [by] "v"(bg.y), [bz] "v"(bg.z)
-      : "scc");
-}
 template <int NL>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k_render_lean1(
     const FastParams params_by_value) {
@@ -2433,12 +2408,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
   static_assert(kLeanRun == 4, "a run is one s_load_dwordx4");
   using Run = int32_t __attribute__((ext_vector_type(4)));
   const RT_CONST Run* runs = (const RT_CONST Run*)cp(p->order);
-  Run ent = g < p->ngroups ? runs[g] : Run{-1, -1, -1, -1};
-  while (g < p->ngroups) {
+  const int nruns = list_items(p->list_n, p->ngroups, kLeanRun);
+  Run ent = g < nruns ? runs[g] : Run{-1, -1, -1, -1};
+  while (g < nruns) {
     qj = __builtin_amdgcn_readfirstlane(qj_next);
     if (lane == 0) qj_next = (int)atomicAdd(head, 1u);
     const int gn = qj * p->shards + shard;
-    const Run ent_next = gn < p->ngroups ? runs[gn] : Run{-1, -1, -1, -1};
+    const Run ent_next = gn < nruns ? runs[gn] : Run{-1, -1, -1, -1};
 #pragma unroll 1
     for (int r = 0; r < kLeanRun; ++r) {
       const int gg = ent.x;
@@ -2545,7 +2521,7 @@ __device__ __forceinline__ GroupPix lane_pixel(KP p, int g) {
 // k_render_lean1q's work loop over one list (order: 64 / LP entries per
 // item, ngroups items, dequeued from the shard heads at `queue`); also the
 // second phase of k_render_mix1.
-template <int NL, int LP, int MODE>
+template <int NL, int LP>
 __device__ __forceinline__ void lean1q_loop(KP p, const int32_t* order, int ngroups, unsigned int* queue, int shards,
                                             Stats32& ws, unsigned long long* tot, int& nflush) {
   const int lane = (int)__lane_id();
@@ -2586,40 +2562,11 @@ __device__ __forceinline__ void lean1q_loop(KP p, const int32_t* order, int ngro
   constexpr int V = 64 / LP;   // virtual lanes per lane
   constexpr int PPI = 64 / LP; // pixels per work item
   const int q = lane & (LP - 1);  // this lane's share of its pixel's virtual lanes
-  // MODE 0: each light's shadow ray tested against the plane. MODE 1
-  // (rtmi.cpp lights_one_side): every light on the same side of the
-  // plane (plane reciprocals m_l finite, of one sign, |m_l| >= 1), or none
-  // with one (all NaN). A lit sample's shadow rays then all hit the plane or
-  // all miss it — ts_l = -(X) * m_l, X = soy + ty finite and far from
-  // overflow for a lit sample (the host bounds the camera, plane and bias),
-  // is >= 0 exactly when X <= 0 (m > 0) or X >= 0 (m < 0), zeros of either
-  // sign counting (no product underflows to a zero with |m| >= 1), and a NaN
-  // m_l never hits — so one class test of X decides them all, and the
-  // sample's colour is one of three wave-uniform values: albedo x E over all
-  // lights (formed in the order of the per-light loop below), albedo x E
-  // with every light occluded — +-0 for finite albedo and light colours,
-  // which leaves the running sum unchanged (it starts at +0 and is never
-  // -0) — and the background.
-  // MODE 2 (rtmi.cpp lean_no_occ): as MODE 1 with every light above the
-  // plane (m > 0) and a bias the host proved larger than the rounding of
-  // X = soy + ty (bias > 1e-6 (|cam y| + 2 |ty|): X > 0 for every lit
-  // sample), so no lit sample is occluded and its colour is albedo x E; with
-  // 1e-20 <= |nroy| <= 1e30 and a bounded camera, t = nroy rcp(dy) is
-  // finite and nonzero for |dy| > 1e-6, so the lit test "t in [-0, +inf),
-  // |dy| > 1e-6" is sg dy > 1e-6 (sg = the sign of nroy) — formed as
-  // fma(cy, sg c7, sg ay) rl, which is sg dy exactly (negation commutes with
-  // rounding): no t, no shadow origin.
-  const int occ_classes = __builtin_isnan(mulp[0]) ? 0 : (mulp[0] > 0.0f ? 0x78 : 0x1E0);
-  const float sg = nroy > 0.0f ? 1.0f : -1.0f, c7s = p->cam[7] * sg;
-  F3 av = f3(0.0f, 0.0f, 0.0f);
-  {
-    F3 ev = av;
-#pragma unroll
-    for (int l = 0; l < NL; ++l)
-      ev = f3(__builtin_fmaf(ci[l][0], ndl[l], ev.x), __builtin_fmaf(ci[l][1], ndl[l], ev.y),
-              __builtin_fmaf(ci[l][2], ndl[l], ev.z));
-    av = mul3(alb, ev);
-  }
+  // Every lit sample traces each light's shadow ray: against the plane here
+  // (ts = -(soy + ty) m_l, a hit at ts in [0, +inf) occludes it), against the
+  // mesh by the pixel's record — a lean pixel's skip bits, built this call
+  // (rt_frame.hip k_frame_records), say that no shadow ray leaving a camera
+  // hit of the pixel can meet a face of the mesh.
   while (g < ngroups) {
     const int gg = order[g * PPI + lane / LP];  // this lane's pixel (list entry; -1: padding)
     qj = __builtin_amdgcn_readfirstlane(qj_next);
@@ -2659,8 +2606,6 @@ __device__ __forceinline__ void lean1q_loop(KP p, const int32_t* order, int ngro
         const float cx = (px - p->cam_b) * p->cam_a;
         q0[h] = __builtin_fmaf(cx, cx, 1.0f);
         ay[h] = __builtin_fmaf(cx, p->cam[4], -p->cam[10]);
-        if constexpr (MODE == 2) ay[h] = ay[h] * sg;
-        if constexpr (MODE == 2) q0[h] = gg >= 0 ? q0[h] : __builtin_nanf("");  // padding: rl NaN, never lit
         acc[h] = f3(0.0f, 0.0f, 0.0f);
       }
       // iters is a multiple of 4 (rtmi.cpp lean1_ok): four samples per step
@@ -2673,18 +2618,6 @@ __device__ __forceinline__ void lean1q_loop(KP p, const int32_t* order, int ngro
       for (int h = 0; h < 2; ++h) {
         const float cy = cyc[it];
         const float rl = rsq(__builtin_fmaf(cy, cy, q0[h]));
-        if constexpr (MODE == 2) {
-          const float dys = __builtin_fmaf(cy, c7s, ay[h]) * rl;  // sg dy
-          const unsigned long long litm = bal(dys > 1e-6f);  // (padding lanes: NaN)
-          nlit += pc(litm);
-#ifdef RTMI_LEAN2_SELECT
-          const bool lit = lane_in(litm);
-          acc[h] = f3(acc[h].x + (lit ? av.x : bg.x), acc[h].y + (lit ? av.y : bg.y), acc[h].z + (lit ? av.z : bg.z));
-#else
-          acc_vis_bg(acc[h], litm, litm, av, bg);
-#endif
-          continue;
-        }
         const float dy = __builtin_fmaf(cy, p->cam[7], ay[h]) * rl;
         // (|dy| <= 1e-6: no hit; t is only read on lit lanes)
         const float t = nroy * rcp(dy);
@@ -2692,24 +2625,17 @@ __device__ __forceinline__ void lean1q_loop(KP p, const int32_t* order, int ngro
         nlit += pc(litm);
         const bool lit = lane_in(litm);
         const float soy = __builtin_fmaf(1.0f, bias, __builtin_fmaf(dy, t, oy));
-        if constexpr (MODE == 1) {
-          (void)lit;
-          const unsigned long long occ = m_class(soy + ty, occ_classes) & litm;  // every light's shadow ray alike
-          nocc += (unsigned)NL * pc(occ);
-          acc_vis_bg(acc[h], litm & ~occ, litm, av, bg);
-        } else {
-          F3 E = f3(0.0f, 0.0f, 0.0f);
+        F3 E = f3(0.0f, 0.0f, 0.0f);
 #pragma unroll
-          for (int l = 0; l < NL; ++l) {
-            const float ts = -(soy + ty) * mulp[l];
-            const unsigned long long occ = m_hit0(ts) & litm;
-            nocc += pc(occ);
-            const float x = lane_in(litm & ~occ) ? ndl[l] : 0.0f;
-            E = f3(__builtin_fmaf(ci[l][0], x, E.x), __builtin_fmaf(ci[l][1], x, E.y), __builtin_fmaf(ci[l][2], x, E.z));
-          }
-          const F3 a = mul3(alb, E);
-          acc[h] = f3(acc[h].x + (lit ? a.x : bg.x), acc[h].y + (lit ? a.y : bg.y), acc[h].z + (lit ? a.z : bg.z));
+        for (int l = 0; l < NL; ++l) {
+          const float ts = -(soy + ty) * mulp[l];
+          const unsigned long long occ = m_hit0(ts) & litm;
+          nocc += pc(occ);
+          const float x = lane_in(litm & ~occ) ? ndl[l] : 0.0f;
+          E = f3(__builtin_fmaf(ci[l][0], x, E.x), __builtin_fmaf(ci[l][1], x, E.y), __builtin_fmaf(ci[l][2], x, E.z));
         }
+        const F3 a = mul3(alb, E);
+        acc[h] = f3(acc[h].x + (lit ? a.x : bg.x), acc[h].y + (lit ? a.y : bg.y), acc[h].z + (lit ? a.z : bg.z));
       }
       }
       // push the pair's sum: pair index P = j / 2 pairs with the stack while
@@ -2767,7 +2693,7 @@ __device__ __forceinline__ void lean1q_loop(KP p, const int32_t* order, int ngro
   }
 }
 
-template <int NL, int LP, int MODE>
+template <int NL, int LP>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k_render_lean1q(
     const FastParams params_by_value) {
   (void)params_by_value;
@@ -2780,7 +2706,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
 #pragma unroll
   for (int k = 0; k < kStatSlots; ++k) ws.v[k] = 0u;
   int nflush = 0;
-  lean1q_loop<NL, LP, MODE>(p, p->order, p->ngroups, p->queue, p->shards, ws, lds_tot[wib], nflush);
+  lean1q_loop<NL, LP>(p, p->order, list_items(p->list_n, p->ngroups, 64 / LP), p->queue, p->shards, ws,
+                      lds_tot[wib], nflush);
   flush_stats(ws, lds_tot[wib], lane);
   const int wave = (int)(blockIdx.x * (blockDim.x >> 6) + threadIdx.x / 64u);
   if (lane < kStatSlots) p->partials[(size_t)wave * kStatSlots + lane] = lds_tot[wib][lane];
@@ -2823,7 +2750,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RTMI_GEN_WA
   if (__lane_id() == 0) qj_next = (int)atomicAdd(head, 1u);
   int g = qj * p->shards + shard;
   int nflush = 0;
-  while (g < p->ngroups) {
+  const int ngroups = list_items(p->list_n, p->ngroups, 1);
+  while (g < ngroups) {
     p = params();
     const int iters = p->iters;
     const int gg = cp(p->order)[g];
@@ -2898,7 +2826,8 @@ __device__ __forceinline__ void gen1_loop(KP p, LdsF* ls, Stats32& ws, unsigned 
   int qj_next = 0;
   if (__lane_id() == 0) qj_next = (int)atomicAdd(head, 1u);
   int g = qj * p->shards + shard;
-  while (g < p->ngroups) {
+  const int ngroups = list_items(p->list_n, p->ngroups, 1);
+  while (g < ngroups) {
     p = params();
     const int iters = p->iters;
     const int gg = cp(p->order)[g];
@@ -2974,7 +2903,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RTMI_GEN1_W
 // set of queue heads) — one ramp and one tail per launch instead of two, the
 // expensive items first and the cheap ones filling the tail. Frames and
 // Stats those of the two kernels.
-template <int NL, int LP, int MODE>
+template <int NL, int LP>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RTMI_GEN1_WAVES))) void k_render_mix1(
     const FastParams params_by_value) {
   (void)params_by_value;
@@ -2990,7 +2919,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RTMI_GEN1_W
   int nflush = 0;
   gen1_loop<NL>(p, ls, ws, lds_tot[wib], nflush);
   p = params();
-  lean1q_loop<NL, LP, MODE>(p, p->order2, p->ngroups2, p->queue + kQueueShards * kQueueStride, p->shards2, ws,
+  lean1q_loop<NL, LP>(p, p->order2, list_items(p->list_n2, p->ngroups2, 64 / LP), p->queue + kQueueShards * kQueueStride, p->shards2, ws,
                       lds_tot[wib], nflush);
   p = params();
   const int lane = (int)__lane_id();

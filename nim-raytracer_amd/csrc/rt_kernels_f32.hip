@@ -58,35 +58,18 @@ template __global__ void fast::k_render_fast<true, fast::F_ALL>(const FastParams
 // lean pixels of one-plane scenes (rtmi.cpp lean1_ok), one or two lights
 template __global__ void fast::k_render_lean1<1>(const FastParams);
 template __global__ void fast::k_render_lean1<2>(const FastParams);
-// (MODE 0: a plane test per light, 1: one for all, 2: none needed — rt_fast.h lean1q_loop)
-template __global__ void fast::k_render_lean1q<1, 4, 0>(const FastParams);
-template __global__ void fast::k_render_lean1q<1, 4, 1>(const FastParams);
-template __global__ void fast::k_render_lean1q<1, 4, 2>(const FastParams);
-template __global__ void fast::k_render_lean1q<2, 4, 0>(const FastParams);
-template __global__ void fast::k_render_lean1q<2, 4, 1>(const FastParams);
-template __global__ void fast::k_render_lean1q<2, 4, 2>(const FastParams);
-template __global__ void fast::k_render_lean1q<1, 16, 0>(const FastParams);
-template __global__ void fast::k_render_lean1q<1, 16, 1>(const FastParams);
-template __global__ void fast::k_render_lean1q<1, 16, 2>(const FastParams);
-template __global__ void fast::k_render_lean1q<2, 16, 0>(const FastParams);
-template __global__ void fast::k_render_lean1q<2, 16, 1>(const FastParams);
-template __global__ void fast::k_render_lean1q<2, 16, 2>(const FastParams);
+template __global__ void fast::k_render_lean1q<1, 4>(const FastParams);
+template __global__ void fast::k_render_lean1q<2, 4>(const FastParams);
+template __global__ void fast::k_render_lean1q<1, 16>(const FastParams);
+template __global__ void fast::k_render_lean1q<2, 16>(const FastParams);
 // general pixels of the same scenes
 template __global__ void fast::k_render_gen1<1>(const FastParams);
 template __global__ void fast::k_render_gen1<2>(const FastParams);
 // both classes of a one-plane launch in one kernel
-template __global__ void fast::k_render_mix1<1, 4, 0>(const FastParams);
-template __global__ void fast::k_render_mix1<1, 4, 1>(const FastParams);
-template __global__ void fast::k_render_mix1<1, 4, 2>(const FastParams);
-template __global__ void fast::k_render_mix1<2, 4, 0>(const FastParams);
-template __global__ void fast::k_render_mix1<2, 4, 1>(const FastParams);
-template __global__ void fast::k_render_mix1<2, 4, 2>(const FastParams);
-template __global__ void fast::k_render_mix1<1, 16, 0>(const FastParams);
-template __global__ void fast::k_render_mix1<1, 16, 1>(const FastParams);
-template __global__ void fast::k_render_mix1<1, 16, 2>(const FastParams);
-template __global__ void fast::k_render_mix1<2, 16, 0>(const FastParams);
-template __global__ void fast::k_render_mix1<2, 16, 1>(const FastParams);
-template __global__ void fast::k_render_mix1<2, 16, 2>(const FastParams);
+template __global__ void fast::k_render_mix1<1, 4>(const FastParams);
+template __global__ void fast::k_render_mix1<2, 4>(const FastParams);
+template __global__ void fast::k_render_mix1<1, 16>(const FastParams);
+template __global__ void fast::k_render_mix1<2, 16>(const FastParams);
 
 }  // namespace rtmi
 
@@ -167,14 +150,12 @@ extern "C" int rtmi_lean1_quads() {
 extern "C" int rtmi_launch_lean1_f32(const rtmi::FastParams* p, int nl, int lp, int blocks, void* stream) {
   if (lp == 4 || lp == 16) {
     using namespace rtmi::fast;
-    const int mode = p->lean_no_occ ? 2 : p->lights_one_side ? 1 : 0;
-#define RTMI_LQ(nl_, lp_, m_) \
-  if (nl == nl_ && lp == lp_ && mode == m_) { \
-    hipLaunchKernelGGL((k_render_lean1q<nl_, lp_, m_>), dim3(blocks), dim3(256), 0, (hipStream_t)stream, *p); \
+#define RTMI_LQ(nl_, lp_) \
+  if (nl == nl_ && lp == lp_) { \
+    hipLaunchKernelGGL((k_render_lean1q<nl_, lp_>), dim3(blocks), dim3(256), 0, (hipStream_t)stream, *p); \
     return (int)hipGetLastError(); \
   }
-    RTMI_LQ(1, 4, 0) RTMI_LQ(1, 4, 1) RTMI_LQ(1, 4, 2) RTMI_LQ(2, 4, 0) RTMI_LQ(2, 4, 1) RTMI_LQ(2, 4, 2)
-    RTMI_LQ(1, 16, 0) RTMI_LQ(1, 16, 1) RTMI_LQ(1, 16, 2) RTMI_LQ(2, 16, 0) RTMI_LQ(2, 16, 1) RTMI_LQ(2, 16, 2)
+    RTMI_LQ(1, 4) RTMI_LQ(2, 4) RTMI_LQ(1, 16) RTMI_LQ(2, 16)
 #undef RTMI_LQ
     return (int)hipErrorInvalidValue;
   }
@@ -187,10 +168,19 @@ extern "C" int rtmi_launch_lean1_f32(const rtmi::FastParams* p, int nl, int lp, 
   return (int)hipGetLastError();
 }
 
-extern "C" int rtmi_lean1_f32_blocks_per_cu(int nl) {
+// Resident blocks per CU of the one-plane lean kernel actually launched:
+// k_render_lean1q<nl, lp> (lp = 4 or 16), k_render_lean1<nl> (lp = 64).
+extern "C" int rtmi_lean1_f32_blocks_per_cu(int nl, int lp) {
+  using namespace rtmi::fast;
   int nb = 0;
-  const hipError_t e = nl == 1 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, rtmi::fast::k_render_lean1<1>, 256, 0)
-                               : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, rtmi::fast::k_render_lean1<2>, 256, 0);
+  hipError_t e = hipErrorInvalidValue;
+#define RTMI_OQ(nl_, lp_) \
+  if (nl == nl_ && lp == lp_) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_render_lean1q<nl_, lp_>, 256, 0);
+  RTMI_OQ(1, 4) RTMI_OQ(2, 4) RTMI_OQ(1, 16) RTMI_OQ(2, 16)
+#undef RTMI_OQ
+  if (lp == 64 && (nl == 1 || nl == 2))
+    e = nl == 1 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_render_lean1<1>, 256, 0)
+                : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_render_lean1<2>, 256, 0);
   return e == hipSuccess && nb > 0 ? nb : 1;
 }
 
@@ -208,23 +198,26 @@ extern "C" int rtmi_launch_gen1_f32(const rtmi::FastParams* p, int nl, int block
 // The one-plane merged kernel (general items, then lean items with lp lanes per pixel).
 extern "C" int rtmi_launch_mix1_f32(const rtmi::FastParams* p, int nl, int lp, int blocks, void* stream) {
   using namespace rtmi::fast;
-  const int mode = p->lean_no_occ ? 2 : p->lights_one_side ? 1 : 0;
-#define RTMI_MX(nl_, lp_, m_) \
-  if (nl == nl_ && lp == lp_ && mode == m_) { \
-    hipLaunchKernelGGL((k_render_mix1<nl_, lp_, m_>), dim3(blocks), dim3(256), 0, (hipStream_t)stream, *p); \
+#define RTMI_MX(nl_, lp_) \
+  if (nl == nl_ && lp == lp_) { \
+    hipLaunchKernelGGL((k_render_mix1<nl_, lp_>), dim3(blocks), dim3(256), 0, (hipStream_t)stream, *p); \
     return (int)hipGetLastError(); \
   }
-  RTMI_MX(1, 4, 0) RTMI_MX(1, 4, 1) RTMI_MX(1, 4, 2) RTMI_MX(2, 4, 0) RTMI_MX(2, 4, 1) RTMI_MX(2, 4, 2)
-  RTMI_MX(1, 16, 0) RTMI_MX(1, 16, 1) RTMI_MX(1, 16, 2) RTMI_MX(2, 16, 0) RTMI_MX(2, 16, 1) RTMI_MX(2, 16, 2)
+  RTMI_MX(1, 4) RTMI_MX(2, 4) RTMI_MX(1, 16) RTMI_MX(2, 16)
 #undef RTMI_MX
   return (int)hipErrorInvalidValue;
 }
 
-extern "C" int rtmi_mix1_f32_blocks_per_cu(int nl) {
+// Resident blocks per CU of k_render_mix1<nl, lp> (each launched
+// instantiation sized from its own register use).
+extern "C" int rtmi_mix1_f32_blocks_per_cu(int nl, int lp) {
+  using namespace rtmi::fast;
   int nb = 0;
-  const hipError_t e = nl == 1
-      ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, rtmi::fast::k_render_mix1<1, 4, 1>, 256, 0)
-      : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, rtmi::fast::k_render_mix1<2, 4, 0>, 256, 0);
+  hipError_t e = hipErrorInvalidValue;
+#define RTMI_OM(nl_, lp_) \
+  if (nl == nl_ && lp == lp_) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_render_mix1<nl_, lp_>, 256, 0);
+  RTMI_OM(1, 4) RTMI_OM(2, 4) RTMI_OM(1, 16) RTMI_OM(2, 16)
+#undef RTMI_OM
   return e == hipSuccess && nb > 0 ? nb : 1;
 }
 

@@ -221,6 +221,17 @@ int rt_render_frame_multi(rt_multi* m, const rt_options* opts, float* fb, int32_
   return RT_OK;
 }
 
+int rt_multi_set_camera(rt_multi* m, const double camera_to_world[16], double fov_deg) {
+  if (!m) return rtmi_fail_msg(RT_E_INVALID, "null argument");
+  std::lock_guard<std::mutex> lk(m->mu);
+  CurrentDevice keep;
+  for (rt_scene* s : m->scene) {
+    const int rc = rt_scene_set_camera(s, camera_to_world, fov_deg);
+    if (rc) return rc;
+  }
+  return RT_OK;
+}
+
 int rt_multi_destroy(rt_multi* m) {
   if (!m) return rtmi_fail_msg(RT_E_INVALID, "null argument");
   {

@@ -26,6 +26,7 @@
 #include "rt_bins.h"
 #include "rt_bvh.h"
 #include "rt_common.h"
+#include "rt_frame.h"
 
 using namespace rtmi;
 
@@ -143,6 +144,9 @@ struct rt_scene {
   // kernel's slots as that kernel's waves drain (no tail between the two)
   hipStream_t aux = nullptr;
   hipEvent_t fork = nullptr, join = nullptr;
+  // RT_FLAG_TIMING: call start, render kernels' start, call end
+  hipEvent_t tev[3] = {nullptr, nullptr, nullptr};
+  bool timed = false;
   int64_t last_lean = 0, last_general = 0;  // rt_scene_last_split
   int32_t last_lean_kind = 0;                // rt_scene_last_lean_kernel
   bool stats_kept = true;                    // the last call reduced its Stats (no RT_FLAG_NO_STATS)
@@ -150,10 +154,6 @@ struct rt_scene {
   int32_t nobj = 0, nlight = 0, nmesh = 0;
   int32_t shadow_mesh = -1;  // the only mesh object, or -1 (FastParams.shadow_mesh)
   int32_t has_point_light = 0;
-  int32_t lights_one_side = 0;  // FastParams.lights_one_side (with the per-call bounds of fill_fast)
-  float max_abs_ty = 0.0f;      // max |world_to_object y translation| over the objects
-  bool lights_all_above = false;  // lights_one_side, every shadow ray going up (-dir.y > 1e-6)
-  float plane_ty = 0.0f;          // the non-mesh object's y translation (two-object scenes)
   unsigned f32_subset = 0;   // SUB_* feature bits of the scene (kernel specialisation)
   bool any_reflective = false;
   double fov = 50.0;
@@ -183,16 +183,6 @@ struct rt_scene {
     }
   };
   std::vector<std::unique_ptr<Order>> orders;  // most recently used first, at most 8
-  struct Split {                   // one launch mapping's lean / general pixel group lists
-    std::array<int64_t, 14> key;
-    DevBuf<int32_t> lean, heavy;
-    int n_lean = 0, n_heavy = 0;
-    ~Split() {
-      lean.release();
-      heavy.release();
-    }
-  };
-  std::vector<std::unique_ptr<Split>> splits;  // most recently used first, at most 8
   // bins of the float32 kernel (rt_bins.h), for the scene's only mesh object
   std::vector<BinTri> bin_tris;    // its faces (object space) + TriFast byte offsets
   double mesh_o2w[16], mesh_w2o[16];
@@ -205,36 +195,29 @@ struct rt_scene {
   std::vector<LightGridHost> grid_host;  // per light: the cell lists + face boxes the shadow lists gather from
   std::vector<SkipPlane> skip_planes;
   bool skippable = false;
-  struct PixelBins {               // camera-ray lists of one image size
+  // camera-dependent data of the float32 kernels (rt_frame.h): rebuilt on
+  // the device by every render call; only the buffers outlive a call
+  DevBuf<DevBinTri> bin_dev;       // the binned mesh's faces (float64, leaf order)
+  double mesh_lo[3] = {0, 0, 0}, mesh_hi[3] = {0, 0, 0};  // its AABB (object space, calcAABB)
+  DevBuf<int32_t> sat_dev;         // the light grids' occupancy prefix sums, back to back
+  int64_t sat_off[8] = {};
+  struct Frame {                   // per-call buffers of one image size
     int w = 0, h = 0;
-    bool ok = false;               // mesh face lists
-    bool obj_ok = false;           // object masks
-    DevBuf<int32_t> off, ent;
+    DevBuf<int32_t> cnt, off, ent, rect, lean, heavy, ctr;
+    DevBuf<double> proj;
+    DevBuf<uint32_t> info;
     DevBuf<unsigned long long> omask;
-    std::vector<int32_t> host_off; // the lists' offsets (the pixel records are built from them)
-    // pixel records (FastParams.pix_info) per shadow bias, most recently
-    // used first (at most 4): callers alternating biases switch buffers
-    // instead of rebuilding and reallocating
-    struct Records {
-      double bias = 0.0;
-      DevBuf<uint32_t> info;
-      std::vector<uint32_t> host;  // the records (two-class launches list lean pixels from them)
-      DevBuf<int32_t> sl, sl_ent;  // per-pixel shadow lists (rt_bins.h), or empty
-      int sl_nl = 0;
-      ~Records() {
-        info.release();
-        sl.release();
-        sl_ent.release();
-      }
-    };
-    std::vector<std::unique_ptr<Records>> records;
-    ~PixelBins() {
-      off.release();
-      ent.release();
-      omask.release();
-      records.clear();
+    DevBuf<unsigned char> scan_tmp;
+    // launch row sets whose list entries `ent` is known to hold for the
+    // current camera (the first call of a row set reads its entry count)
+    std::vector<std::array<int64_t, 9>> sized;
+    bool counted = false;          // the last launch's lean / general lists were counted on the device
+    void release() {
+      cnt.release(); off.release(); ent.release(); rect.release(); lean.release(); heavy.release(); ctr.release();
+      proj.release(); info.release(); omask.release(); scan_tmp.release();
+      sized.clear();
     }
-  };
+  } fr;
   // object bins (rt_bins.h ObjBox), scenes of 4..64 objects
   std::vector<ObjBox> obj_boxes;
   bool objbins = false;
@@ -242,7 +225,7 @@ struct rt_scene {
   DevBuf<unsigned long long> obj_grid_mask;
   unsigned long long obj_off_grid = 0;
   bool has_obj_grids = false;
-  std::vector<std::unique_ptr<PixelBins>> pixel_bins;  // most recently used first, at most 4
+  DevBuf<DevObjBox> objbox_dev;
   DevBuf<float> fb_scratch;
   int max_waves = 0;
   int64_t num_triangles = 0, num_nodes = 0;
@@ -262,10 +245,14 @@ struct rt_scene {
     grid_ent.release();
     obj_grids.release();
     obj_grid_mask.release();
-    pixel_bins.clear();
-    splits.clear();
+    fr.release();
+    bin_dev.release();
+    sat_dev.release();
+    objbox_dev.release();
     if (done) (void)hipEventDestroy(done);
     if (fork) (void)hipEventDestroy(fork);
+    for (hipEvent_t& e : tev)
+      if (e) (void)hipEventDestroy(e);
     if (join) (void)hipEventDestroy(join);
     if (aux) (void)hipStreamDestroy(aux);
     if (stream) (void)hipStreamDestroy(stream);
@@ -733,6 +720,7 @@ extern "C" int rt_scene_create(const rt_scene_desc* d, rt_scene** out_scene) {
   HIP_TRY(hipStreamCreateWithFlags(&s->aux, hipStreamNonBlocking));
   HIP_TRY(hipEventCreateWithFlags(&s->fork, hipEventDisableTiming));
   HIP_TRY(hipEventCreateWithFlags(&s->join, hipEventDisableTiming));
+  for (hipEvent_t& e : s->tev) HIP_TRY(hipEventCreate(&e));
   {
     std::vector<DevObject<float>> o;
     std::vector<DevLight<float>> l;
@@ -745,29 +733,6 @@ extern "C" int rt_scene_create(const rt_scene_desc* d, rt_scene** out_scene) {
     std::vector<FMesh> fm;
     std::vector<FLight> fl;
     fill_fast_records(d, m, fo, fx, fm, fl);
-    {  // rt_fast.h lean1q_loop ONE: the shadow-ray y components (-dir.y) all
-       // of one sign with |.| in (1e-6, 1], or all within 1e-6 of 0; finite
-       // light colours and albedos (an occluded sample's colour is +-0)
-      int up = 0, down = 0, flat = 0;
-      bool ok = true;
-      for (const FLight& L : fl) {
-        const float sy = -L.v[1];
-        if (L.type != LIGHT_DISTANT) continue;
-        if (fabsf(sy) > 1e-6f) (sy > 0.0f ? up : down) += 1;
-        else flat += 1;
-        ok = ok && fabsf(sy) <= 1.0f && std::isfinite(L.ci[0]) && std::isfinite(L.ci[1]) && std::isfinite(L.ci[2]);
-      }
-      float ty = 0.0f;
-      for (size_t i = 0; i < fo.size(); ++i) {
-        ty = std::max(ty, fabsf(fo[i].t[1]));
-        for (int k = 0; k < 3; ++k) ok = ok && std::isfinite(fx[i].albedo_pi[k]);
-      }
-      s->lights_one_side = ok && std::isfinite(ty) && (up == 0 || down == 0) && (flat == 0 || up + down == 0);
-      s->lights_all_above = s->lights_one_side && up > 0 && down == 0 && flat == 0;
-      s->max_abs_ty = ty;
-      // the plane of a mesh + plane scene (FastParams.shadow_mesh's partner)
-      s->plane_ty = fo.size() == 2 ? fo[fo[0].type == RT_MESH ? 1 : 0].t[1] : 0.0f;
-    }
     int rc;
     if ((rc = s->f32.objs.upload(fo)) || (rc = s->f32.objx.upload(fx)) || (rc = s->f32.meshes.upload(fm)) ||
         (rc = s->f32.lights.upload(fl)) || (rc = s->f32.normals.upload(n)))
@@ -847,6 +812,16 @@ extern "C" int rt_scene_create(const rt_scene_desc* d, rt_scene** out_scene) {
     std::memcpy(s->mesh_o2w, ob.object_to_world, sizeof s->mesh_o2w);
     std::memcpy(s->mesh_w2o, ob.world_to_object, sizeof s->mesh_w2o);
     s->binnable = !s->bin_tris.empty();
+    static_assert(sizeof(BinTri) == sizeof(DevBinTri) && offsetof(BinTri, rec) == offsetof(DevBinTri, rec),
+                  "BinTri and DevBinTri share one layout");
+    if (s->binnable) {
+      if ((rc = s->bin_dev.alloc(s->bin_tris.size()))) return rc;
+      HIP_TRY(hipMemcpy(s->bin_dev.p, s->bin_tris.data(), s->bin_tris.size() * sizeof(BinTri), hipMemcpyHostToDevice));
+      for (int k = 0; k < 3; ++k) {
+        s->mesh_lo[k] = aabbs[(size_t)m][k];
+        s->mesh_hi[k] = aabbs[(size_t)m][3 + k];
+      }
+    }
     // light grids of the distant lights
     std::vector<LightGrid> gh((size_t)std::max(1, d->num_lights), LightGrid{});
     s->grid_occ.assign((size_t)d->num_lights, GridOcc{});
@@ -886,6 +861,14 @@ extern "C" int rt_scene_create(const rt_scene_desc* d, rt_scene** out_scene) {
         s->skip_planes.push_back(sp);
       }
       if (!s->skippable) s->skip_planes.clear();
+      // the occupancy prefix sums the per-call shadow skips read (rt_frame.h)
+      std::vector<int32_t> sat;
+      for (int li = 0; li < std::min(8, d->num_lights); ++li) {
+        s->sat_off[li] = (int64_t)sat.size();
+        sat.insert(sat.end(), s->grid_occ[(size_t)li].sat.begin(), s->grid_occ[(size_t)li].sat.end());
+      }
+      if (sat.empty()) sat.push_back(0);
+      if ((rc = s->sat_dev.upload(sat))) return rc;
     }
     mark("light grids");
   }
@@ -917,6 +900,17 @@ extern "C" int rt_scene_create(const rt_scene_desc* d, rt_scene** out_scene) {
         if (!std::isfinite(b.lo[k]) || !std::isfinite(b.hi[k])) b.always = true;
     }
     s->objbins = true;
+    std::vector<DevObjBox> ob((size_t)d->num_objects);
+    for (int i = 0; i < d->num_objects; ++i) {
+      const ObjBox& b = s->obj_boxes[(size_t)i];
+      for (int k = 0; k < 3; ++k) {
+        ob[(size_t)i].lo[k] = b.lo[k];
+        ob[(size_t)i].hi[k] = b.hi[k];
+      }
+      ob[(size_t)i].always = b.always ? 1 : 0;
+      ob[(size_t)i].pad = 0;
+    }
+    if ((rc = s->objbox_dev.upload(ob))) return rc;
     std::vector<LightGrid> gh((size_t)std::max(1, d->num_lights), LightGrid{});
     std::vector<unsigned long long> gm;
     bool any = false;
@@ -975,6 +969,25 @@ extern "C" int rt_scene_get_info(const rt_scene* s, rt_scene_info* out) {
   out->device_bytes = (int64_t)(s->f32.bytes() + s->f64.bytes() + s->nodes.bytes() +
                                 s->partials.bytes() + s->queue.bytes());
   out->build_ms = s->build_ms;
+  return RT_OK;
+}
+
+extern "C" int rt_scene_set_camera(rt_scene* s, const double c2w[16], double fov_deg) {
+  if (!s || !c2w) return fail(RT_E_INVALID, "null argument");
+  for (int k = 0; k < 16; ++k)
+    if (!std::isfinite(c2w[k])) return fail(RT_E_INVALID, "camera_to_world[%d] is not finite", k);
+  if (!(fov_deg > 0.0 && fov_deg < 180.0)) return fail(RT_E_INVALID, "fov %g outside (0, 180)", fov_deg);
+  std::lock_guard<std::mutex> lk(s->mu);
+  const int prev = device_of_current();
+  if (prev != s->device) (void)hipSetDevice(s->device);
+  // earlier calls may still read the launch orders measured for the old camera
+  const hipError_t e = hipEventSynchronize(s->done);
+  std::memcpy(s->c2w, c2w, sizeof s->c2w);
+  s->fov = fov_deg;
+  s->fr.sized.clear();  // list entry counts change with the camera
+  s->orders.clear();    // measured per-group costs (launch order) too
+  if (prev >= 0 && prev != s->device) (void)hipSetDevice(prev);
+  if (e != hipSuccess) return fail(RT_E_DEVICE, "waiting for the scene's earlier calls: %s", hipGetErrorString(e));
   return RT_OK;
 }
 
@@ -1182,73 +1195,190 @@ OrderUse group_order(rt_scene* s, const rt_options* o, const Mapping& mp, const 
   return u;
 }
 
-// Camera-ray lists for one image size (rt_bins.h), built on first use and
-// cached; nullptr when the camera set-up does not allow them (the kernel then
-// traverses the BVH).
-rt_scene::PixelBins* pixel_bins(rt_scene* s, int w, int h) {
-  size_t i = 0;
-  while (i < s->pixel_bins.size() && !(s->pixel_bins[i]->w == w && s->pixel_bins[i]->h == h)) ++i;
-  if (i == s->pixel_bins.size()) {
-    std::unique_ptr<rt_scene::PixelBins> pb(new rt_scene::PixelBins());
-    pb->w = w;
-    pb->h = h;
-    const char* why = "";
-    if (s->binnable) {
-      PixelBinsHost hb;
-      pb->ok = build_pixel_bins(s->bin_tris, s->mesh_o2w, s->mesh_w2o, s->c2w, s->fov, w, h, &hb, &why) &&
-               pb->off.upload(hb.off) == RT_OK && pb->ent.upload(hb.ent) == RT_OK;
-      if (pb->ok) pb->host_off.swap(hb.off);
-    }
-    if (s->objbins) {
-      std::vector<unsigned long long> om;
-      pb->obj_ok = build_object_pixel_masks(s->obj_boxes, s->c2w, s->fov, w, h, &om, &why) &&
-                   pb->omask.upload(om) == RT_OK;
-    }
-    s->pixel_bins.insert(s->pixel_bins.begin(), std::move(pb));
-    if (s->pixel_bins.size() > 4) s->pixel_bins.pop_back();
-    i = 0;
-  }
-  std::rotate(s->pixel_bins.begin(), s->pixel_bins.begin() + (long)i, s->pixel_bins.begin() + (long)i + 1);
-  return s->pixel_bins[0].get();
+// ---- camera-dependent data, rebuilt by every float32 render call (rt_frame.h)
+
+FrameRows frame_rows(const Mapping& mp, int height) {
+  FrameRows r;
+  r.mode = mp.mode;
+  r.y0 = mp.y0;
+  r.nrows = mp.nrows;
+  r.step = mp.step;
+  r.band_h = mp.band_h;
+  r.rank = mp.rank;
+  r.world = mp.world;
+  r.height = height;
+  return r;
 }
 
-// The pixel records of one image size for o->bias (built on first use,
-// cached per bias, LRU of 4); nullptr if they cannot be built.
-const rt_scene::PixelBins::Records* pixel_records(rt_scene* s, rt_scene::PixelBins* pb, const rt_options* o) {
-  auto& rs = pb->records;
-  size_t i = 0;
-  while (i < rs.size() && rs[i]->bias != o->bias) ++i;
-  if (i < rs.size()) {
-    std::rotate(rs.begin(), rs.begin() + (long)i, rs.begin() + (long)i + 1);
-    return rs[0].get();
+// The per-call buffers of one image size (contents are rebuilt by each call).
+int frame_buffers(rt_scene* s, int w, int h, hipStream_t st) {
+  rt_scene::Frame& f = s->fr;
+  if (f.w == w && f.h == h) return RT_OK;
+  HIP_TRY(hipStreamSynchronize(st));  // an earlier call may still read the old buffers
+  HIP_TRY(hipDeviceSynchronize());
+  const size_t npx = (size_t)w * (size_t)h;
+  const size_t nf = s->bin_tris.size();
+  int rc;
+  f.w = f.h = 0;
+  f.sized.clear();
+  if ((rc = f.cnt.alloc(npx + 1)) || (rc = f.off.alloc(npx + 1)) || (rc = f.info.alloc(npx)) ||
+      (rc = f.lean.alloc(npx + 64)) || (rc = f.heavy.alloc(npx)) || (rc = f.ctr.alloc(FC_WORDS)))
+    return rc;
+  if (s->objbins && (rc = f.omask.alloc(npx))) return rc;
+  if (nf > 0 && (f.rect.n < 4 * nf || f.proj.n < 6 * nf)) {
+    if ((rc = f.rect.alloc(4 * nf)) || (rc = f.proj.alloc(6 * nf))) return rc;
   }
-  const size_t npx = (size_t)o->width * (size_t)o->height;
-  std::vector<uint32_t> sk;
-  std::vector<int32_t> sl, sl_ent;
-  const char* why = "";
-  const int sl_nl = std::min(s->nlight, 8);
-  const bool lists = sl_nl > 0 && !std::getenv("RTMI_NO_SHADOW_LISTS");  // diagnostic A/B
-  if (!(s->skippable && build_shadow_skips(pb->host_off, s->skip_planes, s->mesh_w2o, s->grid_occ, s->c2w, s->fov,
-                                           o->width, o->height, o->bias, &sk, &why, lists ? &sl : nullptr,
-                                           lists ? &sl_ent : nullptr, sl_nl))) {
-    sk.assign((npx + 3) / 4, 0u);
-    sl.clear();
+  if (!f.ent.p && (rc = f.ent.alloc(1 << 16))) return rc;
+  // the bin counts are zero between calls (the fill pass counts them down)
+  HIP_TRY(hipMemset(f.cnt.p, 0, f.cnt.bytes()));
+  HIP_TRY(hipMemset(f.ctr.p, 0, f.ctr.bytes()));
+  f.w = w;
+  f.h = h;
+  return RT_OK;
+}
+
+// The mesh's camera-ray lists for the launch's rows (k_frame_bins_count /
+// scan / k_frame_bins_fill). *ok = false: no lists for this camera (a mesh
+// vertex may lie at or behind the camera plane), the kernels traverse the BVH.
+int frame_bins(rt_scene* s, const rt_options* o, const Mapping& mp, hipStream_t st, bool* ok) {
+  *ok = false;
+  if (!s->binnable) return RT_OK;
+  BinsLaunch a;
+  std::memset(&a, 0, sizeof a);
+  if (!pixel_camera(s->mesh_o2w, s->mesh_w2o, s->c2w, s->fov, o->width, o->height, &a.cam)) return RT_OK;
+  // every vertex strictly in front of the camera plane (face_pixel_rect's
+  // test): the test's left side is convex in the point, so the mesh box's
+  // corners bound it
+  for (int c = 0; c < 8; ++c) {
+    const double q[3] = {(c & 1) ? s->mesh_hi[0] : s->mesh_lo[0], (c & 2) ? s->mesh_hi[1] : s->mesh_lo[1],
+                         (c & 4) ? s->mesh_hi[2] : s->mesh_lo[2]};
+    double pw[3], pc[3];
+    bg::xform_point(s->mesh_o2w, q, pw);
+    bg::xform_point(a.cam.w2c, pw, pc);
+    if (!(pc[2] < -1e-9 * (1.0 + std::fabs(pc[0]) + std::fabs(pc[1])))) return RT_OK;
   }
-  std::unique_ptr<rt_scene::PixelBins::Records> r(new rt_scene::PixelBins::Records());
-  r->bias = o->bias;
-  if (!sl.empty() && sl_ent.size() > (size_t)kBinPad) {
-    if (r->sl.upload(sl) != RT_OK || r->sl_ent.upload(sl_ent) != RT_OK) return nullptr;
-    r->sl_nl = sl_nl;
+  int rc = frame_buffers(s, o->width, o->height, st);
+  if (rc) return rc;
+  rt_scene::Frame& f = s->fr;
+  a.tris = s->bin_dev.p;
+  a.nf = (int32_t)s->bin_tris.size();
+  a.rows = frame_rows(mp, o->height);
+  a.rect = f.rect.p;
+  a.proj = f.proj.p;
+  a.cnt = f.cnt.p;
+  a.off = f.off.p;
+  a.ent = f.ent.p;
+  a.cap = (int64_t)f.ent.n;
+  a.ctr = f.ctr.p;
+  a.pad_rec = s->bin_tris[0].rec;
+  const int64_t w = o->width;
+  if (mp.mode == 0) {  // the scan covers the launch's rows only
+    const int64_t last = mp.y0 + (int64_t)(mp.nrows - 1) * mp.step;
+    a.scan_lo = mp.y0 * w;
+    a.scan_n = (last + 1) * w - a.scan_lo + 1;
+  } else {
+    a.scan_lo = 0;
+    a.scan_n = w * o->height + 1;
   }
-  r->host.resize(npx);
-  for (size_t k = 0; k < npx; ++k) {
-    const uint32_t n = (uint32_t)(pb->host_off[k + 1] - pb->host_off[k]);
-    r->host[k] = std::min<uint32_t>(n, kPixCount) | (sk[k >> 2] >> (8 * (k & 3)) & 0xffu) << 24;
+  size_t bytes = 0;
+  if ((rc = rtmi_frame_bins_count(&a, nullptr, &bytes, st)))
+    return fail(RT_E_DEVICE, "bin scan size query failed: %s", hipGetErrorString((hipError_t)rc));
+  if (f.scan_tmp.n < bytes) {
+    HIP_TRY(hipStreamSynchronize(st));
+    if ((rc = f.scan_tmp.alloc(bytes))) return rc;
   }
-  if (r->info.upload(r->host) != RT_OK) return nullptr;
-  rs.insert(rs.begin(), std::move(r));
-  if (rs.size() > 4) rs.pop_back();
-  return rs[0].get();
+  bytes = f.scan_tmp.n;
+  if ((rc = rtmi_frame_bins_count(&a, f.scan_tmp.p, &bytes, st)))
+    return fail(RT_E_DEVICE, "bin count launch failed: %s", hipGetErrorString((hipError_t)rc));
+  // the first call of a row set under this camera reads its entry count and
+  // sizes the entry buffer; later calls of the same set list the same faces
+  const std::array<int64_t, 9> key = {w, o->height, mp.mode, mp.y0, mp.nrows, mp.step, mp.band_h, mp.rank, mp.world};
+  if (std::find(f.sized.begin(), f.sized.end(), key) == f.sized.end()) {
+    int32_t total = 0;
+    HIP_TRY(hipMemcpyAsync(&total, f.off.p + a.scan_lo + a.scan_n - 1, sizeof total, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    if (total < 0) return fail(RT_E_UNSUPPORTED, "more than 2^31 camera-ray list entries");
+    const size_t need = (size_t)total + kBinPad;
+    if (f.ent.n < need) {
+      if ((rc = f.ent.alloc(need + need / 4))) return rc;
+      a.ent = f.ent.p;
+      a.cap = (int64_t)f.ent.n;
+    }
+    f.sized.push_back(key);
+  }
+  if ((rc = rtmi_frame_bins_fill(&a, st)))
+    return fail(RT_E_DEVICE, "bin fill launch failed: %s", hipGetErrorString((hipError_t)rc));
+  *ok = true;
+  return RT_OK;
+}
+
+// Pixel records of the launch's one-pixel groups and, with split, the lean /
+// general lists (k_frame_records).
+int frame_records(rt_scene* s, const rt_options* o, const Mapping& mp, const FastParams& p, bool split,
+                  hipStream_t st) {
+  RecordsLaunch r;
+  std::memset(&r, 0, sizeof r);
+  r.mode = mp.mode;
+  r.y0 = mp.y0;
+  r.nrows = mp.nrows;
+  r.ncols = mp.ncols;
+  r.step = mp.step;
+  r.max_step = mp.max_step;
+  r.band_h = mp.band_h;
+  r.rank = mp.rank;
+  r.world = mp.world;
+  r.width = o->width;
+  r.height = o->height;
+  r.ngroups = p.ngroups;
+  r.order = p.order;
+  r.off = s->fr.off.p;
+  r.info = s->fr.info.p;
+  if (s->skippable && s->skip_planes.size() <= (size_t)kFrameMaxPlanes) {
+    std::vector<bg::SkipPlaneC> pcs;
+    if (skip_camera(s->skip_planes, s->mesh_w2o, s->c2w, s->fov, o->width, o->height, o->bias, &r.cam, &pcs)) {
+      r.nplanes = (int32_t)pcs.size();
+      std::copy(pcs.begin(), pcs.end(), r.planes);
+      r.nl = std::min(8, s->nlight);
+      for (int l = 0; l < r.nl; ++l) r.have |= s->grid_occ[(size_t)l].g.gu > 0 ? 1u << l : 0u;
+      r.grids = s->grids.p;
+      r.sat = s->sat_dev.p;
+      for (int l = 0; l < 8; ++l) r.sat_off[l] = s->sat_off[l];
+    }
+  }
+  r.split = split ? 1 : 0;
+  r.full = s->nlight >= 32 ? ~0u : (1u << s->nlight) - 1u;
+  r.lean = s->fr.lean.p;
+  r.heavy = s->fr.heavy.p;
+  r.ctr = s->fr.ctr.p;
+  const int e = rtmi_frame_records(&r, st);
+  if (e) return fail(RT_E_DEVICE, "pixel record launch failed: %s", hipGetErrorString((hipError_t)e));
+  return RT_OK;
+}
+
+// Object masks of the launch's rows (k_frame_obj_masks).
+int frame_obj_masks(rt_scene* s, const rt_options* o, const Mapping& mp, hipStream_t st, bool* ok) {
+  *ok = false;
+  ObjMaskLaunch a;
+  std::memset(&a, 0, sizeof a);
+  static const double kIdentity[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
+  bg::PixCam pc;
+  if (!pixel_camera(kIdentity, kIdentity, s->c2w, s->fov, o->width, o->height, &pc)) return RT_OK;
+  int rc = frame_buffers(s, o->width, o->height, st);
+  if (rc) return rc;
+  a.objs = s->objbox_dev.p;
+  a.nobj = s->nobj;
+  a.width = o->width;
+  a.height = o->height;
+  std::memcpy(a.w2c, pc.w2c, sizeof a.w2c);
+  a.cam_a = pc.cam_a;
+  a.cam_c = pc.cam_c;
+  a.margin = kPixelMargin;
+  a.rows = frame_rows(mp, o->height);
+  a.masks = s->fr.omask.p;
+  const int e = rtmi_frame_obj_masks(&a, st);
+  if (e) return fail(RT_E_DEVICE, "object mask launch failed: %s", hipGetErrorString((hipError_t)e));
+  *ok = true;
+  return RT_OK;
 }
 
 // Every sample offset of the sampler lies in [0, 1) x [0, 1) of its pixel
@@ -1267,9 +1397,13 @@ bool sampler_in_pixel(int32_t aa_kind) {
   }
 }
 
-void fill_fast(rt_scene* s, const rt_options* o, const Mapping& mp, float* fb, FastParams& p, int* blocks,
-               rt_scene::Order** measuring,
-               const std::vector<int32_t>** host_order) {
+// The float32 launch's parameters, and this call's camera-dependent data
+// built on the device (rt_frame.h) in stream order before the render
+// kernels: the mesh's camera-ray lists (>= 16 samples per pixel), the object
+// masks, and for one-pixel waves the pixel records — with *split, also the
+// lean / general lists of a two-class launch.
+int fill_fast(rt_scene* s, const rt_options* o, const Mapping& mp, float* fb, FastParams& p, int* blocks,
+              rt_scene::Order** measuring, hipStream_t st, bool* split) {
   std::memset(&p, 0, sizeof p);
   p.objs = s->f32.objs.p;
   p.objx = s->f32.objx.p;
@@ -1305,18 +1439,6 @@ void fill_fast(rt_scene* s, const rt_options* o, const Mapping& mp, float* fb, F
     if (m == (1 << k)) p.log2_grid_m = k;
   p.nobj = s->nobj;
   p.nlight = s->nlight;
-  // the lean kernels' one-test occlusion needs |soy + ty| far from overflow
-  // (rt_fast.h lean1q_loop): it is about |cam y + ty| rounding plus the bias
-  p.lights_one_side = s->lights_one_side && std::isfinite(p.bias) && std::isfinite(p.cam[1]) &&
-                      3.0f * (fabsf(p.cam[1]) + s->max_abs_ty) + fabsf(p.bias) < 1e30f;
-  {  // rt_fast.h lean1q_loop MODE 2: the plane's nroy as the kernel forms it,
-     // nonzero and bounded; a bias above the shadow origin's rounding
-    const float nroy = -(p.cam[1] + s->plane_ty);
-    bool cam_ok = true;
-    for (int k = 3; k < 12; ++k) cam_ok = cam_ok && fabsf(p.cam[k]) <= 1e6f;
-    p.lean_no_occ = p.lights_one_side && s->lights_all_above && cam_ok && fabsf(nroy) >= 1e-20f &&
-                    fabsf(nroy) <= 1e30f && p.bias > 1e-6f * (fabsf(p.cam[1]) + 2.0f * fabsf(s->plane_ty));
-  }
   p.has_point_light = s->has_point_light;
   p.seed = o->seed;
   p.width = o->width;
@@ -1364,24 +1486,8 @@ void fill_fast(rt_scene* s, const rt_options* o, const Mapping& mp, float* fb, F
   }
   // binned searches (rt_bins.h): camera rays when a wave spans at most 4
   // pixels (>= 16 samples per pixel), shadow rays to distant lights
-  if (!(o->flags & RT_FLAG_NO_BINNING)) {
-    if ((s->binnable || s->objbins) && pl.L >= 16 && sampler_in_pixel(o->aa_kind)) {
-      rt_scene::PixelBins* pb = pixel_bins(s, o->width, o->height);
-      if (pb->ok) {
-        p.pix_off = pb->off.p;
-        p.pix_ent = pb->ent.p;
-      }
-      // one-pixel waves: the pixel records (list length + shadow skips for
-      // this bias, rt_bins.h), one set per bias (cached)
-      const rt_scene::PixelBins::Records* rec = (pb->ok && pl.L == 64) ? pixel_records(s, pb, o) : nullptr;
-      if (rec) p.pix_info = rec->info.p;
-      if (rec && rec->sl_nl > 0) {
-        p.pix_sl = rec->sl.p;
-        p.pix_sl_ent = rec->sl_ent.p;
-        p.pix_sl_nl = rec->sl_nl;
-      }
-      if (pb->obj_ok) p.obj_pix = pb->omask.p;
-    }
+  const bool binning = !(o->flags & RT_FLAG_NO_BINNING);
+  if (binning) {
     if (s->has_grids) {
       p.grids = s->grids.p;
       p.grid_off = s->grid_off.p;
@@ -1403,8 +1509,33 @@ void fill_fast(rt_scene* s, const rt_options* o, const Mapping& mp, float* fb, F
   p.order = ou.order;
   p.cost = ou.cost;
   *measuring = ou.entry;
-  *host_order = ou.host_order;
   *blocks = pl.blocks;
+  *split = false;
+  if (!binning || pl.L < 16 || !sampler_in_pixel(o->aa_kind)) return RT_OK;
+  // this call's camera-dependent data (nothing of it is kept from earlier calls)
+  int rc;
+  bool lists = false, masks = false;
+  if ((rc = frame_bins(s, o, mp, st, &lists))) return rc;
+  if (lists) {
+    p.pix_off = s->fr.off.p;
+    p.pix_ent = s->fr.ent.p;
+  }
+  if (s->objbins) {
+    if ((rc = frame_obj_masks(s, o, mp, st, &masks))) return rc;
+    if (masks) p.obj_pix = s->fr.omask.p;
+  }
+  if (!lists || pl.L != 64) return RT_OK;
+  // two-class launch (one pixel per wave): the lean pixels — no camera ray
+  // can hit the mesh, every light a distant light whose shadow rays from the
+  // pixel provably miss it, no reflection — get a kernel of their own; not
+  // for the measuring launch of a launch order or instrumented launches
+  static const char* cost_dump = std::getenv("RTMI_COST_DUMP");
+  const unsigned sub = f32_subset(s, o);
+  *split = !(o->flags & (RT_FLAG_NO_SPLIT | RT_FLAG_COUNT_TRAVERSAL)) && !p.cost && !cost_dump && s->nlight <= 8 &&
+           rtmi_lean_f32_blocks_per_cu(sub, f32_table_lds(o)) > 0;
+  if ((rc = frame_records(s, o, mp, p, *split, st))) return rc;
+  p.pix_info = s->fr.info.p;
+  return RT_OK;
 }
 
 template <class R>
@@ -1485,79 +1616,6 @@ void fill_params(rt_scene* s, const PrecisionData<R>& pd, const rt_options* o, c
   *blocks = (int)std::max(1LL, std::min<long long>(want, cap));
 }
 
-// Two-class launches (float32, one pixel per wave, pixel records present):
-// the launch's pixel groups split into the lean ones — no camera ray of the
-// pixel can hit the mesh and every light is a distant light whose shadow
-// rays from the pixel provably miss it (rt_bins.h pixel records), no
-// reflection — and the rest. The general kernel renders the rest from one
-// list, k_render_lean (rt_fast.h) the lean ones from the other: the lean
-// path's register allocation is then its own (C3: ~90 % of the pixels).
-// Groups outside the image / skipped by a progressive pass are in neither
-// list (they render nothing). Lists are built per launch mapping on the
-// host from the records and cached (LRU, 8). Scheduling only: the image
-// and Stats are those of the one-kernel launch.
-rt_scene::Split* split_lists(rt_scene* s, const rt_options* o, const Mapping& mp, const FastParams& p,
-                             const std::vector<int32_t>* host_order) {
-  if (o->flags & (RT_FLAG_NO_SPLIT | RT_FLAG_COUNT_TRAVERSAL)) return nullptr;
-  // a short launch with a longest-first order (group_order: a multi-GPU
-  // rank's band set) keeps that order within each list (C3 in 8 bands,
-  // rank time: one kernel in LPT order 0.316 ms)
-  if (p.lanes_per_px != 64 || !p.pix_info || p.cost || s->nlight > 8) return nullptr;
-  if (p.order && (!host_order || (long long)host_order->size() != (long long)p.ngroups)) return nullptr;
-  const unsigned sub = f32_subset(s, o);
-  if (rtmi_lean_f32_blocks_per_cu(sub, f32_table_lds(o)) <= 0) return nullptr;
-  rt_scene::PixelBins* pb = s->pixel_bins.empty() ? nullptr : s->pixel_bins[0].get();
-  if (!pb || pb->w != o->width || pb->h != o->height || pb->records.empty() || pb->records[0]->bias != o->bias ||
-      pb->records[0]->info.p != p.pix_info)
-    return nullptr;
-  const std::vector<uint32_t>& host_info = pb->records[0]->host;
-  int64_t bias_bits;
-  std::memcpy(&bias_bits, &o->bias, sizeof bias_bits);
-  const std::array<int64_t, 14> key = {o->width,   o->height,  bias_bits, mp.mode,  mp.y0,    mp.nrows, mp.ncols,
-                                       mp.step,    mp.max_step, mp.band_h, mp.rank, mp.world, s->nlight,
-                                       p.order ? 1 : 0};
-  size_t i = 0;
-  while (i < s->splits.size() && s->splits[i]->key != key) ++i;
-  if (i < s->splits.size()) {
-    std::rotate(s->splits.begin(), s->splits.begin() + (long)i, s->splits.begin() + (long)i + 1);
-    return s->splits[0].get();
-  }
-  const uint32_t full = (1u << s->nlight) - 1u;
-  std::vector<int32_t> lean, heavy;
-  for (int64_t gi = 0; gi < (int64_t)p.ngroups; ++gi) {  // group_pixel (rt_fast.h) for one-pixel groups
-    const int64_t g = p.order ? (int64_t)(*host_order)[(size_t)gi] : gi;
-    const int k = (int)(g / mp.ncols), j = (int)(g % mp.ncols);
-    const int x = j * mp.step;
-    int y;
-    if (mp.mode == 0) {
-      y = mp.y0 + k * mp.step;
-    } else {
-      y = (k / mp.band_h * mp.world + mp.rank) * mp.band_h + k % mp.band_h;
-      if (y >= o->height) continue;
-    }
-    if (mp.step < mp.max_step) {
-      const int mask = mp.step * 2 - 1;
-      if ((x & mask) == 0 && (y & mask) == 0) continue;
-    }
-    const uint32_t r = host_info[(size_t)y * o->width + x];
-    const bool is_lean = (r & kPixCount) == 0u && ((r >> 24) & full) == full;
-    (is_lean ? lean : heavy).push_back((int32_t)g);
-  }
-  std::unique_ptr<rt_scene::Split> e(new rt_scene::Split());
-  e->key = key;
-  e->n_lean = (int)lean.size();
-  e->n_heavy = (int)heavy.size();
-  // k_render_lean takes runs of kLeanRun entries, k_render_lean1q items of
-  // 16: padded with -1 to a multiple of 64
-  while (lean.size() % 64) lean.push_back(-1);
-  if (lean.empty()) lean.assign(64, -1);  // keep both allocations non-empty
-  if (heavy.empty()) heavy.push_back(0);
-  if (e->lean.upload(lean) != RT_OK || e->heavy.upload(heavy) != RT_OK) return nullptr;
-  s->splits.insert(s->splits.begin(), std::move(e));
-  if (s->splits.size() > 8) s->splits.pop_back();
-  return s->splits[0].get();
-}
-
 // k_render_lean1 (rt_fast.h) renders the lean pixels when the scene's only
 // analytic object is one plane and every transform a translation (the
 // mesh + plane feature subset, nothing else), with one or two distant lights,
@@ -1568,13 +1626,9 @@ rt_scene::Split* split_lists(rt_scene* s, const rt_options* o, const Mapping& mp
 // Whether a one-plane two-class launch runs as one merged kernel
 // (k_render_mix1). RTMI_MIX=0/1 forces it (diagnostic A/B); by default:
 // always.
-bool mix_policy(long long n_heavy, long long lean_items, const rt_scene* s) {
+bool mix_policy() {
   static const int force = std::getenv("RTMI_MIX") ? std::atoi(std::getenv("RTMI_MIX")) : -1;
-  (void)n_heavy;
-  (void)lean_items;
-  (void)s;
-  if (force >= 0) return force != 0;
-  return true;
+  return force != 0;
 }
 
 bool lean1_ok(const rt_scene* s, const rt_options* o, const FastParams& p, unsigned sub) {
@@ -1589,6 +1643,7 @@ int launch(rt_scene* s, const rt_options* o, const Mapping& mp, float* d_out, hi
   if (o->precision == RT_FP64) {
     RenderParams<double> p;
     fill_params<double>(s, s->f64, o, mp, d_out, p, &blocks);
+    if (o->flags & RT_FLAG_TIMING) HIP_TRY(hipEventRecord(s->tev[1], st));
     if (p.ngroups == 0) return RT_OK;
     if (p.aa_kind >= RT_AA_JITTERED) {
       const size_t need = (size_t)blocks * 256 * 2 * (size_t)p.spp;
@@ -1608,8 +1663,11 @@ int launch(rt_scene* s, const rt_options* o, const Mapping& mp, float* d_out, hi
   } else {
     FastParams p;
     rt_scene::Order* measuring = nullptr;
-    const std::vector<int32_t>* host_order = nullptr;
-    fill_fast(s, o, mp, d_out, p, &blocks, &measuring, &host_order);
+    bool split = false;
+    if (mp.nrows == 0 || mp.ncols == 0) return RT_OK;
+    int rc = fill_fast(s, o, mp, d_out, p, &blocks, &measuring, st, &split);
+    if (rc) return rc;
+    if (o->flags & RT_FLAG_TIMING) HIP_TRY(hipEventRecord(s->tev[1], st));
     if (p.ngroups == 0) return RT_OK;
     // diagnostic (tools/cost_map.py): RTMI_COST_DUMP=<file> records every
     // pixel group's duration (s_memtime cycles) of this launch into <file>
@@ -1618,8 +1676,13 @@ int launch(rt_scene* s, const rt_options* o, const Mapping& mp, float* d_out, hi
     if (cost_dump && !measuring && !p.cost) {
       if (dbg_cost.alloc((size_t)p.ngroups) == RT_OK) p.cost = dbg_cost.p;
     }
-    rt_scene::Split* sp = (cost_dump || measuring) ? nullptr : split_lists(s, o, mp, p, host_order);
-    if (sp) {  // two-class launch: the general kernel on its list, then the lean kernel on its own
+    s->fr.counted = split;
+    if (split) {  // two-class launch: the general kernel on its list, then the lean kernel on its own
+      // the lists and their entry counts come from this call's k_frame_records
+      // (the host never reads them: grids and items are sized for the launch's
+      // groups, the kernels stop at the device counts)
+      int32_t* const n_heavy = s->fr.ctr.p + FC_HEAVY;
+      int32_t* const n_lean = s->fr.ctr.p + FC_LEAN;
       const size_t shmem = f32_table_lds(o);
       const unsigned sub = f32_subset(s, o);
       FastParams ph = p, pl = p;
@@ -1640,51 +1703,53 @@ int launch(rt_scene* s, const rt_options* o, const Mapping& mp, float* d_out, hi
       static const int gen_cap = std::getenv("RTMI_GEN_WAVES_CAP") ? std::atoi(std::getenv("RTMI_GEN_WAVES_CAP")) : 0;
       static const int lean_cap = std::getenv("RTMI_LEAN_WAVES_CAP") ? std::atoi(std::getenv("RTMI_LEAN_WAVES_CAP")) : 0;
       const long long hcap2 = gen_cap > 0 ? std::min<long long>(hcap, (long long)gen_cap * s->num_cus) : hcap;
-      const int hb = (int)std::max(1LL, std::min<long long>(hcap2, ((long long)sp->n_heavy + 3) / 4));
-      ph.order = sp->heavy.p;
-      ph.ngroups = sp->n_heavy;
+      const int hb = (int)std::max(1LL, std::min<long long>(hcap2, ((long long)p.ngroups + 3) / 4));
+      ph.order = s->fr.heavy.p;
+      ph.ngroups = p.ngroups;
+      ph.list_n = n_heavy;
       ph.shards = std::min(kQueueShards, hb);
       const bool lean1 = one_plane && !(o->flags & RT_FLAG_NO_LEAN1);
-      const long long lcap =
-          (long long)(lean1 ? rtmi_lean1_f32_blocks_per_cu(p.nlight) : rtmi_lean_f32_blocks_per_cu(sub, shmem)) *
-          s->num_cus;
       // work items: runs of kLeanRun pixels (k_render_lean, k_render_lean1),
       // 64 / lp pixels (k_render_lean1q, lp lanes per pixel): 16 per item
-      // unless that leaves fewer than 8 items per resident wave (a short
-      // launch, e.g. a multi-GPU rank's bands), then 4
-      const long long lwaves = 4LL * std::min<long long>(lcap, s->max_waves / 4);
-      const int lp = !(lean1 && rtmi_lean1_quads()) ? 64 : ((long long)(sp->n_lean + 15) / 16 >= 8 * lwaves ? 4 : 16);
+      // unless the launch's groups make fewer than 8 items per resident wave
+      // (a short launch, e.g. a multi-GPU rank's bands), then 4
+      const long long lwaves4 =
+          4LL * std::min<long long>((long long)rtmi_lean1_f32_blocks_per_cu(p.nlight, 4) * s->num_cus, s->max_waves / 4);
+      const int lp = !(lean1 && rtmi_lean1_quads()) ? 64 : ((long long)(p.ngroups + 15) / 16 >= 8 * lwaves4 ? 4 : 16);
+      const long long lcap =
+          (long long)(lean1 ? rtmi_lean1_f32_blocks_per_cu(p.nlight, lp) : rtmi_lean_f32_blocks_per_cu(sub, shmem)) *
+          s->num_cus;
       const int lrun = lp == 64 ? kLeanRun : 64 / lp;
-      const int lruns = (sp->n_lean + lrun - 1) / lrun;
+      const int lruns = (p.ngroups + lrun - 1) / lrun;  // at most: the kernels stop at the device count
       const long long lcap2 = lean_cap > 0 ? std::min<long long>(lcap, (long long)lean_cap * s->num_cus) : lcap;
       const int lb = (int)std::max(1LL, std::min<long long>(std::min<long long>(lcap2, s->max_waves / 4),
                                                             ((long long)lruns + 3) / 4));
-      pl.order = sp->lean.p;
+      pl.order = s->fr.lean.p;
       pl.ngroups = lruns;
+      pl.list_n = n_lean;
       pl.stat_flush = std::max(1, p.stat_flush / lrun);
       pl.shards = std::min(kQueueShards, lb);
       pl.queue = s->queue.p + (size_t)kQueueShards * kQueueStride;
       pl.partials = s->partials.p + (size_t)hb * 4 * kStatSlots;
       // one-plane launches: both lists in one kernel (k_render_mix1: the
       // general items first, then the lean ones) — one ramp and one tail
-      const bool mix = gen1 && lean1 && lp != 64 && !(o->flags & RT_FLAG_NO_MIX) && mix_policy(sp->n_heavy, lruns, s);
+      const bool mix = gen1 && lean1 && lp != 64 && !(o->flags & RT_FLAG_NO_MIX) && mix_policy();
       if (mix) {
         FastParams pm = ph;
         pm.order2 = pl.order;
         pm.ngroups2 = pl.ngroups;
+        pm.list_n2 = n_lean;
         pm.stat_flush = std::min(ph.stat_flush, pl.stat_flush);
-        const long long mcap = (long long)rtmi_mix1_f32_blocks_per_cu(p.nlight) * s->num_cus;
+        const long long mcap = (long long)rtmi_mix1_f32_blocks_per_cu(p.nlight, lp) * s->num_cus;
         const int mb = (int)std::max(1LL, std::min<long long>(std::min<long long>(mcap, blocks),
-                                                              ((long long)sp->n_heavy + lruns + 3) / 4));
+                                                              ((long long)p.ngroups + lruns + 3) / 4));
         pm.shards = std::min(kQueueShards, mb);
         pm.shards2 = pm.shards;
         const int e = rtmi_launch_mix1_f32(&pm, p.nlight, lp, mb, st);
         if (e) return fail(RT_E_DEVICE, "render kernel launch failed: %s", hipGetErrorString((hipError_t)e));
         blocks = mb;
-        s->last_lean = sp->n_lean;
-        s->last_lean_kind = 3 | (3 << 2);
-        s->last_general = sp->n_heavy;
-        s->last_batched = sp->n_heavy;
+        s->last_lean_kind = 3 | (3 << 2) | (lp << 8);
+        s->last_batched = -1;  // = the general list (device count)
         goto launched;
       }
       // general kernel first on the caller's stream, the lean kernel on
@@ -1712,10 +1777,8 @@ int launch(rt_scene* s, const rt_options* o, const Mapping& mp, float* d_out, hi
         HIP_TRY(hipStreamWaitEvent(st, s->join, 0));
       }
       blocks = hb + lb;
-      s->last_lean = sp->n_lean;
-      s->last_lean_kind = (lean1 ? 2 : 1) | ((gen1 ? 2 : gen ? 1 : 0) << 2);
-      s->last_general = sp->n_heavy;
-      s->last_batched = gen ? sp->n_heavy : 0;
+      s->last_lean_kind = (lean1 ? 2 : 1) | ((gen1 ? 2 : gen ? 1 : 0) << 2) | (lp << 8);
+      s->last_batched = gen ? -1 : 0;
     } else {
       s->last_lean = 0;
       s->last_lean_kind = 0;
@@ -1784,12 +1847,18 @@ int render_device(rt_scene* s, const rt_options* o, const Mapping& mp, float* d_
   const bool reduce = need_stats || out || !(o->flags & RT_FLAG_NO_STATS) || (o->flags & RT_FLAG_COUNT_TRAVERSAL);
   s->stats_kept = reduce;
   HIP_TRY(hipStreamWaitEvent(st, s->done, 0));
+  s->timed = (o->flags & RT_FLAG_TIMING) != 0;
+  if (s->timed) {  // (tev[1] again before the render kernels; here for launches with nothing to render)
+    HIP_TRY(hipEventRecord(s->tev[0], st));
+    HIP_TRY(hipEventRecord(s->tev[1], st));
+  }
   // one fill: the queue heads (float32) and / or the Stats accumulator behind them
   const size_t q0 = o->precision == RT_FP32 ? 0 : rt_scene::kQueueWords;
   const size_t q1 = rt_scene::kQueueWords + (reduce ? 2 * (size_t)kStatSlots : 0);
   if (q1 > q0) HIP_TRY(hipMemsetAsync(s->queue.p + q0, 0, (q1 - q0) * sizeof(unsigned int), st));
   int rc = launch(s, o, mp, d_out, st, reduce);
   if (rc) return rc;
+  if (s->timed) HIP_TRY(hipEventRecord(s->tev[2], st));
   HIP_TRY(hipEventRecord(s->done, st));
   if (out) return read_stats(s, st, out);
   return RT_OK;
@@ -1889,6 +1958,20 @@ extern "C" int rt_scene_last_stats(rt_scene* s, rt_stats* out) {
   return read_stats(s, s->stream, out);
 }
 
+extern "C" int rt_scene_last_timing(rt_scene* s, double* setup_ms, double* render_ms) {
+  if (!s || !setup_ms || !render_ms) return fail(RT_E_INVALID, "null argument");
+  std::lock_guard<std::mutex> lk(s->mu);
+  if (!s->timed) return fail(RT_E_INVALID, "the last render call did not set RT_FLAG_TIMING");
+  DeviceGuard g(s->device);
+  float a = 0.0f, b = 0.0f;
+  HIP_TRY(hipEventSynchronize(s->tev[2]));
+  HIP_TRY(hipEventElapsedTime(&a, s->tev[0], s->tev[1]));
+  HIP_TRY(hipEventElapsedTime(&b, s->tev[1], s->tev[2]));
+  *setup_ms = a;
+  *render_ms = b;
+  return RT_OK;
+}
+
 extern "C" int rt_unshard_bands_device(const float* d_gathered, float* d_fb, int32_t width, int32_t height,
                                        int32_t band_h, int32_t world, void* stream) {
   if (!d_gathered || !d_fb || width <= 0 || height <= 0 || band_h <= 0 || world <= 0)
@@ -1931,12 +2014,31 @@ extern "C" int rt_rgba_encode_device(const float* d_fb, int32_t width, int32_t h
   return RT_OK;
 }
 
+namespace {
+// The last launch's lean / general list lengths: counted on the device by
+// its k_frame_records (read back here, after the call completed), or the
+// host's (a one-kernel launch: every group general).
+int last_lists(rt_scene* s, int64_t* lean, int64_t* general) {
+  if (!s->fr.counted) {
+    *lean = s->last_lean;
+    *general = s->last_general;
+    return RT_OK;
+  }
+  DeviceGuard g(s->device);
+  int32_t c[FC_WORDS];
+  HIP_TRY(hipEventSynchronize(s->done));
+  HIP_TRY(hipMemcpy(c, s->fr.ctr.p, sizeof c, hipMemcpyDeviceToHost));
+  if (c[FC_OVERFLOW]) return fail(RT_E_DEVICE, "camera-ray list entries overflowed their buffer");
+  *lean = c[FC_LEAN];
+  *general = c[FC_HEAVY];
+  return RT_OK;
+}
+}  // namespace
+
 extern "C" int rt_scene_last_split(rt_scene* s, int64_t* lean_groups, int64_t* general_groups) {
   if (!s || !lean_groups || !general_groups) return fail(RT_E_INVALID, "null argument");
   std::lock_guard<std::mutex> lk(s->mu);
-  *lean_groups = s->last_lean;
-  *general_groups = s->last_general;
-  return RT_OK;
+  return last_lists(s, lean_groups, general_groups);
 }
 
 extern "C" int rt_scene_last_lean_kernel(rt_scene* s, int32_t* kind) {
@@ -1950,6 +2052,11 @@ extern "C" int rt_scene_last_batch(rt_scene* s, int64_t* batched_groups, int64_t
   if (!s || !batched_groups || !fallback_groups) return fail(RT_E_INVALID, "null argument");
   std::lock_guard<std::mutex> lk(s->mu);
   *batched_groups = s->last_batched;
+  if (s->last_batched < 0) {  // the general list of a two-class launch, counted on the device
+    int64_t lean = 0;
+    const int rc = last_lists(s, &lean, batched_groups);
+    if (rc) return rc;
+  }
   *fallback_groups = s->last_fallback;
   return RT_OK;
 }
@@ -1957,6 +2064,9 @@ extern "C" int rt_scene_last_batch(rt_scene* s, int64_t* batched_groups, int64_t
 extern "C" int rt_scene_last_counters(rt_scene* s, rt_traversal_counters* out) {
   if (!s || !out) return fail(RT_E_INVALID, "null argument");
   std::lock_guard<std::mutex> lk(s->mu);
+  // a call without Stats (RT_FLAG_NO_STATS) reduced nothing: its counters
+  // are not in the accumulator
+  if (!s->stats_kept) return fail(RT_E_INVALID, "the last render call set RT_FLAG_NO_STATS");
   DeviceGuard g(s->device);
   unsigned long long h[kStatSlots];
   HIP_TRY(hipEventSynchronize(s->done));
@@ -1966,4 +2076,56 @@ extern "C" int rt_scene_last_counters(rt_scene* s, rt_traversal_counters* out) {
   out->lane_node_visits = h[STAT_LANE_NODES];
   out->lane_tri_tests = h[STAT_LANE_TRIS];
   return RT_OK;
+}
+
+// ---- test hooks (tests/test_gpu_frame.py; not part of include/rtmi.h) ----
+
+// The last render call's device-built camera-ray lists and pixel records
+// (image-sized arrays; only the call's pixels are defined). off: w*h + 1,
+// info: w*h, ent: up to ent_cap entries. Returns the entry capacity copied,
+// or a negative RT_E_* code.
+extern "C" int64_t rtmi_test_frame_lists(rt_scene* s, int32_t* off, int32_t* ent, int64_t ent_cap, uint32_t* info) {
+  if (!s || !off || !ent || !info) return fail(RT_E_INVALID, "null argument");
+  std::lock_guard<std::mutex> lk(s->mu);
+  DeviceGuard g(s->device);
+  const rt_scene::Frame& f = s->fr;
+  if (!f.off.p || f.w == 0) return fail(RT_E_INVALID, "no per-call lists yet");
+  const size_t npx = (size_t)f.w * (size_t)f.h;
+  HIP_TRY(hipEventSynchronize(s->done));
+  HIP_TRY(hipMemcpy(off, f.off.p, (npx + 1) * sizeof(int32_t), hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(info, f.info.p, npx * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  const size_t n = std::min<size_t>(f.ent.n, (size_t)std::max<int64_t>(0, ent_cap));
+  HIP_TRY(hipMemcpy(ent, f.ent.p, n * sizeof(int32_t), hipMemcpyDeviceToHost));
+  int32_t c[FC_WORDS];
+  HIP_TRY(hipMemcpy(c, f.ctr.p, sizeof c, hipMemcpyDeviceToHost));
+  if (c[FC_OVERFLOW]) return fail(RT_E_DEVICE, "camera-ray list entries overflowed their buffer");
+  return (int64_t)n;
+}
+
+// The host builders (rt_bins.cpp build_pixel_bins + build_shadow_skips) on
+// this scene's faces, camera and light grids: the lists and records a render
+// call of this image size and bias must build on the device. off: w*h + 1,
+// info: w*h. Returns the number of entries (those past ent_cap not copied),
+// -1 when the host builder declines the camera.
+extern "C" int64_t rtmi_test_host_lists(rt_scene* s, int32_t w, int32_t h, double bias, int32_t* off, int32_t* ent,
+                                        int64_t ent_cap, uint32_t* info) {
+  if (!s || !off || !ent || !info || w <= 0 || h <= 0) return fail(RT_E_INVALID, "bad argument");
+  std::lock_guard<std::mutex> lk(s->mu);
+  if (!s->binnable) return -1;
+  PixelBinsHost hb;
+  const char* why = "";
+  if (!build_pixel_bins(s->bin_tris, s->mesh_o2w, s->mesh_w2o, s->c2w, s->fov, w, h, &hb, &why)) return -1;
+  const size_t npx = (size_t)w * (size_t)h;
+  std::vector<uint32_t> sk;
+  if (!(s->skippable && build_shadow_skips(hb.off, s->skip_planes, s->mesh_w2o, s->grid_occ, s->c2w, s->fov, w, h,
+                                           bias, &sk, &why)))
+    sk.assign((npx + 3) / 4, 0u);
+  std::copy(hb.off.begin(), hb.off.end(), off);
+  const int64_t total = hb.off.back();
+  std::copy(hb.ent.begin(), hb.ent.begin() + std::min<int64_t>(total, std::max<int64_t>(0, ent_cap)), ent);
+  for (size_t k = 0; k < npx; ++k) {
+    const uint32_t n = (uint32_t)(hb.off[k + 1] - hb.off[k]);
+    info[k] = std::min<uint32_t>(n, kPixCount) | (sk[k >> 2] >> (8 * (k & 3)) & 0xffu) << 24;
+  }
+  return total;
 }

@@ -29,6 +29,7 @@ RT_FLAG_NO_LEAN1 = 0x80
 RT_FLAG_NO_GEN1 = 0x100
 RT_FLAG_NO_STATS = 0x200
 RT_FLAG_NO_MIX = 0x400
+RT_FLAG_TIMING = 0x800
 RT_BVH_SAH = 0
 RT_OBJ_SLASH_INDICES = 0x1
 RT_BVH_PLOC = 1
@@ -166,6 +167,7 @@ SIGNATURES = {
     "rt_scene_create": (C.c_int, [C.POINTER(rt_scene_desc), C.POINTER(_P)]),
     "rt_scene_destroy": (C.c_int, [_P]),
     "rt_scene_get_info": (C.c_int, [_P, C.POINTER(rt_scene_info)]),
+    "rt_scene_set_camera": (C.c_int, [_P, C.POINTER(C.c_double), C.c_double]),
     "rt_render_lines": (C.c_int, [_P, C.POINTER(rt_options), C.POINTER(C.c_float), C.c_int32,
                                   C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
                                   C.POINTER(rt_stats)]),
@@ -189,11 +191,13 @@ SIGNATURES = {
                               C.POINTER(C.c_int64), C.POINTER(C.c_int32)]),
     "rt_write_geom": (C.c_int, [C.c_char_p, C.POINTER(C.c_double), C.c_int64, C.POINTER(C.c_int32), C.c_int64]),
     "rt_scene_last_stats": (C.c_int, [_P, C.POINTER(rt_stats)]),
+    "rt_scene_last_timing": (C.c_int, [_P, C.POINTER(C.c_double), C.POINTER(C.c_double)]),
     "rt_multi_create": (C.c_int, [C.POINTER(rt_scene_desc), C.POINTER(C.c_int32), C.c_int32, C.c_int32,
                                   C.POINTER(_P)]),
     "rt_render_frame_multi_device": (C.c_int, [_P, C.POINTER(rt_options), _P, C.POINTER(rt_stats)]),
     "rt_render_frame_multi": (C.c_int, [_P, C.POINTER(rt_options), C.POINTER(C.c_float), C.c_int32, C.c_int32,
                                         C.POINTER(rt_stats)]),
+    "rt_multi_set_camera": (C.c_int, [_P, C.POINTER(C.c_double), C.c_double]),
     "rt_multi_destroy": (C.c_int, [_P]),
     "rt_queue_create": (C.c_int, [_P, C.POINTER(_P)]),
     "rt_queue_start": (C.c_int, [_P]),

@@ -12,7 +12,7 @@ import ctypes as C
 
 import numpy as np
 
-from . import abi
+from . import abi, glm
 from ._lib import RtmiError, check, lib
 from .scene import Options, Scene, Stats, flatten
 
@@ -56,6 +56,15 @@ class DeviceScene:
         i = abi.rt_scene_info()
         check(lib().rt_scene_get_info(self.h, C.byref(i)))
         return i.as_dict()
+
+    def set_camera(self, cameraToWorld=None, fov=None):
+        """Scene.cameraToWorld / Scene.fov for the next render calls
+        (renderLine re-reads them every call, renderer.nim:135-136,150-153);
+        None: this DeviceScene's Scene's current values."""
+        m = self.scene.cameraToWorld if cameraToWorld is None else cameraToWorld
+        f = self.scene.fov if fov is None else fov
+        arr = (C.c_double * 16)(*[float(x) for x in glm.flat(m)])
+        check(lib().rt_scene_set_camera(self.h, arr, float(f)))
 
     # -- host framebuffer (the pool-compatible path) ----------------------
     def render_lines(self, opts: Options, fb, y0, y1, step=1, maxStep=1) -> Stats:
@@ -103,11 +112,19 @@ class DeviceScene:
 
     def last_lean_kernel(self):
         """Kernels of the last call's two classes: bits 0-1 the lean pixels'
-        (0 none, 1 k_render_lean, 2 k_render_lean1), bits 2-3 the general
-        pixels' (0 k_render_fast, 1 k_render_gen, 2 k_render_gen1)."""
+        (0 none, 1 k_render_lean, 2 k_render_lean1, 3 merged), bits 2-3 the
+        general pixels' (0 k_render_fast, 1 k_render_gen, 2 k_render_gen1,
+        3 merged: k_render_mix1)."""
         k = C.c_int32()
         check(lib().rt_scene_last_lean_kernel(self.h, C.byref(k)))
-        return int(k.value)
+        return int(k.value) & 15
+
+    def last_lean_lanes(self):
+        """Lanes per lean pixel of the last two-class call (4 or 16:
+        k_render_lean1q / k_render_mix1; 64: one pixel per wave), 0 if none."""
+        k = C.c_int32()
+        check(lib().rt_scene_last_lean_kernel(self.h, C.byref(k)))
+        return int(k.value) >> 8
 
     def last_batch(self):
         """(batched, fallback) general pixel groups of the last render call:
@@ -116,6 +133,13 @@ class DeviceScene:
         a, b = C.c_int64(), C.c_int64()
         check(lib().rt_scene_last_batch(self.h, C.byref(a), C.byref(b)))
         return int(a.value), int(b.value)
+
+    def last_timing(self):
+        """(setup_ms, render_ms) of the last call made with RT_FLAG_TIMING:
+        its per-call camera-dependent build and its render kernels (waits)."""
+        a, b = C.c_double(), C.c_double()
+        check(lib().rt_scene_last_timing(self.h, C.byref(a), C.byref(b)))
+        return float(a.value), float(b.value)
 
     def last_counters(self):
         c = abi.rt_traversal_counters()
@@ -180,6 +204,11 @@ class MultiDeviceScene:
         h = C.c_void_p()
         check(lib().rt_multi_create(C.byref(flat.desc), arr, len(self.devices), int(band_h), C.byref(h)))
         self.h = h
+
+    def set_camera(self, cameraToWorld, fov):
+        """rt_scene_set_camera on every rank's scene."""
+        arr = (C.c_double * 16)(*[float(x) for x in glm.flat(cameraToWorld)])
+        check(lib().rt_multi_set_camera(self.h, arr, float(fov)))
 
     def render_frame(self, opts: Options, fb) -> Stats:
         """Whole frame into a host (h, w, 3) float32 array."""

@@ -18,8 +18,10 @@ import os
 import re
 import sys
 
-# the render call's kernels (a regex on the kernel name)
-KERNEL = r"k_render_fast<false|k_render_lean|k_render_gen|k_render_mix1"
+# the render call's kernels (a regex on the kernel name): the render kernels
+# and the per-call camera-dependent builders (rt_frame.hip)
+KERNEL = r"k_render_fast<false|k_render_lean|k_render_gen|k_render_mix1|k_frame_"
+RENDER = re.compile(r"k_render_fast<false|k_render_lean|k_render_gen|k_render_mix1")
 
 
 def means(path, kernel=None):
@@ -43,14 +45,20 @@ def main(pmc_dir, key, out="profiles/pmc_summary.json", note=""):
         if os.path.exists(f):
             for k, cs in means(f).items():
                 per_kernel[k].update(cs)
-    call = collections.defaultdict(float)
-    for cs in per_kernel.values():
+    call = collections.defaultdict(float)    # the render kernels of one call
+    setup = collections.defaultdict(float)   # the call's frame builders
+    for k, cs in per_kernel.items():
         for c, v in cs.items():
-            call[c] += v
+            (call if RENDER.search(k) else setup)[c] += v
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "nim-raytracer_amd"))
+    from rtmi._lib import kernel_source_hash
     d = json.load(open(out)) if os.path.exists(out) else {}
-    e = {"counters_mean_per_dispatch": dict(call), "per_kernel": per_kernel, "note": note}
+    e = {"counters_mean_per_dispatch": dict(call), "setup_counters_per_call": dict(setup),
+         "per_kernel": per_kernel, "note": note, "source_hash": kernel_source_hash()}
     if "FETCH_SIZE" in call and "WRITE_SIZE" in call:
         e["hbm_bytes_per_launch"] = (2 * call["FETCH_SIZE"] + call["WRITE_SIZE"]) * 1024
+        e["hbm_read_bytes_per_launch"] = 2 * call["FETCH_SIZE"] * 1024
+        e["hbm_write_bytes_per_launch"] = call["WRITE_SIZE"] * 1024
     d[key] = e
     json.dump(d, open(out, "w"), indent=1, sort_keys=True)
     print(json.dumps(e, indent=1))
