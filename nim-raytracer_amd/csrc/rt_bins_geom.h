@@ -133,16 +133,19 @@ struct SkipCam {
   double cam_a, cam_c, margin, bias;
   int width, height;
 };
-// Returns the skip bits (subset of `have`), or 0 when a horizon crosses the pixel.
-__host__ __device__ inline unsigned pixel_skip_bits(const SkipCam& c, const SkipPlaneC* planes, int nplanes,
-                                                    const SkipGrid* grids, int nl, unsigned have, int x, int y) {
+// The skip bits (a subset of `have`) shared by every pixel of the rectangle
+// [x0, x1] x [y0, y1] — its grown corner rays bound every pixel's — or 0
+// when a horizon crosses it. One pixel: x0 = x1, y0 = y1.
+__host__ __device__ inline unsigned rect_skip_bits(const SkipCam& c, const SkipPlaneC* planes, int nplanes,
+                                                   const SkipGrid* grids, int nl, unsigned have, int x0, int y0,
+                                                   int x1, int y1) {
   double dw[4][3];
   for (int k = 0; k < 4; ++k) {
-    const double px = (k & 1) ? x + 1 + c.margin : x - c.margin, py = (k & 2) ? y + 1 + c.margin : y - c.margin;
+    const double px = (k & 1) ? x1 + 1 + c.margin : x0 - c.margin, py = (k & 2) ? y1 + 1 + c.margin : y0 - c.margin;
     const double dc[3] = {(px - 0.5 * c.width) * c.cam_a, (0.5 * c.height - py) * c.cam_c, -1.0};
     xform_dir(c.c2w, dc, dw[k]);
-    const double len = norm3(dw[k]);
-    for (int a = 0; a < 3; ++a) dw[k][a] /= len;
+    const double il = 1.0 / norm3(dw[k]);
+    for (int a = 0; a < 3; ++a) dw[k][a] *= il;
   }
   unsigned bits = have;
   for (int k = 0; k < nplanes && bits; ++k) {
@@ -199,6 +202,10 @@ __host__ __device__ inline unsigned pixel_skip_bits(const SkipCam& c, const Skip
     }
   }
   return bits;
+}
+__host__ __device__ inline unsigned pixel_skip_bits(const SkipCam& c, const SkipPlaneC* planes, int nplanes,
+                                                    const SkipGrid* grids, int nl, unsigned have, int x, int y) {
+  return rect_skip_bits(c, planes, nplanes, grids, nl, have, x, y, x, y);
 }
 
 }  // namespace bg

@@ -2566,7 +2566,20 @@ __device__ __forceinline__ void lean1q_loop(KP p, const int32_t* order, int ngro
   // (ts = -(soy + ty) m_l, a hit at ts in [0, +inf) occludes it), against the
   // mesh by the pixel's record — a lean pixel's skip bits, built this call
   // (rt_frame.hip k_frame_records), say that no shadow ray leaving a camera
-  // hit of the pixel can meet a face of the mesh.
+  // hit of the pixel can meet a face of the mesh. When no lane's shadow ray
+  // hits the plane for a sample (the usual case: lights above the plane), a
+  // lit sample's colour is av = albedo x E over all lights — formed once here
+  // in the per-light chain's order, so it is the value that chain gives.
+  F3 av;
+  {
+    F3 E = f3(0.0f, 0.0f, 0.0f);
+#pragma unroll
+    for (int l = 0; l < NL; ++l)
+      E = f3(__builtin_fmaf(ci[l][0], ndl[l], E.x), __builtin_fmaf(ci[l][1], ndl[l], E.y),
+             __builtin_fmaf(ci[l][2], ndl[l], E.z));
+    av = mul3(alb, E);
+  }
+  asm volatile("" : "+v"(av.x), "+v"(av.y), "+v"(av.z));
   while (g < ngroups) {
     const int gg = order[g * PPI + lane / LP];  // this lane's pixel (list entry; -1: padding)
     qj = __builtin_amdgcn_readfirstlane(qj_next);
@@ -2625,16 +2638,24 @@ __device__ __forceinline__ void lean1q_loop(KP p, const int32_t* order, int ngro
         nlit += pc(litm);
         const bool lit = lane_in(litm);
         const float soy = __builtin_fmaf(1.0f, bias, __builtin_fmaf(dy, t, oy));
-        F3 E = f3(0.0f, 0.0f, 0.0f);
+        unsigned long long occ[NL], any = 0ull;
 #pragma unroll
         for (int l = 0; l < NL; ++l) {
           const float ts = -(soy + ty) * mulp[l];
-          const unsigned long long occ = m_hit0(ts) & litm;
-          nocc += pc(occ);
-          const float x = lane_in(litm & ~occ) ? ndl[l] : 0.0f;
-          E = f3(__builtin_fmaf(ci[l][0], x, E.x), __builtin_fmaf(ci[l][1], x, E.y), __builtin_fmaf(ci[l][2], x, E.z));
+          occ[l] = m_hit0(ts) & litm;
+          nocc += pc(occ[l]);
+          any |= occ[l];
         }
-        const F3 a = mul3(alb, E);
+        F3 a = av;
+        if (any != 0ull) {  // some shadow ray hit the plane: the per-light chain
+          F3 E = f3(0.0f, 0.0f, 0.0f);
+#pragma unroll
+          for (int l = 0; l < NL; ++l) {
+            const float x = lane_in(litm & ~occ[l]) ? ndl[l] : 0.0f;
+            E = f3(__builtin_fmaf(ci[l][0], x, E.x), __builtin_fmaf(ci[l][1], x, E.y), __builtin_fmaf(ci[l][2], x, E.z));
+          }
+          a = mul3(alb, E);
+        }
         acc[h] = f3(acc[h].x + (lit ? a.x : bg.x), acc[h].y + (lit ? a.y : bg.y), acc[h].z + (lit ? a.z : bg.z));
       }
       }

@@ -14,9 +14,15 @@
 //   rocprim exclusive scan of the counts -> per-pixel list offsets
 //   k_frame_bins_fill    per face again: scatter its record offset into each
 //                        listed pixel's list (the counts return to zero)
-//   k_frame_records      per pixel group of the launch: the record, and the
-//                        group appended to the lean or the general list
-//                        (wave ballot + mbcnt prefix, one atomic per wave)
+//   k_frame_tiles        per 64 x 4 tile of the launch: the shadow skips the
+//                        tile's pixels share (one test for the whole tile)
+//   k_frame_records      per pixel of the launch: the record (the tile's skip
+//                        bits, or the pixel's own test)
+//   k_frame_class_count  per block of groups in launch order: its lean and
+//                        general counts; a rocprim scan of them; then
+//   k_frame_class_write  the groups written to the lean and general lists at
+//                        their blocks' offsets (wave ballot + mbcnt ranks) —
+//                        the lists in launch order, no global atomics
 //   k_frame_obj_masks    (scenes of 4..64 objects) per pixel: 64-bit object mask
 // Every geometric bound is rt_bins_geom.h's, shared with the host builders
 // the tests compare against (float64, no FMA contraction on either side).
@@ -57,7 +63,8 @@ struct DevBinTri {
   int32_t pad;
 };
 
-// frame counters (one small device array, cleared by k_frame_bins_count)
+// frame counters (one small device array; cleared by k_frame_bins_count,
+// the list lengths written by k_frame_class_write)
 enum : int32_t { FC_OVERFLOW = 0, FC_HEAVY = 1, FC_LEAN = 2, FC_DONE = 3, FC_WORDS = 4 };
 
 struct BinsLaunch {
@@ -119,6 +126,10 @@ extern "C" {
 // count + scan; *scan_tmp_bytes in/out: the scan's scratch size (query with scan_tmp == nullptr)
 int rtmi_frame_bins_count(const rtmi::BinsLaunch* a, void* scan_tmp, size_t* scan_tmp_bytes, void* stream);
 int rtmi_frame_bins_fill(const rtmi::BinsLaunch* a, void* stream);
-int rtmi_frame_records(const rtmi::RecordsLaunch* a, void* stream);
+// records (+ lists); tile_bits: rtmi_frame_tile_bytes(ncols, nrows) bytes;
+// scratch: *scratch_bytes (query with scratch == nullptr)
+int rtmi_frame_records(const rtmi::RecordsLaunch* a, void* tile_bits, void* scratch, size_t* scratch_bytes,
+                       void* stream);
+long long rtmi_frame_tile_bytes(int ncols, int nrows);
 int rtmi_frame_obj_masks(const rtmi::ObjMaskLaunch* a, void* stream);
 }

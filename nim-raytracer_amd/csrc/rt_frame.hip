@@ -3,6 +3,8 @@
 // with -ffp-contract=off like the host builders the tests compare against.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include <rocprim/device/device_scan.hpp>
 
 #include "rt_bins.h"
@@ -79,15 +81,31 @@ __global__ __launch_bounds__(256) void k_frame_bins_fill(const BinsLaunch a) {
   }
 }
 
-// Per pixel group of the launch (one pixel each): the pixel record — list
-// length, and for an empty list the shadow skip bits (rt_bins_geom.h
-// pixel_skip_bits) — and, for a two-class launch, the group appended to the
-// lean list (empty list, every light skipped) or the general list: a wave
-// ballot per list, the lane's slot its mbcnt prefix, one atomic per wave. The
-// last block to finish pads the lean list with -1 to whole 64-entry runs.
-__global__ __launch_bounds__(256) void k_frame_records(const RecordsLaunch a) {
-  __shared__ bool last;
-  __shared__ bg::SkipGrid sg[8];
+// The launch's pixel at launch column j, launch row k (rt_fast.h lane_pixel
+// for one-pixel groups); valid = inside the launch and the image.
+struct LaunchPix {
+  int x, y;
+  bool valid, drawn;  // drawn: not skipped by a progressive pass
+};
+__device__ __forceinline__ LaunchPix launch_pixel(const RecordsLaunch& a, int j, int k) {
+  LaunchPix r;
+  r.x = j * a.step;
+  r.valid = j < a.ncols && k < a.nrows;
+  if (a.mode == 0) {
+    r.y = a.y0 + k * a.step;
+  } else {
+    r.y = (k / a.band_h * a.world + a.rank) * a.band_h + k % a.band_h;
+    r.valid = r.valid && r.y < a.height;
+  }
+  r.drawn = r.valid;
+  if (a.step < a.max_step) {  // progressive refinement skip (renderer.nim:175-178)
+    const int mask = a.step * 2 - 1;
+    if ((r.x & mask) == 0 && (r.y & mask) == 0) r.drawn = false;
+  }
+  return r;
+}
+
+__device__ __forceinline__ void load_skip_grids(const RecordsLaunch& a, bg::SkipGrid* sg) {
   if ((int)threadIdx.x < a.nl) {
     const LightGrid& G = a.grids[threadIdx.x];
     bg::SkipGrid& s = sg[threadIdx.x];
@@ -103,55 +121,110 @@ __global__ __launch_bounds__(256) void k_frame_records(const RecordsLaunch a) {
     s.sat = a.sat + a.sat_off[threadIdx.x];
   }
   __syncthreads();
-  const int gi = (int)(blockIdx.x * 256u + threadIdx.x);
-  bool valid = gi < a.ngroups;
-  const int g = valid ? (a.order ? a.order[gi] : gi) : 0;
+}
+
+// Records are built per tile of kTileW launch columns x kTileH launch rows
+// (one block, one wave per launch row). The tile's shadow skips are tested
+// once for the rectangle its pixels span (rt_bins_geom.h rect_skip_bits:
+// the tile's grown corner rays bound every pixel's, so a tile whose bits
+// cover every light gives each of its pixels exactly the bits the per-pixel
+// test would); the pixels of other tiles take the per-pixel test.
+constexpr int kTileW = 64, kTileH = 4;
+
+// One thread per tile: the tile's skip bits (0 when not every light is skipped).
+__global__ __launch_bounds__(256) void k_frame_tiles(const RecordsLaunch a, int tiles_x, int ntiles, uint8_t* tile_bits) {
+  __shared__ bg::SkipGrid sg[8];
+  load_skip_grids(a, sg);
+  const int t = (int)(blockIdx.x * 256u + threadIdx.x);
+  if (t >= ntiles) return;
+  const int tj = t % tiles_x, tk = t / tiles_x;
+  const int j0 = tj * kTileW, j1 = min(j0 + kTileW, a.ncols) - 1;
+  int ylo = 0x7fffffff, yhi = -1;
+  for (int k = tk * kTileH; k < min(tk * kTileH + kTileH, a.nrows); ++k) {
+    const LaunchPix p = launch_pixel(a, j0, k);
+    if (!p.valid) continue;
+    ylo = min(ylo, p.y);
+    yhi = max(yhi, p.y);
+  }
+  unsigned bits = 0u;
+  if (yhi >= 0) bits = bg::rect_skip_bits(a.cam, a.planes, a.nplanes, sg, a.nl, a.have, j0 * a.step, ylo, j1 * a.step, yhi);
+  tile_bits[t] = (uint8_t)(bits == a.have ? 1u : 0u);
+}
+
+// Per pixel of one tile (block (tile column, tile row)): the pixel record —
+// list length, and for an empty list the shadow skip bits (the tile's, or
+// the pixel's own test).
+__global__ __launch_bounds__(256) void k_frame_records(const RecordsLaunch a, const uint8_t* tile_bits) {
+  __shared__ bg::SkipGrid sg[8];
+  load_skip_grids(a, sg);
+  const int j = (int)blockIdx.x * kTileW + (int)(threadIdx.x & 63u);
+  const int k = (int)blockIdx.y * kTileH + (int)(threadIdx.x >> 6);
+  const LaunchPix p = launch_pixel(a, j, k);
+  if (!p.valid) return;
+  const size_t pix = (size_t)p.y * a.width + p.x;
+  const int32_t n = a.off[pix + 1] - a.off[pix];
+  uint32_t info = n < (int32_t)kPixCount ? (uint32_t)n : kPixCount;
+  if (n == 0 && a.have != 0u) {
+    const bool tile = tile_bits[blockIdx.y * gridDim.x + blockIdx.x] != 0;
+    const unsigned bits = tile ? a.have : bg::pixel_skip_bits(a.cam, a.planes, a.nplanes, sg, a.nl, a.have, p.x, p.y);
+    info |= bits << 24;
+  }
+  a.info[pix] = info;
+}
+
+// The class of the gi-th group of the launch order (order, or screen order):
+// 1 lean (empty list, every light skipped), 2 general, 0 not drawn.
+__device__ __forceinline__ int group_class(const RecordsLaunch& a, int gi, int* g_out) {
+  if (gi >= a.ngroups) return 0;
+  const int g = a.order ? a.order[gi] : gi;
+  *g_out = g;
   const int k = g / a.ncols, j = g - k * a.ncols;
-  const int x = j * a.step;
-  int y;
-  if (a.mode == 0) {
-    y = a.y0 + k * a.step;
-  } else {
-    y = (k / a.band_h * a.world + a.rank) * a.band_h + k % a.band_h;
-    valid = valid && y < a.height;
-  }
-  bool drawn = valid;
-  if (a.step < a.max_step) {  // progressive refinement skip (renderer.nim:175-178)
-    const int mask = a.step * 2 - 1;
-    if ((x & mask) == 0 && (y & mask) == 0) drawn = false;
-  }
-  uint32_t info = 0u;
-  if (valid) {
-    const size_t pix = (size_t)y * a.width + x;
-    const int32_t n = a.off[pix + 1] - a.off[pix];
-    info = n < (int32_t)kPixCount ? (uint32_t)n : kPixCount;
-    if (n == 0 && a.have != 0u) info |= bg::pixel_skip_bits(a.cam, a.planes, a.nplanes, sg, a.nl, a.have, x, y) << 24;
-    a.info[pix] = info;
-  }
-  if (!a.split) return;
-  const bool lean = drawn && (info & kPixCount) == 0u && ((info >> 24) & a.full) == a.full;
-  const bool heavy = drawn && !lean;
-  const unsigned long long ml = __ballot(lean), mh = __ballot(heavy);
-  const int lane = (int)(threadIdx.x & 63u);
-  int bl = 0, bh = 0;
-  if (lane == 0) {
-    if (ml) bl = atomicAdd(&a.ctr[FC_LEAN], (int)__popcll(ml));
-    if (mh) bh = atomicAdd(&a.ctr[FC_HEAVY], (int)__popcll(mh));
-  }
-  bl = __shfl(bl, 0);
-  bh = __shfl(bh, 0);
-  if (lean) a.lean[bl + (int)lane_rank(ml)] = g;
-  if (heavy) a.heavy[bh + (int)lane_rank(mh)] = g;
+  const LaunchPix p = launch_pixel(a, j, k);
+  if (!p.drawn) return 0;
+  const uint32_t info = a.info[(size_t)p.y * a.width + p.x];
+  return (info & kPixCount) == 0u && ((info >> 24) & a.full) == a.full ? 1 : 2;
+}
+
+// The lean / general lists in launch order, without a global atomic per wave
+// (one counter takes ~90 atomics/us: 32 k waves would serialise on it):
+// k_frame_class_count counts each block's lean and general groups (packed
+// lean << 32 | general), an exclusive scan gives every block its offsets,
+// k_frame_class_write writes each block's groups there (wave ballots, mbcnt
+// ranks, the waves' counts through LDS).
+__global__ __launch_bounds__(256) void k_frame_class_count(const RecordsLaunch a, unsigned long long* blk) {
+  __shared__ unsigned long long wsum[4];
+  int g = 0;
+  const int c = group_class(a, (int)(blockIdx.x * 256u + threadIdx.x), &g);
+  const unsigned long long ml = __ballot(c == 1), mh = __ballot(c == 2);
+  if ((threadIdx.x & 63u) == 0) wsum[threadIdx.x >> 6] = ((unsigned long long)__popcll(ml) << 32) | __popcll(mh);
   __syncthreads();
+  if (threadIdx.x == 0) blk[blockIdx.x] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+}
+
+__global__ __launch_bounds__(256) void k_frame_class_write(const RecordsLaunch a, const unsigned long long* blk,
+                                                           const unsigned long long* blk_off) {
+  __shared__ unsigned long long wsum[4];
+  int g = 0;
+  const int c = group_class(a, (int)(blockIdx.x * 256u + threadIdx.x), &g);
+  const unsigned long long ml = __ballot(c == 1), mh = __ballot(c == 2);
+  const int w = (int)(threadIdx.x >> 6);
+  if ((threadIdx.x & 63u) == 0) wsum[w] = ((unsigned long long)__popcll(ml) << 32) | __popcll(mh);
+  __syncthreads();
+  unsigned long long base = blk_off[blockIdx.x];
+  for (int i = 0; i < w; ++i) base += wsum[i];
+  if (c == 1) a.lean[(int)(base >> 32) + (int)lane_rank(ml)] = g;
+  if (c == 2) a.heavy[(int)(base & 0xffffffffu) + (int)lane_rank(mh)] = g;
+  if (blockIdx.x != gridDim.x - 1) return;
+  // the last block: the list lengths, and the lean list padded with -1 to
+  // whole 64-entry runs (the lean kernels read items of 4 / 16 entries)
+  const unsigned long long tot = blk_off[blockIdx.x] + blk[blockIdx.x];
+  const int nl = (int)(tot >> 32), nh = (int)(tot & 0xffffffffu);
   if (threadIdx.x == 0) {
-    __threadfence();
-    last = atomicAdd(&a.ctr[FC_DONE], 1) == (int)gridDim.x - 1;
+    a.ctr[FC_LEAN] = nl;
+    a.ctr[FC_HEAVY] = nh;
   }
-  __syncthreads();
-  if (!last) return;
-  const int n = atomicAdd(&a.ctr[FC_LEAN], 0);
-  const int end = n == 0 ? 64 : (n + 63) / 64 * 64;
-  for (int e = n + (int)threadIdx.x; e < end; e += 256) a.lean[e] = -1;
+  const int end = nl == 0 ? 64 : (nl + 63) / 64 * 64;
+  for (int e = nl + (int)threadIdx.x; e < end; e += 256) a.lean[e] = -1;
 }
 
 // Object masks (rt_bins.cpp build_object_pixel_masks): each block projects
@@ -229,10 +302,50 @@ extern "C" int rtmi_frame_bins_fill(const rtmi::BinsLaunch* a, void* stream) {
   return (int)hipGetLastError();
 }
 
-extern "C" int rtmi_frame_records(const rtmi::RecordsLaunch* a, void* stream) {
-  const int blocks = (a->ngroups + 255) / 256;
-  hipLaunchKernelGGL(rtmi::k_frame_records, dim3(blocks > 0 ? blocks : 1), dim3(256), 0, (hipStream_t)stream, *a);
+extern "C" int rtmi_frame_records(const rtmi::RecordsLaunch* a, void* tile_bits, void* scratch, size_t* scratch_bytes,
+                                  void* stream) {
+  using namespace rtmi;
+  hipStream_t st = (hipStream_t)stream;
+  const int nblk = std::max(1, (a->ngroups + 255) / 256);
+  // scratch: the per-block class counts, their scan, the scan's temporary storage
+  const size_t cnt_bytes = ((size_t)nblk * sizeof(unsigned long long) + 255) / 256 * 256;
+  size_t scan_bytes = 0;
+  hipError_t e = rocprim::exclusive_scan(nullptr, scan_bytes, (unsigned long long*)nullptr,
+                                         (unsigned long long*)nullptr, 0ull, (size_t)nblk,
+                                         rocprim::plus<unsigned long long>(), st);
+  if (e != hipSuccess) return (int)e;
+  if (!scratch) {
+    *scratch_bytes = 2 * cnt_bytes + scan_bytes;
+    return 0;
+  }
+  if (*scratch_bytes < 2 * cnt_bytes + scan_bytes) return (int)hipErrorInvalidValue;
+  const int tiles_x = (a->ncols + kTileW - 1) / kTileW, tiles_y = (a->nrows + kTileH - 1) / kTileH;
+  const int ntiles = tiles_x * tiles_y;
+  if (ntiles <= 0) return 0;
+  if (a->have != 0u) {
+    hipLaunchKernelGGL(k_frame_tiles, dim3((ntiles + 255) / 256), dim3(256), 0, st, *a, tiles_x, ntiles,
+                       (uint8_t*)tile_bits);
+    if ((e = hipGetLastError()) != hipSuccess) return (int)e;
+  }
+  hipLaunchKernelGGL(k_frame_records, dim3(tiles_x, tiles_y), dim3(256), 0, st, *a, (const uint8_t*)tile_bits);
+  if ((e = hipGetLastError()) != hipSuccess || !a->split) return (int)e;
+  unsigned long long* blk = (unsigned long long*)scratch;
+  unsigned long long* blk_off = (unsigned long long*)((char*)scratch + cnt_bytes);
+  void* tmp = (char*)scratch + 2 * cnt_bytes;
+  hipLaunchKernelGGL(k_frame_class_count, dim3(nblk), dim3(256), 0, st, *a, blk);
+  if ((e = hipGetLastError()) != hipSuccess) return (int)e;
+  if ((e = rocprim::exclusive_scan(tmp, scan_bytes, blk, blk_off, 0ull, (size_t)nblk,
+                                   rocprim::plus<unsigned long long>(), st)) != hipSuccess)
+    return (int)e;
+  hipLaunchKernelGGL(k_frame_class_write, dim3(nblk), dim3(256), 0, st, *a, (const unsigned long long*)blk,
+                     (const unsigned long long*)blk_off);
   return (int)hipGetLastError();
+}
+
+// Tile-bit bytes rtmi_frame_records needs for a launch of ncols x nrows groups.
+extern "C" long long rtmi_frame_tile_bytes(int ncols, int nrows) {
+  using namespace rtmi;
+  return (long long)((ncols + kTileW - 1) / kTileW) * ((nrows + kTileH - 1) / kTileH);
 }
 
 extern "C" int rtmi_frame_obj_masks(const rtmi::ObjMaskLaunch* a, void* stream) {

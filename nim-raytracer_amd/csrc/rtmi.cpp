@@ -208,13 +208,16 @@ struct rt_scene {
     DevBuf<uint32_t> info;
     DevBuf<unsigned long long> omask;
     DevBuf<unsigned char> scan_tmp;
+    DevBuf<unsigned char> tiles;   // per-tile shadow skips (k_frame_tiles)
+    DevBuf<unsigned char> cls;     // the class counts' scratch (k_frame_class_count + scan)
     // launch row sets whose list entries `ent` is known to hold for the
     // current camera (the first call of a row set reads its entry count)
     std::vector<std::array<int64_t, 9>> sized;
     bool counted = false;          // the last launch's lean / general lists were counted on the device
     void release() {
       cnt.release(); off.release(); ent.release(); rect.release(); lean.release(); heavy.release(); ctr.release();
-      proj.release(); info.release(); omask.release(); scan_tmp.release();
+      proj.release(); info.release(); omask.release(); scan_tmp.release(); tiles.release();
+      cls.release();
       sized.clear();
     }
   } fr;
@@ -1222,7 +1225,8 @@ int frame_buffers(rt_scene* s, int w, int h, hipStream_t st) {
   f.w = f.h = 0;
   f.sized.clear();
   if ((rc = f.cnt.alloc(npx + 1)) || (rc = f.off.alloc(npx + 1)) || (rc = f.info.alloc(npx)) ||
-      (rc = f.lean.alloc(npx + 64)) || (rc = f.heavy.alloc(npx)) || (rc = f.ctr.alloc(FC_WORDS)))
+      (rc = f.lean.alloc(npx + 64)) || (rc = f.heavy.alloc(npx)) || (rc = f.ctr.alloc(FC_WORDS)) ||
+      (rc = f.tiles.alloc((size_t)rtmi_frame_tile_bytes(w, h))))
     return rc;
   if (s->objbins && (rc = f.omask.alloc(npx))) return rc;
   if (nf > 0 && (f.rect.n < 4 * nf || f.proj.n < 6 * nf)) {
@@ -1350,7 +1354,16 @@ int frame_records(rt_scene* s, const rt_options* o, const Mapping& mp, const Fas
   r.lean = s->fr.lean.p;
   r.heavy = s->fr.heavy.p;
   r.ctr = s->fr.ctr.p;
-  const int e = rtmi_frame_records(&r, st);
+  size_t bytes = 0;
+  int e = rtmi_frame_records(&r, s->fr.tiles.p, nullptr, &bytes, st);
+  if (e) return fail(RT_E_DEVICE, "pixel record scratch query failed: %s", hipGetErrorString((hipError_t)e));
+  if (s->fr.cls.n < bytes) {
+    HIP_TRY(hipStreamSynchronize(st));  // an earlier call may still use the old scratch
+    const int rc = s->fr.cls.alloc(bytes);
+    if (rc) return rc;
+  }
+  bytes = s->fr.cls.n;
+  e = rtmi_frame_records(&r, s->fr.tiles.p, s->fr.cls.p, &bytes, st);
   if (e) return fail(RT_E_DEVICE, "pixel record launch failed: %s", hipGetErrorString((hipError_t)e));
   return RT_OK;
 }
