@@ -17,36 +17,44 @@ __device__ __forceinline__ unsigned lane_rank(unsigned long long m) {
   return __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
 }
 
+// kFaceLanes threads per face: each takes every kFaceLanes-th pixel of the
+// face's rectangle (a face covers a few pixels; one thread per face left the
+// GPU a quarter of a wave per SIMD — latency-bound at 69 k faces).
+constexpr int kFaceLanes = 4;
+
 // Per face: its pixel rectangle and projected vertices (kept for the fill
 // pass), and one count per pixel of the launch's rows that the face's grown
 // projection meets (rt_bins.cpp build_pixel_bins, the same bounds).
 __global__ __launch_bounds__(256) void k_frame_bins_count(const BinsLaunch a) {
-  const int i = (int)(blockIdx.x * 256u + threadIdx.x);
-  if (i == 0) {
+  const int t = (int)(blockIdx.x * 256u + threadIdx.x);
+  if (t == 0) {
 #pragma unroll
     for (int k = 0; k < FC_WORDS; ++k) a.ctr[k] = 0;
   }
+  const int i = t / kFaceLanes, q = t % kFaceLanes;
   if (i >= a.nf) return;
   double v[3][3];
 #pragma unroll
   for (int p = 0; p < 3; ++p)
 #pragma unroll
     for (int k = 0; k < 3; ++k) v[p][k] = a.tris[i].v[p][k];
-  double q[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+  double pr[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
   int r[4];
   // (a vertex at or behind the camera plane: the host checked the mesh box
   // against the camera plane before launching, so this never fails)
-  if (!bg::face_pixel_rect(a.cam, v, q, r)) r[0] = -1;
-  reinterpret_cast<int4*>(a.rect)[i] = make_int4(r[0], r[1], r[2], r[3]);
+  if (!bg::face_pixel_rect(a.cam, v, pr, r)) r[0] = -1;
+  if (q == 0) {
+    reinterpret_cast<int4*>(a.rect)[i] = make_int4(r[0], r[1], r[2], r[3]);
 #pragma unroll
-  for (int k = 0; k < 6; ++k) a.proj[6 * (size_t)i + k] = q[k];
+    for (int k = 0; k < 6; ++k) a.proj[6 * (size_t)i + k] = pr[k];
+  }
   if (r[0] < 0) return;
   const double m = a.cam.margin;
-  for (int y = r[2]; y <= r[3]; ++y) {
-    if (!frame_has_row(a.rows, y)) continue;
-    for (int x = r[0]; x <= r[1]; ++x)
-      if (bg::tri_meets_box(q, x - m, y - m, x + 1 + m, y + 1 + m))
-        atomicAdd(&a.cnt[(size_t)y * a.cam.width + x], 1);
+  const int rw = r[1] - r[0] + 1, area = rw * (r[3] - r[2] + 1);
+  for (int idx = q; idx < area; idx += kFaceLanes) {
+    const int y = r[2] + idx / rw, x = r[0] + idx % rw;
+    if (frame_has_row(a.rows, y) && bg::tri_meets_box(pr, x - m, y - m, x + 1 + m, y + 1 + m))
+      atomicAdd(&a.cnt[(size_t)y * a.cam.width + x], 1);
   }
 }
 
@@ -54,30 +62,31 @@ __global__ __launch_bounds__(256) void k_frame_bins_count(const BinsLaunch a) {
 // slot comes from counting the pixel's count back down, so the counts are
 // zero again for the next call (no clearing pass).
 __global__ __launch_bounds__(256) void k_frame_bins_fill(const BinsLaunch a) {
-  const int i = (int)(blockIdx.x * 256u + threadIdx.x);
-  if (i == 0) {  // read-ahead padding after the last list (rt_bins.h kBinPad)
+  const int t = (int)(blockIdx.x * 256u + threadIdx.x);
+  if (t == 0) {  // read-ahead padding after the last list (rt_bins.h kBinPad)
     const int64_t total = a.off[a.scan_lo + a.scan_n - 1];
     for (int k = 0; k < kBinPad; ++k)
       if (total + k < a.cap) a.ent[total + k] = a.pad_rec;
     if (total + kBinPad > a.cap) atomicOr(&a.ctr[FC_OVERFLOW], 1);
   }
+  const int i = t / kFaceLanes, q = t % kFaceLanes;
   if (i >= a.nf) return;
   const int4 r = reinterpret_cast<const int4*>(a.rect)[i];
   if (r.x < 0) return;
-  double q[6];
+  double pr[6];
 #pragma unroll
-  for (int k = 0; k < 6; ++k) q[k] = a.proj[6 * (size_t)i + k];
+  for (int k = 0; k < 6; ++k) pr[k] = a.proj[6 * (size_t)i + k];
   const int32_t rec = a.tris[i].rec;
   const double m = a.cam.margin;
-  for (int y = r.z; y <= r.w; ++y) {
-    if (!frame_has_row(a.rows, y)) continue;
-    for (int x = r.x; x <= r.y; ++x)
-      if (bg::tri_meets_box(q, x - m, y - m, x + 1 + m, y + 1 + m)) {
-        const size_t pix = (size_t)y * a.cam.width + x;
-        const int64_t slot = (int64_t)a.off[pix] + atomicSub(&a.cnt[pix], 1) - 1;
-        if (slot < a.cap) a.ent[slot] = rec;
-        else atomicOr(&a.ctr[FC_OVERFLOW], 1);
-      }
+  const int rw = r.y - r.x + 1, area = rw * (r.w - r.z + 1);
+  for (int idx = q; idx < area; idx += kFaceLanes) {
+    const int y = r.z + idx / rw, x = r.x + idx % rw;
+    if (frame_has_row(a.rows, y) && bg::tri_meets_box(pr, x - m, y - m, x + 1 + m, y + 1 + m)) {
+      const size_t pix = (size_t)y * a.cam.width + x;
+      const int64_t slot = (int64_t)a.off[pix] + atomicSub(&a.cnt[pix], 1) - 1;
+      if (slot < a.cap) a.ent[slot] = rec;
+      else atomicOr(&a.ctr[FC_OVERFLOW], 1);
+    }
   }
 }
 
@@ -288,7 +297,7 @@ extern "C" int rtmi_frame_bins_count(const rtmi::BinsLaunch* a, void* scan_tmp, 
     return (int)rocprim::exclusive_scan(nullptr, *scan_tmp_bytes, a->cnt, a->off, 0, (size_t)a->scan_n,
                                         rocprim::plus<int32_t>(), st);
   }
-  const int blocks = (a->nf + 255) / 256;
+  const int blocks = (int)(((long long)a->nf * rtmi::kFaceLanes + 255) / 256);
   hipLaunchKernelGGL(rtmi::k_frame_bins_count, dim3(blocks > 0 ? blocks : 1), dim3(256), 0, st, *a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
@@ -297,7 +306,7 @@ extern "C" int rtmi_frame_bins_count(const rtmi::BinsLaunch* a, void* scan_tmp, 
 }
 
 extern "C" int rtmi_frame_bins_fill(const rtmi::BinsLaunch* a, void* stream) {
-  const int blocks = (a->nf + 255) / 256;
+  const int blocks = (int)(((long long)a->nf * rtmi::kFaceLanes + 255) / 256);
   hipLaunchKernelGGL(rtmi::k_frame_bins_fill, dim3(blocks > 0 ? blocks : 1), dim3(256), 0, (hipStream_t)stream, *a);
   return (int)hipGetLastError();
 }
