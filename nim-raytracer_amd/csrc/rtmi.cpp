@@ -1106,9 +1106,13 @@ int order_policy() {
   static const int v = [] {
     // tuning knob: 0 off, 1 LPT, 2 LPT in half octaves, 3 heavy then light
     // (split at the RTMI_ORDER_P cost quantile, screen order within each),
-    // 4 = 3 with the light part longest-first
+    // 4 = 3 with the light part longest-first. Off by default (round 3): the
+    // costs are measured on an earlier frame of the same camera, and no
+    // camera-dependent data is carried from one call to the next; the
+    // two-class launches already hand out the expensive (general) pixels
+    // before the cheap (lean) ones.
     const char* e = std::getenv("RTMI_ORDER");
-    return e ? std::atoi(e) : 1;
+    return e ? std::atoi(e) : 0;
   }();
   return v;
 }

@@ -1,0 +1,182 @@
+"""Parity at the BASELINE.json configs, through the kernels the benchmark runs.
+
+The oracle here is oracle/rt_oracle.c in its same-BVH mode (a per-ray
+float64 BVH whose answers — closest t, lowest face on ties, every Stats count
+— are those of the reference's brute-force TriangleMesh.intersect,
+geom.nim:339-358; tests/test_oracle_bvh.py proves the equality), so the
+frames below are the reference algorithm's at the benchmark's sample counts.
+
+Tolerance (float32 performance path, DESIGN.md "Parity"): per pixel the
+largest channel error |gpu - oracle| <= 2e-3 on >= 99.5 % of the pixels and a
+mean <= 2e-4; primary-ray counts exact; shadow-ray and hit counts within
+1e-4 relative (a float32 camera ray that lands on the other side of a
+silhouette than the float64 one changes one hit and its two shadow rays).
+
+  C1  spheres-warm balls 1-3 + ground, 512x512, akNone (every pixel)
+  C2  boxes2 (16 primitives), 1920x1080, 64 spp (full frame on the GPU,
+      8 full rows against the oracle)
+  C3  bunny + ground, 256 spp: the whole 480x270 frame, and 8 full rows of
+      the 1920x1080 frame — through k_render_mix1, the benchmarked kernel
+  C4  bunny, 3840x2160, 1024 spp on one GPU: properties + 2 oracle rows
+  C5  1M-triangle torus, 3840x2160, 4096 spp on one GPU: properties + 1 row
+"""
+import numpy as np
+import pytest
+
+from rtmi import Antialias, Options, Precision, akGrid, akNone, scenes
+from rtmi.renderer import DeviceScene
+
+pytestmark = pytest.mark.gpu
+
+BIAS = 1e-4
+THREADS = 16  # the GPU box's CPU share
+
+
+def _opts(w, h, m, prec=Precision.fp32):
+    aa = akGrid if m > 1 else akNone
+    return Options(width=w, height=h, antialias=Antialias(aa, m), bias=BIAS, precision=prec)
+
+
+def _check(got, ref, what, frac=0.995, tol=2e-3, mean_tol=2e-4):
+    err = np.abs(got.astype(np.float64) - ref.astype(np.float64)).max(axis=-1)
+    ok = float((err <= tol).mean())
+    assert ok >= frac, f"{what}: only {ok:.5f} of pixels within {tol} (max {err.max():.3g})"
+    assert err.mean() <= mean_tol, f"{what}: mean abs err {err.mean():.3g}"
+    return ok, float(err.max())
+
+
+def _counts_close(gst, rst, rel=1e-4):
+    assert gst.numPrimaryRays == rst.numPrimaryRays
+    assert abs(gst.numShadowRays - rst.numShadowRays) <= rel * rst.numShadowRays + 2, (gst, rst)
+    assert abs(gst.numIntersectionHits - rst.numIntersectionHits) <= rel * rst.numIntersectionHits + 2, (gst, rst)
+    assert gst.numReflectionRays == rst.numReflectionRays
+
+
+def _gpu(ds, opts):
+    import torch
+    fb = torch.zeros(opts.width * opts.height * 3, dtype=torch.float32, device="cuda")
+    st = ds.render_device(opts, fb)
+    return fb.view(opts.height, opts.width, 3).cpu().numpy(), st
+
+
+def _oracle_rows(scene, opts, rows, bvh=True):
+    import oracle
+    ref = np.zeros((opts.height, opts.width, 3), np.float32)
+    o = oracle.OracleScene(scene, bvh=bvh)
+    _, st, _ = o.render(Options(width=opts.width, height=opts.height, antialias=opts.antialias, bias=opts.bias,
+                                precision=Precision.fp64), rows=rows, fb=ref, nthreads=THREADS)
+    return ref, st
+
+
+def _row_stats(ds, opts, rows):
+    """The GPU's Stats over the same rows (one call per row: renderLine)."""
+    import torch
+    from rtmi.scene import Stats
+    fb = torch.zeros(opts.width * opts.height * 3, dtype=torch.float32, device="cuda")
+    tot = Stats()
+    for y in rows:
+        tot += ds.render_device(opts, fb, y0=y, y1=y + 1)
+    return tot
+
+
+def test_c1_512_every_pixel(gpu):
+    """C1: spheres-warm balls 1-3 + ground at 512x512, 1 spp: the whole frame,
+    float64 bit-exact and float32 within tolerance."""
+    sc = scenes.spheres_warm(3)
+    ref, rst = _oracle_rows(sc, _opts(512, 512, 1), list(range(512)), bvh=False)
+    ds = DeviceScene(sc)
+    got64, st64 = _gpu(ds, _opts(512, 512, 1, Precision.fp64))
+    assert np.array_equal(got64, ref) and st64 == rst
+    got32, st32 = _gpu(ds, _opts(512, 512, 1))
+    _check(got32, ref, "C1 fp32")
+    _counts_close(st32, rst, rel=2e-3)
+
+
+def test_c2_1080p_64spp_rows(gpu):
+    """C2: boxes2 at 1920x1080, 64 spp (the benchmark's kernel: object bins,
+    one-pixel waves), 8 full rows against the oracle."""
+    sc = scenes.boxes2()
+    o = _opts(1920, 1080, 8)
+    ds = DeviceScene(sc)
+    got, st = _gpu(ds, o)
+    assert st.numPrimaryRays == 1920 * 1080 * 64
+    rows = [120, 300, 420, 540, 600, 700, 820, 1000]
+    ref, rst = _oracle_rows(sc, o, rows, bvh=False)
+    _check(got[rows], ref[rows], "C2 rows")
+    _counts_close(_row_stats(ds, o, rows), rst)
+
+
+def test_c3_256spp_whole_frame(gpu):
+    """C3's scene and sampling (bunny + ground, akGrid 16 = 256 spp) on a
+    480x270 frame: every pixel against the oracle, rendered by the merged
+    one-plane kernel k_render_mix1 (general pixels, then lean pixels)."""
+    sc = scenes.mesh_bunny()
+    o = _opts(480, 270, 16)
+    ds = DeviceScene(sc)
+    got, st = _gpu(ds, o)
+    assert ds.last_lean_kernel() == 3 | 3 << 2, ds.last_lean_kernel()  # k_render_mix1
+    lean, general = ds.last_split()
+    assert lean > 0 and general > 0 and lean + general == 480 * 270
+    ref, rst = _oracle_rows(sc, o, list(range(270)))
+    _check(got, ref, "C3 480x270")
+    _counts_close(st, rst)
+
+
+def test_c3_1080p_rows(gpu):
+    """C3 at its full size: the 1920x1080 frame of the benchmark (k_render_mix1),
+    8 full rows through the bunny, its shadows and the horizon against the
+    oracle at 256 spp."""
+    sc = scenes.mesh_bunny()
+    o = _opts(1920, 1080, 16)
+    ds = DeviceScene(sc)
+    got, st = _gpu(ds, o)
+    assert ds.last_lean_kernel() == 3 | 3 << 2, ds.last_lean_kernel()
+    assert st.numPrimaryRays == 1920 * 1080 * 256
+    rows = [200, 380, 470, 520, 560, 610, 680, 900]
+    ref, rst = _oracle_rows(sc, o, rows)
+    _check(got[rows], ref[rows], "C3 rows")
+    _counts_close(_row_stats(ds, o, rows), rst)
+
+
+def _properties(ds, o, st_expected_primary):
+    import torch
+    a = torch.zeros(o.width * o.height * 3, dtype=torch.float32, device="cuda")
+    b = torch.zeros_like(a)
+    sa = ds.render_device(o, a)
+    sb = ds.render_device(o, b)
+    assert torch.equal(a, b) and sa == sb  # deterministic frame after frame
+    assert sa.numPrimaryRays == st_expected_primary
+    # one shadow ray per light (2) per shaded camera hit, no reflections
+    assert sa.numShadowRays % 2 == 0 and 0 < sa.numShadowRays < 2 * sa.numPrimaryRays
+    assert sa.numReflectionRays == 0
+    img = a.view(o.height, o.width, 3)
+    assert bool(torch.isfinite(img).all()) and float(img.min()) >= 0.0
+    return img.cpu().numpy(), sa
+
+
+def test_c4_4k_1024spp(gpu):
+    """C4 (bunny, 3840x2160, 1024 spp) on one GPU: determinism, ray
+    accounting, finite non-negative output, and 2 full rows at 1024 spp
+    against the oracle."""
+    sc = scenes.mesh_bunny()
+    o = _opts(3840, 2160, 32)
+    ds = DeviceScene(sc)
+    img, st = _properties(ds, o, 3840 * 2160 * 1024)
+    rows = [1000, 1240]
+    ref, rst = _oracle_rows(sc, o, rows)
+    _check(img[rows], ref[rows], "C4 rows")
+    _counts_close(_row_stats(ds, o, rows), rst)
+
+
+def test_c5_torus_4k_4096spp(gpu):
+    """C5 (1,000,000-triangle torus, 3840x2160, 4096 spp) on one GPU:
+    determinism, ray accounting, and one full row at 4096 spp against the
+    oracle."""
+    sc = scenes.torus_scene()
+    o = _opts(3840, 2160, 64)
+    ds = DeviceScene(sc)
+    img, st = _properties(ds, o, 3840 * 2160 * 4096)
+    rows = [1150]
+    ref, rst = _oracle_rows(sc, o, rows)
+    _check(img[rows], ref[rows], "C5 row")
+    _counts_close(_row_stats(ds, o, rows), rst)
