@@ -206,6 +206,12 @@ typedef struct rt_options {
  * records, lean / general lists, object masks) and its render kernels;
  * rt_scene_last_timing reads them. Same image and Stats. */
 #define RT_FLAG_TIMING 0x800u
+/* float32 kernel, scenes of spheres / boxes / planes with distant lights and
+ * no reflection: trace one sample per lane at a time. By default such pixels
+ * carry 4 samples per lane through their object-binned object and light
+ * loops (and a 64-spp frame uses 16 lanes per pixel to fill that batch).
+ * Same image and Stats. */
+#define RT_FLAG_NO_OBJ_BATCH 0x1000u
 
 /* Stats (src/renderer/stats.nim:4-13) plus ray counts for Mray/s. */
 typedef struct rt_stats {

@@ -21,7 +21,7 @@ enum : int32_t { LIGHT_DISTANT = 0, LIGHT_POINT = 1 };
 // DevObject.xf: what world_to_object is (host-classified, float32 fast paths)
 enum : int32_t { XF_IDENTITY = 0, XF_TRANSLATE = 1, XF_GENERAL = 2 };
 // RenderParams.flags bits
-enum : int32_t { RT_DEV_FLAG_COUNT = 0x2, RT_DEV_FLAG_FALLBACK = 0x40 };
+enum : int32_t { RT_DEV_FLAG_COUNT = 0x2, RT_DEV_FLAG_FALLBACK = 0x40, RT_DEV_FLAG_NO_OBJ_BATCH = 0x1000 };
 
 constexpr int kMaxBvhDepth = 60;      // stack fits one 64-lane VGPR
 constexpr int kLeafMax = 4;           // triangles per BVH leaf (arrays padded by kLeafMax-1)

@@ -1053,8 +1053,9 @@ __device__ __forceinline__ void batch_dirs(KP p, const GroupPix& gp, int it0, co
   // validity without short-circuit branches (a per-lane && became an
   // exec-mask branch with the argument load inside, per sample)
   const int spp = p->spp;
-  if (p->aa_kind == 1 && p->log2_grid_m >= 0 && p->log2_grid_m <= 6) {
-    // m divides 64: sample s = it * 64 + sub keeps the lane's column
+  const int L = p->lanes_per_px;  // 64: one-pixel waves; 16: object-binned batches of 4 pixels
+  if (p->aa_kind == 1 && p->log2_grid_m >= 0 && p->log2_grid_m <= p->log2_lanes) {
+    // m divides L: sample s = it * L + sub keeps the lane's column
     // s & (m-1) = sub & (m-1) in every iteration — px (and the camera ray's
     // cx) once per batch, the same values as per sample
     const int mm = p->grid_m - 1, lg = p->log2_grid_m;
@@ -1062,7 +1063,7 @@ __device__ __forceinline__ void batch_dirs(KP p, const GroupPix& gp, int it0, co
     const float pxl = (float)gp.x + __builtin_fmaf((float)(gp.sub & mm), st, of);
 #pragma unroll
     for (int k = 0; k < S; ++k) {
-      const int s = (it0 + k) * 64 + gp.sub;
+      const int s = (it0 + k) * L + gp.sub;
       sv[k] = gp.valid & (s < spp);
       px[k] = pxl;
       py[k] = (float)gp.y + __builtin_fmaf((float)(s >> lg), st, of);
@@ -1072,7 +1073,7 @@ __device__ __forceinline__ void batch_dirs(KP p, const GroupPix& gp, int it0, co
     const float st = p->sample_step, of = p->sample_off;
 #pragma unroll
     for (int k = 0; k < S; ++k) {
-      const int s = (it0 + k) * 64 + gp.sub;
+      const int s = (it0 + k) * L + gp.sub;
       sv[k] = gp.valid & (s < spp);
       px[k] = (float)gp.x + __builtin_fmaf((float)(s & mm), st, of);
       py[k] = (float)gp.y + __builtin_fmaf((float)(s >> lg), st, of);
@@ -1080,7 +1081,7 @@ __device__ __forceinline__ void batch_dirs(KP p, const GroupPix& gp, int it0, co
   } else {
 #pragma unroll
     for (int k = 0; k < S; ++k) {
-      const int s = (it0 + k) * 64 + gp.sub;
+      const int s = (it0 + k) * L + gp.sub;
       sv[k] = gp.valid & (s < spp);
       camera_pos<F>(p, gp, s < spp ? s : 0, tb, px[k], py[k]);
     }
@@ -1106,9 +1107,15 @@ __device__ __forceinline__ void batch_dirs(KP p, const GroupPix& gp, int it0, co
 #define RTMI_LEAN_BATCH 4
 #endif
 constexpr int kLeanBatch = RTMI_LEAN_BATCH;
-template <unsigned F, int S = kLeanBatch>
+// OB (object-binned batches, scenes without a mesh: k_render_fast): the
+// camera rays visit only the objects of `cmask` (the wave's pixels' object
+// masks, rt_bins.h build_object_pixel_masks) and each light's shadow rays
+// only those of the light-grid cells their origins fall in — in scene order,
+// exactly as trace's object bins (an object no bin lists cannot be hit, so it
+// adds nothing to a closest hit or a hit count).
+template <unsigned F, int S = kLeanBatch, bool OB = false>
 __device__ __forceinline__ void lean_batch(KP p, const GroupPix& gp, int it0, const LdsF* tb, Acc& acc,
-                                           Stats32& ws) {
+                                           Stats32& ws, unsigned long long cmask = ~0ull) {
   // Branch-free: per-sample predicates are lane masks in SGPRs and every
   // update is a select (v_cndmask), so the samples' code is straight-line
   // VALU (no exec-mask save / restore per sample). A masked-off term adds an
@@ -1157,7 +1164,21 @@ __device__ __forceinline__ void lean_batch(KP p, const GroupPix& gp, int it0, co
     for (int i = 0; i < nobj; ++i)
       if (i != mesh) body(i);
   };
-  analytic_objects([&](const int i) {
+  // OB: the objects of a mask in scene order (object bins exist for <= 64 objects)
+  auto masked_objects = [&](unsigned long long m, auto&& body) {
+    if constexpr (OB) {
+      m &= nobj >= 64 ? ~0ull : ((1ull << nobj) - 1ull);
+      while (m != 0ull) {
+        const int i = (int)__builtin_ctzll(m);
+        m &= m - 1ull;
+        if (i != mesh) body(i);
+      }
+    } else {
+      (void)m;
+      analytic_objects(body);
+    }
+  };
+  masked_objects(cmask, [&](const int i) {
     const FObj ob = at(objs, i);
 #pragma unroll
     for (int k = 0; k < S; ++k) {
@@ -1260,7 +1281,37 @@ __device__ __forceinline__ void lean_batch(KP p, const GroupPix& gp, int it0, co
       float ts[S];  // unlit samples start at 0 (take no part)
 #pragma unroll
       for (int k = 0; k < S; ++k) ts[k] = lane_in(litm[k]) ? finf() : 0.0f;
-      analytic_objects([&](const int i) {
+      unsigned long long smask = ~0ull;  // every object
+      if constexpr (OB) {
+        // the light-grid cells of the lit samples' shadow origins (trace's
+        // rule: off the grid -> the unbounded objects; beyond the grid's
+        // float32-safe radius, or more than 4 distinct cells -> every object)
+        if (p->obj_grids && cp(p->obj_grids)[li].gu > 0) {
+          const RT_CONST LightGrid& G = cp(p->obj_grids)[li];
+          unsigned long long m = p->obj_off_grid;
+          bool every = false;
+#pragma unroll
+          for (int k = 0; k < S; ++k) {
+            const bool lk = lane_in(litm[k]);
+            const F3 q = so[k];
+            const float gu = __builtin_fmaf(q.x, G.e1[0], __builtin_fmaf(q.y, G.e1[1], q.z * G.e1[2]));
+            const float gv = __builtin_fmaf(q.x, G.e2[0], __builtin_fmaf(q.y, G.e2[1], q.z * G.e2[2]));
+            const float fu = (gu - G.u0) * G.inv_h, fv = (gv - G.v0) * G.inv_h;
+            const bool safe = fmaxf(fmaxf(fabsf(q.x), fabsf(q.y)), fabsf(q.z)) <= G.rmax;
+            const bool on = fu >= 0.0f && fu < (float)G.gu && fv >= 0.0f && fv < (float)G.gv;
+            const int cell = on ? (int)fv * G.gu + (int)fu : -1;
+            unsigned long long todo = bal(lk && safe && on);
+            for (int it = 0; it < 4 && todo != 0ull; ++it) {
+              const int kc = __builtin_amdgcn_readlane(cell, (int)__builtin_ctzll(todo));
+              todo &= ~bal(cell == kc);
+              m |= cp(p->obj_grid_mask)[G.off_base + kc];
+            }
+            every = every || todo != 0ull || bal(lk && !safe) != 0ull;
+          }
+          smask = every ? smask : m;
+        }
+      }
+      masked_objects(smask, [&](const int i) {
         const FObj ob = at(objs, i);
         if constexpr (kPlanesOnly) {
           // Plane.intersect (geom.nim:240-248) of the parallel shadow rays:
@@ -2222,6 +2273,27 @@ __global__ __launch_bounds__(256) RTMI_OCC void k_render_fast(const FastParams p
       for (; it + kLeanBatch <= iters; it += kLeanBatch) lean_batch<F>(p, gp, it, tb, pacc, ws);
 #endif
       if (it < iters) sample_loop(Bool<true>{}, it);
+    } else if constexpr (!(F & (F_MESH | F_REFLECT | F_POINT)) && (F & (F_SPHERE | F_BOX)) != 0) {
+      // analytic scenes with distant lights (C2): object-binned batches —
+      // kLeanBatch samples per lane through the wave's pixels' object masks
+      // and the shadow rays' light-grid cell masks, so each object visit's
+      // scalar work (record load, dispatch, loop control) serves 64 x
+      // kLeanBatch rays; the remaining iterations one sample at a time
+      unsigned long long cmask = p->nobj >= 64 ? ~0ull : ((1ull << p->nobj) - 1ull);
+      if (p->obj_pix) {
+        const int pix = gp.valid ? gp.y * p->width + gp.x : -1;
+        unsigned long long todo = bal(pix >= 0), m = 0ull;
+        for (int k = 0; k < 4 && todo != 0ull; ++k) {
+          const int kp = __builtin_amdgcn_readlane(pix, (int)__builtin_ctzll(todo));
+          todo &= ~bal(pix == kp);
+          m |= cp(p->obj_pix)[kp];
+        }
+        cmask = todo == 0ull ? m : cmask;
+      }
+      int it = 0;
+      if (!(p->flags & RT_DEV_FLAG_NO_OBJ_BATCH))
+        for (; it + kLeanBatch <= iters; it += kLeanBatch) lean_batch<F, kLeanBatch, true>(p, gp, it, tb, pacc, ws, cmask);
+      if (it < iters) sample_loop(Bool<false>{}, it);
     } else {
       sample_loop(Bool<false>{}, 0);
     }

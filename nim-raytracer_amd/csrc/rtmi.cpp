@@ -1046,10 +1046,26 @@ Plan plan_mapping(const rt_scene* s, const rt_options* o, const Mapping& mp, int
   // float64 parity mode keeps the reference's sequential sample sum (one
   // lane per pixel); float32 spreads a pixel's samples over up to 64 lanes.
   int L = 1, lg = 0;
+  // diagnostic A/B: RTMI_MAX_LANES caps the lanes per pixel (more pixels
+  // and iterations per work item)
+  static const int max_lanes = std::getenv("RTMI_MAX_LANES") ? std::atoi(std::getenv("RTMI_MAX_LANES")) : 64;
   if (o->precision == RT_FP32) {
-    while (L * 2 <= std::min(spp, 64)) {
+    while (L * 2 <= std::min(std::min(spp, 64), std::max(1, max_lanes))) {
       L *= 2;
       ++lg;
+    }
+    // analytic scenes with distant lights (k_render_fast's object-binned
+    // batches): fewer lanes per pixel, so a work item holds at least one
+    // batch of 4 iterations (C2: 64 spp -> 16 lanes, 4 pixels per wave);
+    // the pixel bins need >= 16 lanes (<= 4 pixels per wave)
+    // (the lane count does not depend on the binning / batching flags, so
+    // RT_FLAG_NO_BINNING and RT_FLAG_NO_OBJ_BATCH frames stay bit-identical:
+    // the same samples per lane, summed in the same order)
+    const unsigned sub = f32_subset(s, o);
+    const bool ob_batch = !(sub & (SUB_MESH | SUB_REFLECT | SUB_POINT)) && (sub & (SUB_SPHERE | SUB_BOX));
+    while (ob_batch && L > 16 && spp / L < 4) {
+      L /= 2;
+      --lg;
     }
   }
   const int P = 64 / L;
