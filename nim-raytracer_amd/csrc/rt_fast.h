@@ -1445,13 +1445,43 @@ __device__ __forceinline__ int list_search_batch(KP p, const int32_t* ent, int b
       ++b;
     }
   }
+#ifdef RTMI_LDS_STAGE
+  // A/B variant (DESIGN.md "LDS staging"): the 4 face records of a step
+  // staged through the wave's LDS slice — lane 16 j + w loads dword w of
+  // record j (one coalesced vector load for all four), then every lane
+  // reads each record back as a broadcast (ds_read_b128 x 4) — instead of
+  // one scalar load per record
+  __shared__ uint4 stage_lds[4][16];
+  uint4* stage = stage_lds[threadIdx.x >> 6];
+#endif
   for (int k0 = b; k0 < e; k0 += 4) {
     const RT_CONST int32_t* q = cp(ent) + k0;
     const int r[4] = {q[0], q[1], q[2], q[3]};
+#ifdef RTMI_LDS_STAGE
+    {
+      const int lane = (int)__lane_id(), j = lane >> 4, w = lane & 15;
+      const int rj = j == 0 ? r[0] : j == 1 ? r[1] : j == 2 ? r[2] : r[3];
+      const unsigned int* src = (const unsigned int*)((const char*)p->tree + (unsigned)rj);
+      ((unsigned int*)stage)[lane] = k0 + j < e ? src[w] : 0u;
+      __builtin_amdgcn_wave_barrier();
+    }
+#endif
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       if (j > 0 && k0 + j >= e) break;
+#ifdef RTMI_LDS_STAGE
+      TriRegs T;
+      {
+        const uint4 a = stage[4 * j + 0], bq = stage[4 * j + 1], c = stage[4 * j + 2], d4 = stage[4 * j + 3];
+        T.v0[0] = __uint_as_float(a.x), T.v0[1] = __uint_as_float(a.y), T.v0[2] = __uint_as_float(a.z);
+        T.id = a.w;
+        T.e2[0] = __uint_as_float(bq.x), T.e2[1] = __uint_as_float(bq.y), T.e2[2] = __uint_as_float(bq.z);
+        T.e1n[0] = __uint_as_float(c.x), T.e1n[1] = __uint_as_float(c.y), T.e1n[2] = __uint_as_float(c.z);
+        T.nn[0] = __uint_as_float(d4.x), T.nn[1] = __uint_as_float(d4.y), T.nn[2] = __uint_as_float(d4.z);
+      }
+#else
       const TriRegs T = load_tri(rec<TriFast>(p, r[j]));
+#endif
 #pragma unroll
       for (int k = 0; k < S; ++k)
         if ((fl >> k) & 1u) {

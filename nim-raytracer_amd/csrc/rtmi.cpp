@@ -1026,13 +1026,31 @@ unsigned f32_subset(const rt_scene* s, const rt_options* o) {
   return s->f32_subset | (o->aa_kind >= RT_AA_JITTERED ? SUB_STOCHASTIC : 0u);
 }
 
+// Lanes per pixel of a float32 launch (a power of two, <= 64): as many as
+// the samples fill; scenes of spheres / boxes / planes with distant lights
+// and no reflection (k_render_fast's object-binned batches) use fewer, so a
+// work item holds at least one batch of 4 iterations (C2: 64 spp -> 16 lanes,
+// 4 pixels per wave), but not fewer than 16 (the pixel bins' <= 4 pixels per
+// wave). The count does not depend on the binning / batching flags, so
+// RT_FLAG_NO_BINNING and RT_FLAG_NO_OBJ_BATCH frames stay bit-identical (the
+// same samples per lane, summed in the same order).
+int f32_lanes(const rt_scene* s, const rt_options* o, int spp) {
+  // diagnostic A/B: RTMI_MAX_LANES caps the lanes per pixel
+  static const int max_lanes = std::getenv("RTMI_MAX_LANES") ? std::atoi(std::getenv("RTMI_MAX_LANES")) : 64;
+  int L = 1;
+  while (L * 2 <= std::min(std::min(spp, 64), std::max(1, max_lanes))) L *= 2;
+  const unsigned sub = f32_subset(s, o);
+  const bool ob_batch = !(sub & (SUB_MESH | SUB_REFLECT | SUB_POINT)) && (sub & (SUB_SPHERE | SUB_BOX));
+  while (ob_batch && L > 16 && spp / L < 4) L /= 2;
+  return L;
+}
+
 // Dynamic LDS of a float32 launch: the (multi-)jittered tables, 64/L
 // pixels per wave x 2 x spp floats x 4 waves per block.
-size_t f32_table_lds(const rt_options* o) {
+size_t f32_table_lds(const rt_scene* s, const rt_options* o) {
   if (o->precision != RT_FP32 || o->aa_kind < RT_AA_MULTI_JITTERED) return 0;
   const int spp = o->grid_size * o->grid_size;
-  int L = 1;
-  while (L * 2 <= std::min(spp, 64)) L *= 2;
+  const int L = f32_lanes(s, o, spp);
   return (size_t)4 * (64 / L) * 2 * (size_t)spp * sizeof(float);
 }
 
@@ -1046,27 +1064,9 @@ Plan plan_mapping(const rt_scene* s, const rt_options* o, const Mapping& mp, int
   // float64 parity mode keeps the reference's sequential sample sum (one
   // lane per pixel); float32 spreads a pixel's samples over up to 64 lanes.
   int L = 1, lg = 0;
-  // diagnostic A/B: RTMI_MAX_LANES caps the lanes per pixel (more pixels
-  // and iterations per work item)
-  static const int max_lanes = std::getenv("RTMI_MAX_LANES") ? std::atoi(std::getenv("RTMI_MAX_LANES")) : 64;
   if (o->precision == RT_FP32) {
-    while (L * 2 <= std::min(std::min(spp, 64), std::max(1, max_lanes))) {
-      L *= 2;
-      ++lg;
-    }
-    // analytic scenes with distant lights (k_render_fast's object-binned
-    // batches): fewer lanes per pixel, so a work item holds at least one
-    // batch of 4 iterations (C2: 64 spp -> 16 lanes, 4 pixels per wave);
-    // the pixel bins need >= 16 lanes (<= 4 pixels per wave)
-    // (the lane count does not depend on the binning / batching flags, so
-    // RT_FLAG_NO_BINNING and RT_FLAG_NO_OBJ_BATCH frames stay bit-identical:
-    // the same samples per lane, summed in the same order)
-    const unsigned sub = f32_subset(s, o);
-    const bool ob_batch = !(sub & (SUB_MESH | SUB_REFLECT | SUB_POINT)) && (sub & (SUB_SPHERE | SUB_BOX));
-    while (ob_batch && L > 16 && spp / L < 4) {
-      L /= 2;
-      --lg;
-    }
+    L = f32_lanes(s, o, spp);
+    while ((1 << lg) < L) ++lg;
   }
   const int P = 64 / L;
   int tx = 1, ty = 1;
@@ -1091,7 +1091,7 @@ Plan plan_mapping(const rt_scene* s, const rt_options* o, const Mapping& mp, int
   long long cap = s->max_waves / 4;
   if (o->precision == RT_FP32) {  // work-queue kernel: launch what is resident
     const int per_cu = rtmi_render_f32_blocks_per_cu((o->flags & RT_FLAG_COUNT_TRAVERSAL) ? 1 : 0,
-                                                     f32_subset(s, o), f32_table_lds(o));
+                                                     f32_subset(s, o), f32_table_lds(s, o));
     cap = std::min<long long>(cap, (long long)per_cu * s->num_cus);
   }
   pl.blocks = (int)std::max(1LL, std::min<long long>(want, cap));
@@ -1565,7 +1565,7 @@ int fill_fast(rt_scene* s, const rt_options* o, const Mapping& mp, float* fb, Fa
   static const char* cost_dump = std::getenv("RTMI_COST_DUMP");
   const unsigned sub = f32_subset(s, o);
   *split = !(o->flags & (RT_FLAG_NO_SPLIT | RT_FLAG_COUNT_TRAVERSAL)) && !p.cost && !cost_dump && s->nlight <= 8 &&
-           rtmi_lean_f32_blocks_per_cu(sub, f32_table_lds(o)) > 0;
+           rtmi_lean_f32_blocks_per_cu(sub, f32_table_lds(s, o)) > 0;
   if ((rc = frame_records(s, o, mp, p, *split, st))) return rc;
   p.pix_info = s->fr.info.p;
   return RT_OK;
@@ -1716,7 +1716,7 @@ int launch(rt_scene* s, const rt_options* o, const Mapping& mp, float* d_out, hi
       // groups, the kernels stop at the device counts)
       int32_t* const n_heavy = s->fr.ctr.p + FC_HEAVY;
       int32_t* const n_lean = s->fr.ctr.p + FC_LEAN;
-      const size_t shmem = f32_table_lds(o);
+      const size_t shmem = f32_table_lds(s, o);
       const unsigned sub = f32_subset(s, o);
       FastParams ph = p, pl = p;
       // the general pixels: the batched kernel (k_render_gen) for scenes of
@@ -1817,7 +1817,7 @@ int launch(rt_scene* s, const rt_options* o, const Mapping& mp, float* d_out, hi
       s->last_lean_kind = 0;
       s->last_general = p.ngroups;
       s->last_batched = 0;
-      const int e = rtmi_launch_render_f32(&p, f32_subset(s, o), blocks, f32_table_lds(o), st);
+      const int e = rtmi_launch_render_f32(&p, f32_subset(s, o), blocks, f32_table_lds(s, o), st);
       if (e) return fail(RT_E_DEVICE, "render kernel launch failed: %s", hipGetErrorString((hipError_t)e));
     }
   launched:

@@ -181,3 +181,22 @@ def test_pixel_records_tilted_planes_and_bias(gpu, wall):
             fb, sb = _render(ds, p)
             assert sa == sb, (wall, bias, m)
             assert torch.equal(fa, fb), (wall, bias, m, float((fa - fb).abs().max()))
+
+
+@pytest.mark.parametrize("name", ["boxes2", "spheres_warm"])
+@pytest.mark.parametrize("m", [8, 12, 16])
+def test_object_batches_identical(gpu, name, m):
+    """Analytic scenes with distant lights (C2): the object-binned batches (4
+    samples per lane through the pixels' object masks and the shadow cells'
+    masks) render the frame and Stats of the one-sample loop
+    (RT_FLAG_NO_OBJ_BATCH) and of the unbinned kernel (RT_FLAG_NO_BINNING) —
+    the same samples per lane in the same order (16 lanes per pixel at 64 spp,
+    f32_lanes)."""
+    import torch
+    from rtmi.abi import RT_FLAG_NO_OBJ_BATCH
+    ds = DeviceScene(CASES[name]())
+    fa, sa = _render(ds, _opts(200, 120, m))
+    for flags in (RT_FLAG_NO_OBJ_BATCH, RT_FLAG_NO_BINNING, RT_FLAG_NO_BINNING | RT_FLAG_NO_OBJ_BATCH):
+        fb, sb = _render(ds, _opts(200, 120, m, flags))
+        assert sa == sb, (name, m, flags)
+        assert torch.equal(fa, fb), (name, m, flags, float((fa - fb).abs().max()))
