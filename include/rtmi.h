@@ -212,6 +212,12 @@ typedef struct rt_options {
  * loops (and a 64-spp frame uses 16 lanes per pixel to fill that batch).
  * Same image and Stats. */
 #define RT_FLAG_NO_OBJ_BATCH 0x1000u
+/* float32 kernel, scenes with reflective materials: trace each reflected ray
+ * in the lane of its camera sample, one level after another. By default the
+ * reflected rays are queued per wave and traced in full 64-ray passes (the
+ * image differs by float rounding only: the pixel's deeper levels are summed
+ * in 32.32 fixed point; the Stats are the same). */
+#define RT_FLAG_NO_COMPACT 0x2000u
 
 /* Stats (src/renderer/stats.nim:4-13) plus ray counts for Mray/s. */
 typedef struct rt_stats {
@@ -464,7 +470,8 @@ int rt_scene_last_batch(rt_scene *scene, int64_t *batched_groups, int64_t *fallb
  * one-plane lean kernel, RT_FLAG_NO_LEAN1), bits 2-3 the general pixels'
  * (0 the one-sample kernel, 1 the general batched kernel, 2 the one-plane
  * batched kernel, RT_FLAG_NO_GEN1); 3 in both: the merged one-plane kernel
- * (RT_FLAG_NO_MIX). Host-side bookkeeping, no wait. */
+ * (RT_FLAG_NO_MIX); bit 4: reflected rays compacted per wave (reflective
+ * scenes, RT_FLAG_NO_COMPACT). Host-side bookkeeping, no wait. */
 int rt_scene_last_lean_kernel(rt_scene *scene, int32_t *kind);
 
 /* ---- helpers ----------------------------------------------------------- */

@@ -261,7 +261,17 @@ struct FastParams {
   // nullptr (the lists' lengths are ngroups / ngroups2, items of the kernel)
   const int32_t* list_n;
   const int32_t* list_n2;
+  // reflection-ray compaction (k_render_wave): per-wave ray queues
+  // (kReflQueue entries x kReflFields floats, field-major) and the
+  // call's secondary radiance, 32.32 fixed point per pixel channel, indexed
+  // (out_row * width + x) * 3 + c - sec_base * 3; nullptr: no compaction
+  float* rq;
+  long long* sec;
+  int64_t sec_base;
 };
+// reflection queue of a k_render_wave wave: up to 63 rays left over plus a
+// pass's 64 new ones; fields ro xyz, rd xyz, weight, dst * 16 + depth
+constexpr int kReflQueue = 128, kReflFields = 8;
 
 enum : int32_t {
   STAT_PRIMARY = 0, STAT_TESTS = 1, STAT_HITS = 2, STAT_SHADOW = 3, STAT_REFL = 4,
@@ -286,6 +296,9 @@ constexpr int kLeanRun = 4;
 // Launchers implemented by the precision-specific translation units.
 extern "C" {
 int rtmi_launch_render_f32(const rtmi::FastParams* p, unsigned subset, int blocks, size_t shmem, void* stream);
+int rtmi_launch_wave_f32(const rtmi::FastParams* p, unsigned subset, int blocks, size_t shmem, void* stream);
+int rtmi_wave_f32_blocks_per_cu(unsigned subset, size_t shmem);
+int rtmi_launch_sec_add(float* fb, const long long* sec, size_t n, float scale, int num_cus, void* stream);
 int rtmi_launch_render_f64(const rtmi::RenderParams<double>* p, int blocks, void* stream);
 int rtmi_render_f32_blocks_per_cu(int count, unsigned subset, size_t shmem);
 int rtmi_launch_lean_f32(const rtmi::FastParams* p, unsigned subset, int blocks, size_t shmem, void* stream);

@@ -731,16 +731,137 @@ __device__ __forceinline__ F3 lds_get3(LdsF* ls, int slot) {
   return f3(q[(slot + 0) * 64], q[(slot + 1) * 64], q[(slot + 2) * 64]);
 }
 
-// One camera sample: trace + shade (renderer.nim:71-127), reflections as a
-// loop of levels with forward weights; radiance is added into `acc`.
+// One shading level of renderer.nim's shade (renderer.nim:71-127 at one
+// recursion depth) for the wave's `act` lanes, at forward weight w:
 //  * renderer.nim:94-101: one shadow ray per light from hitW + N*bias; the
 //    light's shadeDiffuse term (shader.nim:12-17) is added when it misses.
 //  * renderer.nim:104-124: reflection > 0 and depth <= maxRayDepth traces
 //    r = i - 2 (n.i) n from hitW + r*bias; the level's local light is
 //    weighted (1 - reflection), the reflected colour reflection.
+// v: the level's radiance of this lane (background x w on a miss, the
+// weighted local light on a hit); reflect / refl: whether the lane reflects
+// (its reflected ray parked in LDS at LDS_RO / LDS_RD) and the hit's
+// Material.reflection (0 without a hit).
 // pix: the sample's pixel index (y * width + x) for the camera ray's bins;
 // pinfo: the wave's pixel record (FastParams.pix_info) when the wave holds
 // one pixel, else kPixCount (nothing known).
+template <bool COUNT, unsigned F, bool LEAN = false>
+__device__ __forceinline__ void shade_level(KP& p, F3 o, F3 d, bool act, int lev, int depth, float w, int pix,
+                                            unsigned pinfo, LdsF* ls, F3& v, bool& reflect, float& refl_out,
+                                            Stats32& ws) {
+  v = f3(0.0f, 0.0f, 0.0f);
+  const Hit hit = trace<COUNT, F>(p, o, d, finf(), act, false, lev == 0 ? pix : -1, -1, ws,
+                                  lev == 0 && (LEAN || (pinfo & kPixCount) == 0u));
+  if (act && hit.obj < 0) v = f3(mul_nc(w, p->bg[0]), mul_nc(w, p->bg[1]), mul_nc(w, p->bg[2]));
+  const bool lit = act && hit.obj >= 0;
+  const F3 hw = f3(__builtin_fmaf(d.x, hit.t, o.x), __builtin_fmaf(d.y, hit.t, o.y), __builtin_fmaf(d.z, hit.t, o.z));
+  F3 N = f3(0.0f, 0.0f, 0.0f);
+  F3 alb = f3(0.0f, 0.0f, 0.0f);
+  float refl = 0.0f;
+  unsigned long long pending = bal(lit);
+  while (pending) {  // one pass per distinct object hit by the wave
+    const int lead = (int)__builtin_ctzll(pending);
+    const int oi = __builtin_amdgcn_readlane(hit.obj, lead);
+    // `mine` compares against an opaque copy: knowing hit.obj == oi inside
+    // the branch, the compiler would otherwise address the object's
+    // uniform records through the per-lane hit.obj (vector loads on the
+    // sample's critical path instead of scalar loads)
+    int oi_cmp = oi;
+    asm volatile("" : "+s"(oi_cmp));
+    const bool mine = lit && hit.obj == oi_cmp;
+    pending &= ~bal(mine);
+    const FObj ob = at(p->objs, oi);
+    const RT_CONST FObjX& ox = at(p->objx, oi);
+    const F3 oalb = f3(ox.albedo_pi[0], ox.albedo_pi[1], ox.albedo_pi[2]);
+    const float orefl = ox.refl;
+    const int nbase = ox.normal_base;
+    if (mine) {
+      F3 n;
+      if ((F & F_MESH) && ob.type == GEOM_MESH) {
+        const float* fn = p->normals + 3 * (size_t)(nbase + hit.tri);
+        n = f3(fn[0], fn[1], fn[2]);
+      } else {
+        F3 ho, unused;
+        to_object<F>(p, ob, oi, hw, f3(0.0f, 0.0f, 0.0f), ho, unused);
+        n = analytic_normal<F>(ob, ho);
+      }
+      if ((F & F_XF_GENERAL) && ob.xf == XF_GENERAL) {  // object_to_world * n, not re-normalised
+        const float* m = ox.o2w;
+        N = f3(__builtin_fmaf(m[0], n.x, __builtin_fmaf(m[3], n.y, m[6] * n.z)),
+               __builtin_fmaf(m[1], n.x, __builtin_fmaf(m[4], n.y, m[7] * n.z)),
+               __builtin_fmaf(m[2], n.x, __builtin_fmaf(m[5], n.y, m[8] * n.z)));
+      } else {
+        N = n;
+      }
+      alb = oalb;
+      refl = orefl;
+    }
+  }
+  reflect = (F & F_REFLECT) && lit && refl > 0.0f && depth <= p->max_depth;
+  refl_out = refl;
+  const float wl = reflect ? w * (1.0f - refl) : w;
+  // albedo/pi * weight waits in LDS across the light loop (the loop's
+  // register peak sits inside the shadow traversal); the lights' terms
+  // are summed into E first (irr_add)
+  lds_put3(ls, LDS_ALB, f3(alb.x * wl, alb.y * wl, alb.z * wl));
+  F3 E = f3(0.0f, 0.0f, 0.0f);
+  if (F & F_REFLECT) ws.v[STAT_REFL] += pc(bal(reflect));
+  if ((F & F_REFLECT) && bal(reflect)) {  // park the reflected ray (renderer.nim:109-118)
+    if (reflect) {
+      const float ndi = 2.0f * dot3(N, d);
+      const F3 rd = f3(d.x - N.x * ndi, d.y - N.y * ndi, d.z - N.z * ndi);
+      lds_put3(ls, LDS_RO, f3(__builtin_fmaf(rd.x, p->bias, hw.x), __builtin_fmaf(rd.y, p->bias, hw.y),
+                              __builtin_fmaf(rd.z, p->bias, hw.z)));
+      lds_put3(ls, LDS_RD, rd);
+    }
+  }
+  const F3 so = f3(__builtin_fmaf(N.x, p->bias, hw.x), __builtin_fmaf(N.y, p->bias, hw.y),
+                   __builtin_fmaf(N.z, p->bias, hw.z));
+  if ((F & F_POINT) && p->has_point_light) lds_put3(ls, LDS_HW, hw);
+  // no lane shaded a hit (the sky): no shadow rays at all
+  const int nl = bal(lit) != 0ull ? p->nlight : 0;
+  // shadow skips of the wave's pixel (camera hits only): bit li set = no
+  // shadow ray to light li can meet the mesh
+  const unsigned skipw = lev == 0 ? pinfo >> 24 : 0u;
+  // two instances of the light loop: with every light's skip bit set the
+  // shadow traces are compiled without the mesh search (C3: most waves),
+  // which the register allocation and scheduling of the loop feel even
+  // when the search is skipped at run time
+  auto light_loop = [&](auto lean) {
+    constexpr bool kLean = decltype(lean)::value;
+    for (int li = 0; li < nl; ++li) {
+      if (!kLean) p = params();
+      const FLight L = at(p->lights, li);
+      F3 sd;
+      float dist, k = 1.0f;
+      if ((F & F_POINT) && L.type == LIGHT_POINT) {  // light.nim:52-62
+        const F3 h = lds_get3(ls, LDS_HW);
+        const F3 lv = f3(h.x - L.v[0], h.y - L.v[1], h.z - L.v[2]);
+        const float r2 = dot3(lv, lv);
+        const float rr = rsq(r2);
+        sd = f3(-lv.x * rr, -lv.y * rr, -lv.z * rr);
+        k = rcp(12.566370614359172f * r2);
+        dist = r2 * rr;
+      } else {  // light.nim:46-50
+        sd = f3(-L.v[0], -L.v[1], -L.v[2]);
+        dist = finf();
+      }
+      ws.v[STAT_SHADOW] += pc(bal(lit));
+      const Hit sh = trace<COUNT, F>(p, so, sd, dist, lit, true, -1, li, ws,
+                                     kLean || (li < 8 && ((skipw >> li) & 1u) != 0u));
+      if (lit && sh.obj < 0) irr_add(E, L.ci, fmaxf(dot3(N, sd), 0.0f) * k);  // shadeDiffuse (shader.nim:12-17)
+    }
+  };
+  if (LEAN || ((F & F_MESH) && nl > 0 && nl <= 8 && skipw == (1u << nl) - 1u))
+    light_loop(Bool<true>{});
+  else
+    light_loop(Bool<false>{});
+  if (lit) v = mul3(lds_get3(ls, LDS_ALB), E);
+}
+
+// One camera sample: trace + shade (renderer.nim:71-127), reflections as a
+// loop of levels with forward weights; each level's radiance is added into
+// `acc` in level order.
 template <bool COUNT, unsigned F, bool LEAN = false>
 __device__ __forceinline__ void shade_path(KP p, F3 o, F3 d, bool active, int pix, unsigned pinfo, LdsF* ls,
                                            Acc& acc, Stats32& ws) {
@@ -750,115 +871,11 @@ __device__ __forceinline__ void shade_path(KP p, F3 o, F3 d, bool active, int pi
   for (int lev = 0; lev < ((F & F_REFLECT) ? kMaxShadeLevels : 1); ++lev) {
     if (LEAN == 0) p = params();
     if (bal(act) == 0ull) break;
-    const Hit hit = trace<COUNT, F>(p, o, d, finf(), act, false, lev == 0 ? pix : -1, -1, ws,
-                                    lev == 0 && (LEAN || (pinfo & kPixCount) == 0u));
-    if (act && hit.obj < 0) acc_add3(acc, mul_nc(w, p->bg[0]), mul_nc(w, p->bg[1]), mul_nc(w, p->bg[2]));
-    const bool lit = act && hit.obj >= 0;
-    const F3 hw = f3(__builtin_fmaf(d.x, hit.t, o.x), __builtin_fmaf(d.y, hit.t, o.y), __builtin_fmaf(d.z, hit.t, o.z));
-    F3 N = f3(0.0f, 0.0f, 0.0f);
-    F3 alb = f3(0.0f, 0.0f, 0.0f);
-    float refl = 0.0f;
-    unsigned long long pending = bal(lit);
-    while (pending) {  // one pass per distinct object hit by the wave
-      const int lead = (int)__builtin_ctzll(pending);
-      const int oi = __builtin_amdgcn_readlane(hit.obj, lead);
-      // `mine` compares against an opaque copy: knowing hit.obj == oi inside
-      // the branch, the compiler would otherwise address the object's
-      // uniform records through the per-lane hit.obj (vector loads on the
-      // sample's critical path instead of scalar loads)
-      int oi_cmp = oi;
-      asm volatile("" : "+s"(oi_cmp));
-      const bool mine = lit && hit.obj == oi_cmp;
-      pending &= ~bal(mine);
-      const FObj ob = at(p->objs, oi);
-      const RT_CONST FObjX& ox = at(p->objx, oi);
-      const F3 oalb = f3(ox.albedo_pi[0], ox.albedo_pi[1], ox.albedo_pi[2]);
-      const float orefl = ox.refl;
-      const int nbase = ox.normal_base;
-      if (mine) {
-        F3 n;
-        if ((F & F_MESH) && ob.type == GEOM_MESH) {
-          const float* fn = p->normals + 3 * (size_t)(nbase + hit.tri);
-          n = f3(fn[0], fn[1], fn[2]);
-        } else {
-          F3 ho, unused;
-          to_object<F>(p, ob, oi, hw, f3(0.0f, 0.0f, 0.0f), ho, unused);
-          n = analytic_normal<F>(ob, ho);
-        }
-        if ((F & F_XF_GENERAL) && ob.xf == XF_GENERAL) {  // object_to_world * n, not re-normalised
-          const float* m = ox.o2w;
-          N = f3(__builtin_fmaf(m[0], n.x, __builtin_fmaf(m[3], n.y, m[6] * n.z)),
-                 __builtin_fmaf(m[1], n.x, __builtin_fmaf(m[4], n.y, m[7] * n.z)),
-                 __builtin_fmaf(m[2], n.x, __builtin_fmaf(m[5], n.y, m[8] * n.z)));
-        } else {
-          N = n;
-        }
-        alb = oalb;
-        refl = orefl;
-      }
-    }
-    const bool reflect = (F & F_REFLECT) && lit && refl > 0.0f && depth <= p->max_depth;
-    const float wl = reflect ? w * (1.0f - refl) : w;
-    // albedo/pi * weight waits in LDS across the light loop (the loop's
-    // register peak sits inside the shadow traversal); the lights' terms
-    // are summed into E first (irr_add)
-    lds_put3(ls, LDS_ALB, f3(alb.x * wl, alb.y * wl, alb.z * wl));
-    F3 E = f3(0.0f, 0.0f, 0.0f);
-    if (F & F_REFLECT) ws.v[STAT_REFL] += pc(bal(reflect));
-    if ((F & F_REFLECT) && bal(reflect)) {  // park the reflected ray (renderer.nim:109-118)
-      if (reflect) {
-        const float ndi = 2.0f * dot3(N, d);
-        const F3 rd = f3(d.x - N.x * ndi, d.y - N.y * ndi, d.z - N.z * ndi);
-        lds_put3(ls, LDS_RO, f3(__builtin_fmaf(rd.x, p->bias, hw.x), __builtin_fmaf(rd.y, p->bias, hw.y),
-                                __builtin_fmaf(rd.z, p->bias, hw.z)));
-        lds_put3(ls, LDS_RD, rd);
-      }
-    }
-    const F3 so = f3(__builtin_fmaf(N.x, p->bias, hw.x), __builtin_fmaf(N.y, p->bias, hw.y),
-                     __builtin_fmaf(N.z, p->bias, hw.z));
-    if ((F & F_POINT) && p->has_point_light) lds_put3(ls, LDS_HW, hw);
-    // no lane shaded a hit (the sky): no shadow rays at all
-    const int nl = bal(lit) != 0ull ? p->nlight : 0;
-    // shadow skips of the wave's pixel (camera hits only): bit li set = no
-    // shadow ray to light li can meet the mesh
-    const unsigned skipw = lev == 0 ? pinfo >> 24 : 0u;
-    // two instances of the light loop: with every light's skip bit set the
-    // shadow traces are compiled without the mesh search (C3: most waves),
-    // which the register allocation and scheduling of the loop feel even
-    // when the search is skipped at run time
-    auto light_loop = [&](auto lean) {
-      constexpr bool kLean = decltype(lean)::value;
-      for (int li = 0; li < nl; ++li) {
-        if (!kLean) p = params();
-        const FLight L = at(p->lights, li);
-        F3 sd;
-        float dist, k = 1.0f;
-        if ((F & F_POINT) && L.type == LIGHT_POINT) {  // light.nim:52-62
-          const F3 h = lds_get3(ls, LDS_HW);
-          const F3 lv = f3(h.x - L.v[0], h.y - L.v[1], h.z - L.v[2]);
-          const float r2 = dot3(lv, lv);
-          const float rr = rsq(r2);
-          sd = f3(-lv.x * rr, -lv.y * rr, -lv.z * rr);
-          k = rcp(12.566370614359172f * r2);
-          dist = r2 * rr;
-        } else {  // light.nim:46-50
-          sd = f3(-L.v[0], -L.v[1], -L.v[2]);
-          dist = finf();
-        }
-        ws.v[STAT_SHADOW] += pc(bal(lit));
-        const Hit sh = trace<COUNT, F>(p, so, sd, dist, lit, true, -1, li, ws,
-                                       kLean || (li < 8 && ((skipw >> li) & 1u) != 0u));
-        if (lit && sh.obj < 0) irr_add(E, L.ci, fmaxf(dot3(N, sd), 0.0f) * k);  // shadeDiffuse (shader.nim:12-17)
-      }
-    };
-    if (LEAN || ((F & F_MESH) && nl > 0 && nl <= 8 && skipw == (1u << nl) - 1u))
-      light_loop(Bool<true>{});
-    else
-      light_loop(Bool<false>{});
-    if (lit) {
-      const F3 a = mul3(lds_get3(ls, LDS_ALB), E);
-      acc_add3(acc, a.x, a.y, a.z);
-    }
+    F3 v;
+    bool reflect;
+    float refl;
+    shade_level<COUNT, F, LEAN>(p, o, d, act, lev, depth, w, pix, pinfo, ls, v, reflect, refl, ws);
+    if (act) acc_add3(acc, v.x, v.y, v.z);
     // every lane reloads (lanes that do not reflect go inactive): o and d
     // are then dead across the light loop instead of carried for them
     if ((F & F_REFLECT) && bal(reflect)) {
@@ -2353,6 +2370,210 @@ __global__ __launch_bounds__(256) RTMI_OCC void k_render_fast(const FastParams p
   const int lane = (int)__lane_id();
   flush_stats(ws, lds_tot[wib], lane);
   const int wave = (int)(blockIdx.x * (blockDim.x >> 6) + threadIdx.x / 64u);
+  if (lane < kStatSlots) p->partials[(size_t)wave * kStatSlots + lane] = lds_tot[wib][lane];
+}
+
+// Reflection rays compacted per wave (renderer.nim:104-124; scenes with
+// reflective materials). In k_render_fast a reflected ray is traced by the
+// lane that shot its camera ray, one level per loop trip, so a level runs
+// with only the wave's reflecting lanes live (spheres-reflection at 1080p:
+// 20-40 % of a level-1 wave, fewer below). Here a camera iteration shades
+// level 0 only; its reflected rays are appended (ballot + mbcnt ranks) to the
+// wave's ray queue, which lives across work items, and whenever 64 rays are
+// waiting they are shaded as one full pass — their own reflections appended
+// again — so secondary levels, and the shadow rays they shoot, run with
+// every lane live. The queue drains when the wave's work runs out.
+//
+// A queued ray's radiance belongs to a pixel the wave may have finished: it
+// is added, as 32.32 fixed point, into the call's per-pixel secondary
+// buffer (p->sec; integer sums are exact, so the frame does not depend on
+// which rays shared a pass); k_sec_add adds it to the framebuffer after the
+// kernel. A ray's level radiance is the same shade_level value as in
+// k_render_fast; the pixel's sum is grouped differently (level 0 summed in
+// float, the deeper levels in fixed point), so frames match k_render_fast's
+// to float rounding and the Stats exactly.
+//
+// The queue is in global memory (L2-resident, kReflQueue x kReflFields
+// floats per wave): in LDS its 4 KB per wave would cut the 8 resident waves
+// per SIMD of the analytic reflective kernels to 5.
+__device__ __forceinline__ long long sec_fix(float v) { return __float2ll_rn(v * 4294967296.0f); }
+__device__ __forceinline__ long long wave_sum_i64(long long v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    const unsigned lo = (unsigned)__shfl_xor((int)(unsigned)v, off);
+    const unsigned hi = (unsigned)__shfl_xor((int)(unsigned)((unsigned long long)v >> 32), off);
+    v += (long long)(((unsigned long long)hi << 32) | lo);
+  }
+  return v;
+}
+// A pass's radiance into p->sec: lanes sharing a destination pixel (high
+// spp: a pass is mostly one or two pixels' rays) are summed in the wave
+// first, one atomic per channel; scattered destinations add per lane.
+__device__ __forceinline__ void sec_add(KP p, bool act, int dst, F3 v) {
+  const long long c0 = sec_fix(v.x), c1 = sec_fix(v.y), c2 = sec_fix(v.z);
+  const bool any = act && (c0 | c1 | c2) != 0;
+  unsigned long long pend = bal(any);
+  const int lane = lane_id_fresh();
+  long long* sec = p->sec - p->sec_base * 3;
+  for (int k = 0; k < 4 && pend != 0ull; ++k) {
+    const int lead = (int)__builtin_ctzll(pend);
+    const int d0 = __builtin_amdgcn_readlane(dst, lead);
+    const bool mine = any && dst == d0;
+    const unsigned long long mm = bal(mine);
+    if (pc(mm) < 4u) break;  // scattered: per lane below
+    pend &= ~mm;
+    const long long s0 = wave_sum_i64(mine ? c0 : 0), s1 = wave_sum_i64(mine ? c1 : 0),
+                    s2 = wave_sum_i64(mine ? c2 : 0);
+    if (lane == lead) {
+      long long* q = sec + (size_t)d0 * 3;
+      atomicAdd((unsigned long long*)q + 0, (unsigned long long)s0);
+      atomicAdd((unsigned long long*)q + 1, (unsigned long long)s1);
+      atomicAdd((unsigned long long*)q + 2, (unsigned long long)s2);
+    }
+  }
+  if ((pend >> lane) & 1ull) {
+    long long* q = sec + (size_t)dst * 3;
+    atomicAdd((unsigned long long*)q + 0, (unsigned long long)c0);
+    atomicAdd((unsigned long long*)q + 1, (unsigned long long)c1);
+    atomicAdd((unsigned long long*)q + 2, (unsigned long long)c2);
+  }
+}
+// queue entries: read back with device-scope loads (they bypass the CU's
+// L1, which may hold an older copy of the slot), after the wave's stores
+// have completed (the release fence)
+__device__ __forceinline__ float rq_load(const float* q) {
+  return __uint_as_float(__hip_atomic_load((const unsigned*)q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+
+template <unsigned F>
+__global__ __launch_bounds__(256) RTMI_OCC void k_render_wave(const FastParams params_by_value) {
+  static_assert(F & F_REFLECT, "the compacting kernel serves reflective scenes");
+  (void)params_by_value;
+  KP p = params();
+  __shared__ float lds[4][kLdsSlots][64];
+  extern __shared__ float sample_lds[];
+  __shared__ unsigned long long lds_tot[4][kStatSlots];
+  const int wib = (int)(threadIdx.x >> 6);
+  LdsF* ls = (LdsF*)&lds[wib][0][__lane_id()];
+  if (__lane_id() < (unsigned)kStatSlots) lds_tot[wib][__lane_id()] = 0ull;
+  Stats32 ws;
+#pragma unroll
+  for (int k = 0; k < kStatSlots; ++k) ws.v[k] = 0u;
+  const int wave = (int)(blockIdx.x * (blockDim.x >> 6) + threadIdx.x / 64u);
+  float* const rq = p->rq + (size_t)wave * (kReflQueue * kReflFields);
+  // work queue as in k_render_fast (sharded heads, one item ahead)
+  const int shard = (int)(blockIdx.x % (unsigned int)p->shards);
+  unsigned int* head = p->queue + shard * kQueueStride;
+  int qj = 0;
+  if (__lane_id() == 0) qj = (int)atomicAdd(head, 1u);
+  qj = __builtin_amdgcn_readfirstlane(qj);
+  int qj_next = 0;
+  if (__lane_id() == 0) qj_next = (int)atomicAdd(head, 1u);
+  int g = qj * p->shards + shard;
+  const int ngroups = list_items(p->list_n, p->ngroups, 1);
+  int nflush = 0, qn = 0, it = 0, gg = 0;
+  bool have = false;
+  unsigned t_item = 0u, pinfo = kPixCount;
+  GroupPix gp{};
+  LdsF* tb = nullptr;
+  Acc pacc;
+  pacc.v = f3(0.0f, 0.0f, 0.0f);
+  auto next_item = [&]() {
+    have = g < ngroups;
+    if (!have) return;
+    p = params();
+    gg = p->order ? cp(p->order)[g] : g;
+    t_item = (unsigned)__builtin_amdgcn_s_memtime();
+    gp = group_pixel(p, gg, lane_id_fresh());
+    tb = sample_table<F>(p, gp, sample_lds, wib, p->lanes_per_px);
+    pacc.v = f3(0.0f, 0.0f, 0.0f);
+    it = 0;
+    pinfo = kPixCount;
+    if ((F & F_MESH) && p->pix_info) {
+      const unsigned long long vm = bal(gp.valid);
+      if (vm != 0ull) pinfo = at(p->pix_info, __builtin_amdgcn_readlane(gp.y * p->width + gp.x, (int)__builtin_ctzll(vm)));
+    }
+    qj = __builtin_amdgcn_readfirstlane(qj_next);
+    if (__lane_id() == 0) qj_next = (int)atomicAdd(head, 1u);
+    g = qj * p->shards + shard;
+  };
+  next_item();
+  for (;;) {
+    p = params();
+    if (have && it >= p->iters) {  // the item's camera samples are all shaded
+      finish_item(p, gp, pacc.v, p->lanes_per_px);
+      if (p->cost && lane_id_fresh() == 0) p->cost[gg] = (unsigned)__builtin_amdgcn_s_memtime() - t_item;
+      if (++nflush >= p->stat_flush) {
+        flush_stats(ws, lds_tot[wib], lane_id_fresh());
+        nflush = 0;
+      }
+      next_item();
+      continue;
+    }
+    const bool from_q = qn >= 64 || (!have && qn > 0);
+    if (!from_q && !have) break;
+    const int lane = lane_id_fresh();
+    F3 o, d;
+    bool act;
+    float w;
+    int depth, dst, lev;
+    if (from_q) {  // a pass over the newest min(qn, 64) queued rays
+      const int n = min(qn, 64);
+      qn -= n;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      act = lane < n;
+      const float* e = rq + qn + (act ? lane : 0);
+      o = f3(rq_load(e + 0 * kReflQueue), rq_load(e + 1 * kReflQueue), rq_load(e + 2 * kReflQueue));
+      d = f3(rq_load(e + 3 * kReflQueue), rq_load(e + 4 * kReflQueue), rq_load(e + 5 * kReflQueue));
+      w = rq_load(e + 6 * kReflQueue);
+      const int meta = __float_as_int(rq_load(e + 7 * kReflQueue));
+      dst = meta >> 4;
+      depth = meta & 15;
+      lev = 1;
+    } else {  // the item's next camera iteration: level 0 of its samples
+      const int s = it * p->lanes_per_px + gp.sub;
+      act = gp.valid & (s < p->spp);
+      d = camera_dir<F>(p, gp, s < p->spp ? s : 0, tb);
+      o = f3(p->cam[0], p->cam[1], p->cam[2]);
+      ws.v[STAT_PRIMARY] += pc(bal(act));
+      w = 1.0f;
+      depth = 1;
+      dst = gp.out_row * p->width + gp.x;
+      lev = 0;
+      ++it;
+    }
+    F3 v;
+    bool reflect;
+    float refl;
+    shade_level<false, F, false>(p, o, d, act, lev, depth, w, lev == 0 && act ? gp.y * p->width + gp.x : -1, pinfo,
+                                 ls, v, reflect, refl, ws);
+    p = params();
+    if (lev == 0) {
+      if (act) acc_add3(pacc, v.x, v.y, v.z);
+    } else {
+      sec_add(p, act, dst, v);
+    }
+    const unsigned long long rm = bal(reflect);
+    if (rm != 0ull) {  // append the reflected rays (parked in LDS by shade_level)
+      if (reflect) {
+        const int slot = qn + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(rm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)rm, 0u));
+        const F3 ro = lds_get3(ls, LDS_RO), rd = lds_get3(ls, LDS_RD);
+        float* e = rq + slot;
+        e[0 * kReflQueue] = ro.x;
+        e[1 * kReflQueue] = ro.y;
+        e[2 * kReflQueue] = ro.z;
+        e[3 * kReflQueue] = rd.x;
+        e[4 * kReflQueue] = rd.y;
+        e[5 * kReflQueue] = rd.z;
+        e[6 * kReflQueue] = w * refl;
+        e[7 * kReflQueue] = __int_as_float(dst * 16 + depth + 1);
+      }
+      qn += (int)pc(rm);
+    }
+  }
+  p = params();
+  const int lane = (int)__lane_id();
+  flush_stats(ws, lds_tot[wib], lane);
   if (lane < kStatSlots) p->partials[(size_t)wave * kStatSlots + lane] = lds_tot[wib][lane];
 }
 

@@ -11,9 +11,12 @@
 // float64 vertices. Each render call runs, on its own stream, in order:
 //   k_frame_bins_count   per face: its pixel rectangle, a SAT test per pixel
 //                        of the launch's rows, one atomic count per listed pixel
+//                        (faces of more than kBigFace pixels: onto the big list)
+//   k_frame_bins_big     the big faces' pixels spread over the whole grid
 //   rocprim exclusive scan of the counts -> per-pixel list offsets
 //   k_frame_bins_fill    per face again: scatter its record offset into each
 //                        listed pixel's list (the counts return to zero)
+//   k_frame_bins_big     the same for the big faces
 //   k_frame_tiles        per 64 x 4 tile of the launch: the shadow skips the
 //                        tile's pixels share (one test for the whole tile)
 //   k_frame_records      per pixel of the launch: the record (the tile's skip
@@ -65,7 +68,18 @@ struct DevBinTri {
 
 // frame counters (one small device array; cleared by k_frame_bins_count,
 // the list lengths written by k_frame_class_write)
-enum : int32_t { FC_OVERFLOW = 0, FC_HEAVY = 1, FC_LEAN = 2, FC_DONE = 3, FC_WORDS = 4 };
+// (FC_BIG: the big-face list's length, appended by k_frame_bins_count,
+// moved to FC_BIG_N and cleared by k_frame_bins_fill)
+enum : int32_t { FC_OVERFLOW = 0, FC_HEAVY = 1, FC_LEAN = 2, FC_DONE = 3, FC_BIG = 4, FC_BIG_N = 5, FC_WORDS = 6 };
+
+// Faces whose pixel rectangle holds more than kBigFace pixels are not walked
+// by their own kFaceLanes threads (a few large faces, e.g. a 576-face torus
+// filling a quarter of a 1080p frame, left a handful of threads looping over
+// thousands of pixels each: 3 ms per call); they go to a list of up to
+// kBigCap faces whose pixels the whole grid shares (k_frame_bins_big).
+constexpr int kBigFace = 64, kBigCap = 4096;
+// rect[4 * face] of a face on the big list carries this bit
+constexpr int32_t kRectBig = 1 << 30;
 
 struct BinsLaunch {
   const DevBinTri* tris;
@@ -79,6 +93,7 @@ struct BinsLaunch {
   int32_t* ent;    // list entries (TriFast byte offsets), capacity cap
   int64_t cap;
   int32_t* ctr;    // FC_* counters
+  int32_t* big;    // the big-face list (kBigCap faces)
   int64_t scan_lo, scan_n;
   int32_t pad_rec; // a valid record offset for the read-ahead padding
 };

@@ -48,13 +48,93 @@ __global__ __launch_bounds__(256) void k_frame_bins_count(const BinsLaunch a) {
 #pragma unroll
     for (int k = 0; k < 6; ++k) a.proj[6 * (size_t)i + k] = pr[k];
   }
-  if (r[0] < 0) return;
+  const int rw = r[1] - r[0] + 1, area = r[0] < 0 ? 0 : rw * (r[3] - r[2] + 1);
+  // a big face goes onto the big list (its first thread takes the slot;
+  // the face's kFaceLanes threads are adjacent lanes of one wave)
+  int slot = kBigCap;
+  if (q == 0 && area > kBigFace) slot = atomicAdd(&a.ctr[FC_BIG], 1);
+  slot = __shfl(slot, (int)(threadIdx.x & 63u) - q);
+  const bool big = slot < kBigCap;
+  if (q == 0) {
+    reinterpret_cast<int4*>(a.rect)[i] = make_int4(big ? (r[0] | kRectBig) : r[0], r[1], r[2], r[3]);
+#pragma unroll
+    for (int k = 0; k < 6; ++k) a.proj[6 * (size_t)i + k] = pr[k];
+    if (big) a.big[slot] = i;
+  }
+  if (r[0] < 0 || big) return;
   const double m = a.cam.margin;
-  const int rw = r[1] - r[0] + 1, area = rw * (r[3] - r[2] + 1);
   for (int idx = q; idx < area; idx += kFaceLanes) {
     const int y = r[2] + idx / rw, x = r[0] + idx % rw;
     if (frame_has_row(a.rows, y) && bg::tri_meets_box(pr, x - m, y - m, x + 1 + m, y + 1 + m))
       atomicAdd(&a.cnt[(size_t)y * a.cam.width + x], 1);
+  }
+}
+
+// The big faces' pixels (FILL false: counted, true: filled), spread over the
+// whole grid: each block scans the list's rectangle areas in LDS, then its
+// threads take every (gridDim * 256)-th pixel of the concatenated rectangles
+// (a binary search finds the face).
+template <bool FILL>
+__global__ __launch_bounds__(256) void k_frame_bins_big(const BinsLaunch a) {
+  __shared__ int32_t pre[kBigCap + 1];
+  __shared__ int32_t part[256];
+  const int n = min(a.ctr[FILL ? FC_BIG_N : FC_BIG], kBigCap);
+  if (n == 0) return;
+  const int t = (int)threadIdx.x;
+  // exclusive scan of the areas: 16 per thread, then the 256 partial sums
+  constexpr int kPer = kBigCap / 256;
+  int32_t loc[kPer];
+  int32_t sum = 0;
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    const int e = t * kPer + k;
+    int32_t ar = 0;
+    if (e < n) {
+      const int4 r = reinterpret_cast<const int4*>(a.rect)[a.big[e]];
+      ar = ((r.x & ~kRectBig) <= r.y) ? (r.y - (r.x & ~kRectBig) + 1) * (r.w - r.z + 1) : 0;
+    }
+    loc[k] = sum;
+    sum += ar;
+  }
+  part[t] = sum;
+  __syncthreads();
+  for (int off = 1; off < 256; off <<= 1) {
+    const int32_t v = t >= off ? part[t - off] : 0;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  const int32_t base = t > 0 ? part[t - 1] : 0;
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) pre[t * kPer + k] = base + loc[k];
+  if (t == 255) pre[kBigCap] = part[255];
+  __syncthreads();
+  const int32_t total = pre[kBigCap];
+  const double m = a.cam.margin;
+  for (int32_t idx = (int32_t)(blockIdx.x * 256u) + t; idx < total; idx += (int32_t)(gridDim.x * 256u)) {
+    int lo = 0, hi = n - 1;  // the last face e with pre[e] <= idx
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (pre[mid] <= idx) lo = mid;
+      else hi = mid - 1;
+    }
+    const int i = a.big[lo];
+    const int4 r = reinterpret_cast<const int4*>(a.rect)[i];
+    const int x0 = r.x & ~kRectBig, rw = r.y - x0 + 1, local = idx - pre[lo];
+    const int y = r.z + local / rw, x = x0 + local % rw;
+    if (!frame_has_row(a.rows, y)) continue;
+    double pr[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) pr[k] = a.proj[6 * (size_t)i + k];
+    if (!bg::tri_meets_box(pr, x - m, y - m, x + 1 + m, y + 1 + m)) continue;
+    const size_t pix = (size_t)y * a.cam.width + x;
+    if (!FILL) {
+      atomicAdd(&a.cnt[pix], 1);
+    } else {
+      const int64_t slot = (int64_t)a.off[pix] + atomicSub(&a.cnt[pix], 1) - 1;
+      if (slot < a.cap) a.ent[slot] = a.tris[i].rec;
+      else atomicOr(&a.ctr[FC_OVERFLOW], 1);
+    }
   }
 }
 
@@ -68,11 +148,13 @@ __global__ __launch_bounds__(256) void k_frame_bins_fill(const BinsLaunch a) {
     for (int k = 0; k < kBinPad; ++k)
       if (total + k < a.cap) a.ent[total + k] = a.pad_rec;
     if (total + kBinPad > a.cap) atomicOr(&a.ctr[FC_OVERFLOW], 1);
+    a.ctr[FC_BIG_N] = a.ctr[FC_BIG];  // the count pass's big list, for the big fill pass
+    a.ctr[FC_BIG] = 0;
   }
   const int i = t / kFaceLanes, q = t % kFaceLanes;
   if (i >= a.nf) return;
   const int4 r = reinterpret_cast<const int4*>(a.rect)[i];
-  if (r.x < 0) return;
+  if (r.x < 0 || (r.x & kRectBig)) return;  // off screen / the big fill pass's
   double pr[6];
 #pragma unroll
   for (int k = 0; k < 6; ++k) pr[k] = a.proj[6 * (size_t)i + k];
@@ -290,6 +372,10 @@ __global__ __launch_bounds__(256) void k_frame_obj_masks(const ObjMaskLaunch a) 
 }  // namespace
 }  // namespace rtmi
 
+namespace {
+constexpr int kBigBlocks = 512;  // the big-face passes' grid (their blocks exit at once on an empty list)
+}
+
 extern "C" int rtmi_frame_bins_count(const rtmi::BinsLaunch* a, void* scan_tmp, size_t* scan_tmp_bytes,
                                      void* stream) {
   hipStream_t st = (hipStream_t)stream;
@@ -301,6 +387,8 @@ extern "C" int rtmi_frame_bins_count(const rtmi::BinsLaunch* a, void* scan_tmp, 
   hipLaunchKernelGGL(rtmi::k_frame_bins_count, dim3(blocks > 0 ? blocks : 1), dim3(256), 0, st, *a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
+  hipLaunchKernelGGL(rtmi::k_frame_bins_big<false>, dim3(kBigBlocks), dim3(256), 0, st, *a);
+  if ((e = hipGetLastError()) != hipSuccess) return (int)e;
   return (int)rocprim::exclusive_scan(scan_tmp, *scan_tmp_bytes, a->cnt + a->scan_lo, a->off + a->scan_lo, 0,
                                       (size_t)a->scan_n, rocprim::plus<int32_t>(), st);
 }
@@ -308,6 +396,9 @@ extern "C" int rtmi_frame_bins_count(const rtmi::BinsLaunch* a, void* scan_tmp, 
 extern "C" int rtmi_frame_bins_fill(const rtmi::BinsLaunch* a, void* stream) {
   const int blocks = (int)(((long long)a->nf * rtmi::kFaceLanes + 255) / 256);
   hipLaunchKernelGGL(rtmi::k_frame_bins_fill, dim3(blocks > 0 ? blocks : 1), dim3(256), 0, (hipStream_t)stream, *a);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return (int)e;
+  hipLaunchKernelGGL(rtmi::k_frame_bins_big<true>, dim3(kBigBlocks), dim3(256), 0, (hipStream_t)stream, *a);
   return (int)hipGetLastError();
 }
 

@@ -1,6 +1,7 @@
 // rt_kernels_f32.hip — float (performance mode) instantiation of the render
 // kernel, plus the precision-independent helper kernels (stats reduction,
 // multi-GPU band un-interleave). Built with FMA contraction on.
+#include <algorithm>
 #include <cstdlib>
 
 #include "rt_fast.h"
@@ -53,6 +54,17 @@ __global__ __launch_bounds__(256) void k_unshard_scalar(const float* __restrict_
   for (int i = threadIdx.x; i < row_f; i += blockDim.x) fb[(size_t)y * row_f + i] = gathered[src_row * row_f + i];
 }
 
+// After k_render_wave: the framebuffer's pixels += their queued rays'
+// radiance (p->sec, 32.32 fixed point), scaled like the pixel's level-0 sum
+// (calcPixel's 1 / len, renderer.nim:159).
+__global__ __launch_bounds__(256) void k_sec_add(float* __restrict__ fb, const long long* __restrict__ sec, size_t n,
+                                                 float scale) {
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+    const long long v = sec[i];
+    if (v != 0) fb[i] += (float)((double)v * 0x1p-32) * scale;
+  }
+}
+
 // the instrumented (RT_FLAG_COUNT_TRAVERSAL) kernel: all features
 template __global__ void fast::k_render_fast<true, fast::F_ALL>(const FastParams);
 // lean pixels of one-plane scenes (rtmi.cpp lean1_ok), one or two lights
@@ -80,7 +92,9 @@ template __global__ void fast::k_render_mix1<2, 16>(const FastParams);
   extern "C" int rtmi_launch_lean_f32_part##k(unsigned, const rtmi::FastParams*, int, size_t, void*);   \
   extern "C" int rtmi_lean_f32_part_blocks_per_cu##k(unsigned, size_t);                              \
   extern "C" int rtmi_launch_gen_f32_part##k(unsigned, const rtmi::FastParams*, int, size_t, void*);    \
-  extern "C" int rtmi_gen_f32_part_blocks_per_cu##k(unsigned, size_t);
+  extern "C" int rtmi_gen_f32_part_blocks_per_cu##k(unsigned, size_t);                              \
+  extern "C" int rtmi_launch_wave_f32_part##k(unsigned, const rtmi::FastParams*, int, size_t, void*);   \
+  extern "C" int rtmi_wave_f32_part_blocks_per_cu##k(unsigned, size_t);
 RTMI_PART_DECL(0) RTMI_PART_DECL(1) RTMI_PART_DECL(2) RTMI_PART_DECL(3)
 RTMI_PART_DECL(4) RTMI_PART_DECL(5) RTMI_PART_DECL(6) RTMI_PART_DECL(7)
 RTMI_PART_DECL(8) RTMI_PART_DECL(9) RTMI_PART_DECL(10) RTMI_PART_DECL(11)
@@ -111,7 +125,34 @@ int (*const kLaunchGen[16])(unsigned, const rtmi::FastParams*, int, size_t, void
 int (*const kOccupancyGen[16])(unsigned, size_t) = {
     RTMI_GO(0), RTMI_GO(1), RTMI_GO(2),  RTMI_GO(3),  RTMI_GO(4),  RTMI_GO(5),  RTMI_GO(6),  RTMI_GO(7),
     RTMI_GO(8), RTMI_GO(9), RTMI_GO(10), RTMI_GO(11), RTMI_GO(12), RTMI_GO(13), RTMI_GO(14), RTMI_GO(15)};
+#define RTMI_LW(k) rtmi_launch_wave_f32_part##k
+#define RTMI_WO(k) rtmi_wave_f32_part_blocks_per_cu##k
+int (*const kLaunchWave[16])(unsigned, const rtmi::FastParams*, int, size_t, void*) = {
+    RTMI_LW(0), RTMI_LW(1), RTMI_LW(2),  RTMI_LW(3),  RTMI_LW(4),  RTMI_LW(5),  RTMI_LW(6),  RTMI_LW(7),
+    RTMI_LW(8), RTMI_LW(9), RTMI_LW(10), RTMI_LW(11), RTMI_LW(12), RTMI_LW(13), RTMI_LW(14), RTMI_LW(15)};
+int (*const kOccupancyWave[16])(unsigned, size_t) = {
+    RTMI_WO(0), RTMI_WO(1), RTMI_WO(2),  RTMI_WO(3),  RTMI_WO(4),  RTMI_WO(5),  RTMI_WO(6),  RTMI_WO(7),
+    RTMI_WO(8), RTMI_WO(9), RTMI_WO(10), RTMI_WO(11), RTMI_WO(12), RTMI_WO(13), RTMI_WO(14), RTMI_WO(15)};
 }  // namespace
+
+// The reflection-compacting kernel of a reflective feature subset.
+extern "C" int rtmi_launch_wave_f32(const rtmi::FastParams* p, unsigned subset, int blocks, size_t shmem,
+                                    void* stream) {
+  return kLaunchWave[(subset >> 3) & 15u](subset & 127u, p, blocks, shmem, stream);
+}
+
+// Resident blocks per CU of the reflection-compacting kernel; 0: none for the subset.
+extern "C" int rtmi_wave_f32_blocks_per_cu(unsigned subset, size_t shmem) {
+  return kOccupancyWave[(subset >> 3) & 15u](subset & 127u, shmem);
+}
+
+// fb[i] += sec[i] (32.32 fixed point) * scale where sec[i] != 0, i < n
+extern "C" int rtmi_launch_sec_add(float* fb, const long long* sec, size_t n, float scale, int num_cus, void* stream) {
+  const size_t want = (n + 255) / 256;
+  const unsigned blocks = (unsigned)std::min<size_t>(want > 0 ? want : 1, (size_t)num_cus * 16);
+  hipLaunchKernelGGL(rtmi::k_sec_add, dim3(blocks), dim3(256), 0, (hipStream_t)stream, fb, sec, n, scale);
+  return (int)hipGetLastError();
+}
 
 // The batched general-pixel kernel of a feature subset (two-class launches).
 extern "C" int rtmi_launch_gen_f32(const rtmi::FastParams* p, unsigned subset, int blocks, size_t shmem,

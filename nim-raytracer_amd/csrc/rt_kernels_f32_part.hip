@@ -84,6 +84,30 @@ int occupancy_gen_one(size_t shmem) {
   }
 }
 
+// the reflection-compacting kernel exists for the reflective subsets
+constexpr bool has_wave(unsigned i) { return (i & 32u) != 0u; }
+
+template <unsigned I>
+int launch_wave_one(const FastParams* p, int blocks, size_t shmem, void* stream) {
+  if constexpr (has_wave(I)) {
+    hipLaunchKernelGGL((f::k_render_wave<subset_mask(I)>), dim3(blocks), dim3(256), shmem, (hipStream_t)stream, *p);
+    return (int)hipGetLastError();
+  } else {
+    return (int)hipErrorInvalidDeviceFunction;
+  }
+}
+
+template <unsigned I>
+int occupancy_wave_one(size_t shmem) {
+  if constexpr (has_wave(I)) {
+    int nb = 0;
+    const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, f::k_render_wave<subset_mask(I)>, 256, shmem);
+    return e == hipSuccess && nb > 0 ? nb : 1;
+  } else {
+    return 0;
+  }
+}
+
 constexpr unsigned B = RTMI_PART * 8u;
 
 }  // namespace
@@ -171,5 +195,33 @@ extern "C" int RTMI_CAT(rtmi_gen_f32_part_blocks_per_cu, RTMI_PART)(unsigned i, 
     case 5: return occupancy_gen_one<B + 5>(shmem);
     case 6: return occupancy_gen_one<B + 6>(shmem);
     default: return occupancy_gen_one<B + 7>(shmem);
+  }
+}
+
+// the reflection-compacting kernel (same subsets as k_render_fast's reflective ones)
+extern "C" int RTMI_CAT(rtmi_launch_wave_f32_part, RTMI_PART)(unsigned i, const FastParams* p, int blocks, size_t shmem,
+                                                              void* stream) {
+  switch (i & 7u) {
+    case 0: return launch_wave_one<B + 0>(p, blocks, shmem, stream);
+    case 1: return launch_wave_one<B + 1>(p, blocks, shmem, stream);
+    case 2: return launch_wave_one<B + 2>(p, blocks, shmem, stream);
+    case 3: return launch_wave_one<B + 3>(p, blocks, shmem, stream);
+    case 4: return launch_wave_one<B + 4>(p, blocks, shmem, stream);
+    case 5: return launch_wave_one<B + 5>(p, blocks, shmem, stream);
+    case 6: return launch_wave_one<B + 6>(p, blocks, shmem, stream);
+    default: return launch_wave_one<B + 7>(p, blocks, shmem, stream);
+  }
+}
+
+extern "C" int RTMI_CAT(rtmi_wave_f32_part_blocks_per_cu, RTMI_PART)(unsigned i, size_t shmem) {
+  switch (i & 7u) {
+    case 0: return occupancy_wave_one<B + 0>(shmem);
+    case 1: return occupancy_wave_one<B + 1>(shmem);
+    case 2: return occupancy_wave_one<B + 2>(shmem);
+    case 3: return occupancy_wave_one<B + 3>(shmem);
+    case 4: return occupancy_wave_one<B + 4>(shmem);
+    case 5: return occupancy_wave_one<B + 5>(shmem);
+    case 6: return occupancy_wave_one<B + 6>(shmem);
+    default: return occupancy_wave_one<B + 7>(shmem);
   }
 }

@@ -170,6 +170,8 @@ struct rt_scene {
   static constexpr size_t kQueueWords = (size_t)2 * kQueueShards * kQueueStride;
   unsigned long long* acc() const { return reinterpret_cast<unsigned long long*>(queue.p + kQueueWords); }
   DevBuf<double> f64_tables;       // float64 kernel per-lane stochastic sample tables
+  DevBuf<float> refl_queue;        // k_render_wave's per-wave ray queues
+  DevBuf<long long> refl_sec;      // k_render_wave's per-pixel secondary radiance (32.32)
   struct Order {                   // one launch mapping's measured costs -> launch order
     std::array<int64_t, 17> key;
     DevBuf<unsigned> cost;         // cycles per pixel group, written by the measuring launch
@@ -203,7 +205,7 @@ struct rt_scene {
   int64_t sat_off[8] = {};
   struct Frame {                   // per-call buffers of one image size
     int w = 0, h = 0;
-    DevBuf<int32_t> cnt, off, ent, rect, lean, heavy, ctr;
+    DevBuf<int32_t> cnt, off, ent, rect, lean, heavy, ctr, big;
     DevBuf<double> proj;
     DevBuf<uint32_t> info;
     DevBuf<unsigned long long> omask;
@@ -1246,6 +1248,7 @@ int frame_buffers(rt_scene* s, int w, int h, hipStream_t st) {
   f.sized.clear();
   if ((rc = f.cnt.alloc(npx + 1)) || (rc = f.off.alloc(npx + 1)) || (rc = f.info.alloc(npx)) ||
       (rc = f.lean.alloc(npx + 64)) || (rc = f.heavy.alloc(npx)) || (rc = f.ctr.alloc(FC_WORDS)) ||
+      (rc = f.big.alloc(kBigCap)) ||
       (rc = f.tiles.alloc((size_t)rtmi_frame_tile_bytes(w, h))))
     return rc;
   if (s->objbins && (rc = f.omask.alloc(npx))) return rc;
@@ -1294,6 +1297,7 @@ int frame_bins(rt_scene* s, const rt_options* o, const Mapping& mp, hipStream_t 
   a.ent = f.ent.p;
   a.cap = (int64_t)f.ent.n;
   a.ctr = f.ctr.p;
+  a.big = f.big.p;
   a.pad_rec = s->bin_tris[0].rec;
   const int64_t w = o->width;
   if (mp.mode == 0) {  // the scan covers the launch's rows only
@@ -1817,8 +1821,45 @@ int launch(rt_scene* s, const rt_options* o, const Mapping& mp, float* d_out, hi
       s->last_lean_kind = 0;
       s->last_general = p.ngroups;
       s->last_batched = 0;
-      const int e = rtmi_launch_render_f32(&p, f32_subset(s, o), blocks, f32_table_lds(s, o), st);
-      if (e) return fail(RT_E_DEVICE, "render kernel launch failed: %s", hipGetErrorString((hipError_t)e));
+      const unsigned sub = f32_subset(s, o);
+      const size_t shmem = f32_table_lds(s, o);
+      // reflective scenes: reflected rays compacted per wave (k_render_wave),
+      // unless RT_FLAG_NO_COMPACT, an instrumented launch or a progressive
+      // pass that fills step x step blocks (its pixels' sums are stored
+      // more than once)
+      const long long span = (long long)mp.nrows * o->width;
+      const int wbpc = (sub & SUB_REFLECT) && !(o->flags & (RT_FLAG_NO_COMPACT | RT_FLAG_COUNT_TRAVERSAL)) &&
+                               !(mp.mode == 0 && mp.step > 1) && span < (1ll << 27)
+                           ? rtmi_wave_f32_blocks_per_cu(sub, shmem)
+                           : 0;
+      if (wbpc > 0) {
+        const int wb = (int)std::max(1LL, std::min<long long>(std::min<long long>((long long)wbpc * s->num_cus,
+                                                                                  s->max_waves / 4),
+                                                              ((long long)p.ngroups + 3) / 4));
+        const size_t qfl = (size_t)wb * 4 * kReflQueue * kReflFields;
+        const size_t nsec = (size_t)span * 3;
+        if (s->refl_queue.n < qfl || s->refl_sec.n < nsec) {
+          HIP_TRY(hipStreamSynchronize(st));  // an earlier launch may still use the old buffers
+          int rc2 = s->refl_queue.n < qfl ? s->refl_queue.alloc(qfl) : RT_OK;
+          if (!rc2 && s->refl_sec.n < nsec) rc2 = s->refl_sec.alloc(nsec);
+          if (rc2) return rc2;
+        }
+        HIP_TRY(hipMemsetAsync(s->refl_sec.p, 0, nsec * sizeof(long long), st));
+        p.rq = s->refl_queue.p;
+        p.sec = s->refl_sec.p;
+        p.sec_base = mp.mode == 0 ? (int64_t)mp.y0 * o->width : 0;
+        p.shards = std::min(kQueueShards, wb);
+        int e = rtmi_launch_wave_f32(&p, sub, wb, shmem, st);
+        if (!e)
+          e = rtmi_launch_sec_add(d_out + (size_t)p.sec_base * 3, p.sec, nsec, o->aa_kind != RT_AA_NONE ? p.inv_len : 1.0f,
+                                  s->num_cus, st);
+        if (e) return fail(RT_E_DEVICE, "render kernel launch failed: %s", hipGetErrorString((hipError_t)e));
+        blocks = wb;
+        s->last_lean_kind = 16;
+      } else {
+        const int e = rtmi_launch_render_f32(&p, sub, blocks, shmem, st);
+        if (e) return fail(RT_E_DEVICE, "render kernel launch failed: %s", hipGetErrorString((hipError_t)e));
+      }
     }
   launched:
     if (measuring) HIP_TRY(hipEventRecord(measuring->measured, st));

@@ -119,6 +119,13 @@ class DeviceScene:
         check(lib().rt_scene_last_lean_kernel(self.h, C.byref(k)))
         return int(k.value) & 15
 
+    def last_compacted(self):
+        """Whether the last call traced its reflected rays in per-wave
+        compacted passes (k_render_wave; reflective scenes, RT_FLAG_NO_COMPACT)."""
+        k = C.c_int32()
+        check(lib().rt_scene_last_lean_kernel(self.h, C.byref(k)))
+        return bool(int(k.value) & 16)
+
     def last_lean_lanes(self):
         """Lanes per lean pixel of the last two-class call (4 or 16:
         k_render_lean1q / k_render_mix1; 64: one pixel per wave), 0 if none."""
