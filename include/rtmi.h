@@ -212,12 +212,14 @@ typedef struct rt_options {
  * loops (and a 64-spp frame uses 16 lanes per pixel to fill that batch).
  * Same image and Stats. */
 #define RT_FLAG_NO_OBJ_BATCH 0x1000u
-/* float32 kernel, scenes with reflective materials: trace each reflected ray
- * in the lane of its camera sample, one level after another. By default the
- * reflected rays are queued per wave and traced in full 64-ray passes (the
- * image differs by float rounding only: the pixel's deeper levels are summed
- * in 32.32 fixed point; the Stats are the same). */
-#define RT_FLAG_NO_COMPACT 0x2000u
+/* float32 kernel, scenes with reflective materials: queue the reflected rays
+ * per wave and trace them in full 64-ray passes (k_render_wave), the pixel's
+ * deeper levels summed in 32.32 fixed point — the image differs from the
+ * default by float rounding only, the Stats are the same. By default each
+ * reflected ray is traced in the lane of its camera sample, one level after
+ * another: measured faster on the scenes here, whose reflected rays stay
+ * coherent within a wave (DESIGN.md "Reflection-ray compaction"). */
+#define RT_FLAG_COMPACT 0x2000u
 
 /* Stats (src/renderer/stats.nim:4-13) plus ray counts for Mray/s. */
 typedef struct rt_stats {
@@ -471,7 +473,7 @@ int rt_scene_last_batch(rt_scene *scene, int64_t *batched_groups, int64_t *fallb
  * (0 the one-sample kernel, 1 the general batched kernel, 2 the one-plane
  * batched kernel, RT_FLAG_NO_GEN1); 3 in both: the merged one-plane kernel
  * (RT_FLAG_NO_MIX); bit 4: reflected rays compacted per wave (reflective
- * scenes, RT_FLAG_NO_COMPACT). Host-side bookkeeping, no wait. */
+ * scenes, RT_FLAG_COMPACT). Host-side bookkeeping, no wait. */
 int rt_scene_last_lean_kernel(rt_scene *scene, int32_t *kind);
 
 /* ---- helpers ----------------------------------------------------------- */

@@ -429,6 +429,74 @@ __device__ __forceinline__ float analytic_t(KP p, const FObj& ob, int i, F3 o, F
   return -finf();
 }
 
+// analytic_t for S rays against one object: the object's transform kind
+// and type are dispatched once (uniform branches) with the S rays inside
+// each case — called per ray, the dispatch and the object's record loads
+// were repeated for every ray (C2's batches: ~20 scalar instructions per ray
+// and object on the CU's busiest pipe). Same arithmetic per ray as
+// analytic_t (bit-identical t); body(k, t) consumes ray k's t at once, and a
+// scheduling barrier between rays keeps their temporaries from overlapping
+// (interleaved, the S rays' transforms spilled).
+template <unsigned F, int S, class Body>
+__device__ __forceinline__ void analytic_t_batch(KP p, const FObj& ob, int i, const F3 (&o)[S], const F3 (&d)[S],
+                                                 Body&& body) {
+#ifdef RTMI_PER_RAY_DISPATCH  // diagnostic A/B: the dispatch per ray
+#pragma unroll
+  for (int k = 0; k < S; ++k) body(k, analytic_t<F>(p, ob, i, o[k], d[k]));
+  return;
+#endif
+  auto cases = [&](auto general) {
+    constexpr bool G = decltype(general)::value;
+    auto xform = [&](int k, F3& ro, F3& rd) {
+      if constexpr (G) {
+        const RT_CONST FObjX& x = at(p->objx, i);
+        const float* m = x.w2o;
+        ro = f3(__builtin_fmaf(m[0], o[k].x, __builtin_fmaf(m[3], o[k].y, __builtin_fmaf(m[6], o[k].z, m[9]))),
+                __builtin_fmaf(m[1], o[k].x, __builtin_fmaf(m[4], o[k].y, __builtin_fmaf(m[7], o[k].z, m[10]))),
+                __builtin_fmaf(m[2], o[k].x, __builtin_fmaf(m[5], o[k].y, __builtin_fmaf(m[8], o[k].z, m[11]))));
+        rd = f3(__builtin_fmaf(m[0], d[k].x, __builtin_fmaf(m[3], d[k].y, m[6] * d[k].z)),
+                __builtin_fmaf(m[1], d[k].x, __builtin_fmaf(m[4], d[k].y, m[7] * d[k].z)),
+                __builtin_fmaf(m[2], d[k].x, __builtin_fmaf(m[5], d[k].y, m[8] * d[k].z)));
+      } else {
+        ro = f3(o[k].x + ob.t[0], o[k].y + ob.t[1], o[k].z + ob.t[2]);
+        rd = d[k];
+      }
+    };
+    if (!(F & (F_SPHERE | F_BOX)) || ob.type == GEOM_PLANE) {
+#pragma unroll
+      for (int k = 0; k < S; ++k) {
+        F3 ro, rd;
+        xform(k, ro, rd);
+        body(k, plane(ro, rd));
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    } else if ((F & F_SPHERE) && ob.type == GEOM_SPHERE) {
+#pragma unroll
+      for (int k = 0; k < S; ++k) {
+        F3 ro, rd;
+        xform(k, ro, rd);
+        body(k, sphere(ob.r, ro, rd));
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    } else if (F & F_BOX) {
+#pragma unroll
+      for (int k = 0; k < S; ++k) {
+        F3 ro, rd;
+        xform(k, ro, rd);
+        body(k, aabb(ob.lo, ob.hi, ro, f3(rcp(rd.x), rcp(rd.y), rcp(rd.z))));
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < S; ++k) body(k, -finf());
+    }
+  };
+  if ((F & F_XF_GENERAL) && ob.xf == XF_GENERAL)
+    cases(Bool<true>{});
+  else
+    cases(Bool<false>{});
+}
+
 // trace (renderer.nim:47-67): linear closest hit over the objects in order;
 // an object counts as a hit only when it beats the running minimum.
 //
@@ -892,18 +960,23 @@ __device__ __forceinline__ void shade_path(KP p, F3 o, F3 d, bool active, int pi
 #define RTMI_QUEUE_AHEAD 1
 #endif
 
-// Occupancy target: the kernel is latency-bound (serial node-fetch chains),
-// so resident waves matter more than a few spills in the outer loops.
-// 8 waves/SIMD (<= 64 VGPRs) for every feature subset except meshes combined
-// with point lights or reflection, which spill inside the traversal at 8 and
-// run at 7 (<= 72 VGPRs). C3 (mesh + plane): 8 waves 8.06 ms vs 7 waves
-// 8.38 ms (DESIGN.md "Occupancy").
+// Occupancy target (k_render_fast, k_render_wave). Fewer resident waves
+// buy registers: the instances whose loops spilled at 8 waves/SIMD run at 5
+// (<= 96 VGPRs): meshes with point lights or reflection (mesh-mix 1080p/64
+// spp: 8 -> 5 waves 4.20 -> 3.44 ms) and the analytic scenes, whose
+// object-binned batches carry 4 samples per lane (C2 0.98 -> 0.85 ms with the
+// per-object dispatch below; spheres-* unchanged). The mesh + plane instance
+// stays at RTMI_MESH_WAVES (its searches are latency-bound: round 1 measured
+// C3 8 waves 8.06 ms vs 7 waves 8.38 ms; DESIGN.md "Occupancy").
+#ifndef RTMI_MESH_WAVES
+#define RTMI_MESH_WAVES 8
+#endif
 template <unsigned F>
 constexpr unsigned waves_per_eu() {
 #ifdef RTMI_WAVES_PER_EU
   return RTMI_WAVES_PER_EU;
 #else
-  return ((F & 8u) && (F & (32u | 64u))) ? 7u : 8u;  // F_MESH && (F_POINT || F_REFLECT)
+  return ((F & F_MESH) && !(F & (F_POINT | F_REFLECT))) ? RTMI_MESH_WAVES : 5u;
 #endif
 }
 #define RTMI_OCC __attribute__((amdgpu_waves_per_eu(waves_per_eu<F>())))
@@ -1195,17 +1268,18 @@ __device__ __forceinline__ void lean_batch(KP p, const GroupPix& gp, int it0, co
       analytic_objects(body);
     }
   };
+  F3 oc[S];
+#pragma unroll
+  for (int k = 0; k < S; ++k) oc[k] = o;
   masked_objects(cmask, [&](const int i) {
     const FObj ob = at(objs, i);
-#pragma unroll
-    for (int k = 0; k < S; ++k) {
+    analytic_t_batch<F, S>(p, ob, i, oc, d, [&](int k, float t) {
       // trace's rule (t >= 0 ? t : inf) < th, as two compares (th <= inf)
-      const float t = analytic_t<F>(p, ob, i, o, d[k]);
       const bool c = t >= 0.0f && t < th[k];
       th[k] = c ? t : th[k];
       hob[k] = c ? i : hob[k];
       hitl += c ? 1u : 0u;
-    }
+    });
   });
   // shade (renderer.nim:71-127): normals per distinct object hit, the shadow
   // origins hitW + N * bias. A hit has t < inf (it beat the initial limit).
@@ -1347,13 +1421,14 @@ __device__ __forceinline__ void lean_batch(KP p, const GroupPix& gp, int it0, co
             hitl += c ? 1u : 0u;
           }
         } else {
+          F3 sdk[S];
 #pragma unroll
-          for (int k = 0; k < S; ++k) {
-            const float t = analytic_t<F>(p, ob, i, so[k], sd);
+          for (int k = 0; k < S; ++k) sdk[k] = sd;
+          analytic_t_batch<F, S>(p, ob, i, so, sdk, [&](int k, float t) {
             const bool c = t >= 0.0f && t < ts[k];
             ts[k] = c ? t : ts[k];
             hitl += c ? 1u : 0u;
-          }
+          });
         }
       });
       // unoccluded: shadeDiffuse (shader.nim:12-17)

@@ -27,9 +27,9 @@ constexpr int kFaceLanes = 4;
 // projection meets (rt_bins.cpp build_pixel_bins, the same bounds).
 __global__ __launch_bounds__(256) void k_frame_bins_count(const BinsLaunch a) {
   const int t = (int)(blockIdx.x * 256u + threadIdx.x);
-  if (t == 0) {
+  if (t == 0) {  // (not FC_BIG: other blocks append to it now; k_frame_bins_fill zeroes it)
 #pragma unroll
-    for (int k = 0; k < FC_WORDS; ++k) a.ctr[k] = 0;
+    for (int k = 0; k < FC_BIG; ++k) a.ctr[k] = 0;
   }
   const int i = t / kFaceLanes, q = t % kFaceLanes;
   if (i >= a.nf) return;

@@ -1823,12 +1823,12 @@ int launch(rt_scene* s, const rt_options* o, const Mapping& mp, float* d_out, hi
       s->last_batched = 0;
       const unsigned sub = f32_subset(s, o);
       const size_t shmem = f32_table_lds(s, o);
-      // reflective scenes: reflected rays compacted per wave (k_render_wave),
-      // unless RT_FLAG_NO_COMPACT, an instrumented launch or a progressive
+      // RT_FLAG_COMPACT, reflective scenes: reflected rays compacted per wave
+      // (k_render_wave); not for an instrumented launch or a progressive
       // pass that fills step x step blocks (its pixels' sums are stored
       // more than once)
       const long long span = (long long)mp.nrows * o->width;
-      const int wbpc = (sub & SUB_REFLECT) && !(o->flags & (RT_FLAG_NO_COMPACT | RT_FLAG_COUNT_TRAVERSAL)) &&
+      const int wbpc = (sub & SUB_REFLECT) && (o->flags & RT_FLAG_COMPACT) && !(o->flags & RT_FLAG_COUNT_TRAVERSAL) &&
                                !(mp.mode == 0 && mp.step > 1) && span < (1ll << 27)
                            ? rtmi_wave_f32_blocks_per_cu(sub, shmem)
                            : 0;

@@ -121,7 +121,7 @@ class DeviceScene:
 
     def last_compacted(self):
         """Whether the last call traced its reflected rays in per-wave
-        compacted passes (k_render_wave; reflective scenes, RT_FLAG_NO_COMPACT)."""
+        compacted passes (k_render_wave; reflective scenes with RT_FLAG_COMPACT)."""
         k = C.c_int32()
         check(lib().rt_scene_last_lean_kernel(self.h, C.byref(k)))
         return bool(int(k.value) & 16)

@@ -1,10 +1,10 @@
 """Reflection-ray compaction (k_render_wave, rt_fast.h; row n2).
 
-Reflective scenes trace their reflected rays (renderer.nim:104-124) in
-per-wave queues and full 64-ray passes; a queued ray's radiance is summed per
+With RT_FLAG_COMPACT, reflective scenes trace their reflected rays
+(renderer.nim:104-124) in per-wave queues and full 64-ray passes; a queued ray's radiance is summed per
 pixel in 32.32 fixed point and added after the kernel (k_sec_add). Checked
 here:
-  * against the one-sample level loop (RT_FLAG_NO_COMPACT): Stats identical,
+  * against the default one-sample level loop: Stats identical,
     pixels equal to float rounding (the deeper levels are grouped
     differently: <= 2e-6 relative + 1e-6);
   * determinism: the fixed-point sums do not depend on which rays shared a
@@ -21,7 +21,7 @@ import numpy as np
 import pytest
 
 from rtmi import Antialias, Options, Precision, akGrid, akNone, scenes
-from rtmi.abi import RT_FLAG_NO_COMPACT
+from rtmi.abi import RT_FLAG_COMPACT
 from rtmi.renderer import DeviceScene, band_rows, unshard_bands_device
 
 pytestmark = pytest.mark.gpu
@@ -51,11 +51,11 @@ CASES = [("spheres-reflection", 320, 240, 1), ("spheres-reflection", 160, 120, 4
 def test_compact_matches_level_loop(gpu, name, w, h, m):
     import torch
     ds = DeviceScene(scenes.SCENES[name]())
-    a, sa = _render(ds, _opts(w, h, m))
+    a, sa = _render(ds, _opts(w, h, m, RT_FLAG_COMPACT))
     assert ds.last_compacted()
-    a2, sa2 = _render(ds, _opts(w, h, m))
+    a2, sa2 = _render(ds, _opts(w, h, m, RT_FLAG_COMPACT))
     assert torch.equal(a, a2) and sa == sa2  # deterministic
-    b, sb = _render(ds, _opts(w, h, m, RT_FLAG_NO_COMPACT))
+    b, sb = _render(ds, _opts(w, h, m))
     assert not ds.last_compacted()
     assert sa == sb
     assert sa.numReflectionRays > 0
@@ -68,7 +68,7 @@ def test_compact_matches_level_loop(gpu, name, w, h, m):
 def test_compact_rows_and_bands_match_full_frame(gpu, name):
     import torch
     w, h = 173, 131
-    o = _opts(w, h, 4)
+    o = _opts(w, h, 4, RT_FLAG_COMPACT)
     ds = DeviceScene(scenes.SCENES[name]())
     full, _ = _render(ds, o)
     part, _ = _render(ds, o, 37, 90)
@@ -111,7 +111,7 @@ def _oracle_rows(scene, o, rows, bvh):
 ])
 def test_compact_oracle(gpu, name, w, h, m, rows):
     sc = scenes.SCENES[name]()
-    o = _opts(w, h, m)
+    o = _opts(w, h, m, RT_FLAG_COMPACT)
     ds = DeviceScene(sc)
     fb, st = _render(ds, o)
     assert ds.last_compacted()
