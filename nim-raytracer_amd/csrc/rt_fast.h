@@ -966,10 +966,12 @@ __device__ __forceinline__ void shade_path(KP p, F3 o, F3 d, bool active, int pi
 // spp: 8 -> 5 waves 4.20 -> 3.44 ms) and the analytic scenes, whose
 // object-binned batches carry 4 samples per lane (C2 0.98 -> 0.85 ms with the
 // per-object dispatch below; spheres-* unchanged). The mesh + plane instance
-// stays at RTMI_MESH_WAVES (its searches are latency-bound: round 1 measured
-// C3 8 waves 8.06 ms vs 7 waves 8.38 ms; DESIGN.md "Occupancy").
+// runs at RTMI_MESH_WAVES = 7 (<= 72 VGPRs; 8 / 7 / 6 waves, 1080p: bunny
+// 256 spp one-kernel 2.36 / 2.09 / 2.18 ms, bunny 4 spp 0.334 / 0.308 /
+// 0.320, two-meshes 64 spp 3.11 / 2.92 / 3.00; round 1's 8-wave choice
+// predates the pixel records and batched lean paths).
 #ifndef RTMI_MESH_WAVES
-#define RTMI_MESH_WAVES 8
+#define RTMI_MESH_WAVES 7
 #endif
 template <unsigned F>
 constexpr unsigned waves_per_eu() {
