@@ -15,7 +15,8 @@
 //   k_frame_bins_big     the big faces' pixels spread over the whole grid
 //   rocprim exclusive scan of the counts -> per-pixel list offsets
 //   k_frame_bins_fill    per face again: scatter its record offset into each
-//                        listed pixel's list (the counts return to zero)
+//                        listed pixel's list (the pixels are the count pass's
+//                        per-face bit mask; the counts return to zero)
 //   k_frame_bins_big     the same for the big faces
 //   k_frame_tiles        per 64 x 4 tile of the launch: the shadow skips the
 //                        tile's pixels share (one test for the whole tile)
@@ -94,6 +95,7 @@ struct BinsLaunch {
   int64_t cap;
   int32_t* ctr;    // FC_* counters
   int32_t* big;    // the big-face list (kBigCap faces)
+  unsigned long long* fmask;  // per face (not big): its listed pixels, bit = index in its rectangle
   int64_t scan_lo, scan_n;
   int32_t pad_rec; // a valid record offset for the read-ahead padding
 };

@@ -63,11 +63,22 @@ __global__ __launch_bounds__(256) void k_frame_bins_count(const BinsLaunch a) {
   }
   if (r[0] < 0 || big) return;
   const double m = a.cam.margin;
+  // the listed pixels as a bit mask over the rectangle (area <= kBigFace =
+  // 64 here), kept for the fill pass: it scatters without re-testing
+  unsigned long long bits = 0ull;
   for (int idx = q; idx < area; idx += kFaceLanes) {
     const int y = r[2] + idx / rw, x = r[0] + idx % rw;
-    if (frame_has_row(a.rows, y) && bg::tri_meets_box(pr, x - m, y - m, x + 1 + m, y + 1 + m))
+    if (frame_has_row(a.rows, y) && bg::tri_meets_box(pr, x - m, y - m, x + 1 + m, y + 1 + m)) {
       atomicAdd(&a.cnt[(size_t)y * a.cam.width + x], 1);
+      if (idx < 64) bits |= 1ull << idx;
+    }
   }
+#pragma unroll
+  for (int k = 1; k < kFaceLanes; k <<= 1) {
+    const unsigned lo = (unsigned)__shfl_xor((int)(unsigned)bits, k), hi = (unsigned)__shfl_xor((int)(unsigned)(bits >> 32), k);
+    bits |= ((unsigned long long)hi << 32) | lo;
+  }
+  if (q == 0) a.fmask[i] = bits;  // (unused for a face of more than 64 pixels: the fill pass tests again)
 }
 
 // The big faces' pixels (FILL false: counted, true: filled), spread over the
@@ -155,20 +166,34 @@ __global__ __launch_bounds__(256) void k_frame_bins_fill(const BinsLaunch a) {
   if (i >= a.nf) return;
   const int4 r = reinterpret_cast<const int4*>(a.rect)[i];
   if (r.x < 0 || (r.x & kRectBig)) return;  // off screen / the big fill pass's
-  double pr[6];
-#pragma unroll
-  for (int k = 0; k < 6; ++k) pr[k] = a.proj[6 * (size_t)i + k];
   const int32_t rec = a.tris[i].rec;
-  const double m = a.cam.margin;
   const int rw = r.y - r.x + 1, area = rw * (r.w - r.z + 1);
-  for (int idx = q; idx < area; idx += kFaceLanes) {
-    const int y = r.z + idx / rw, x = r.x + idx % rw;
-    if (frame_has_row(a.rows, y) && bg::tri_meets_box(pr, x - m, y - m, x + 1 + m, y + 1 + m)) {
-      const size_t pix = (size_t)y * a.cam.width + x;
-      const int64_t slot = (int64_t)a.off[pix] + atomicSub(&a.cnt[pix], 1) - 1;
-      if (slot < a.cap) a.ent[slot] = rec;
-      else atomicOr(&a.ctr[FC_OVERFLOW], 1);
+  if (area > kBigFace) {  // a big face the full big list left here: test again
+    double pr[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) pr[k] = a.proj[6 * (size_t)i + k];
+    const double m = a.cam.margin;
+    for (int idx = q; idx < area; idx += kFaceLanes) {
+      const int y = r.z + idx / rw, x = r.x + idx % rw;
+      if (frame_has_row(a.rows, y) && bg::tri_meets_box(pr, x - m, y - m, x + 1 + m, y + 1 + m)) {
+        const size_t pix = (size_t)y * a.cam.width + x;
+        const int64_t slot = (int64_t)a.off[pix] + atomicSub(&a.cnt[pix], 1) - 1;
+        if (slot < a.cap) a.ent[slot] = rec;
+        else atomicOr(&a.ctr[FC_OVERFLOW], 1);
+      }
     }
+    return;
+  }
+  // the count pass's mask: lane q takes the listed pixels idx = q mod kFaceLanes
+  unsigned long long bits = a.fmask[i] & (0x1111111111111111ull << q);
+  while (bits != 0ull) {
+    const int idx = (int)__builtin_ctzll(bits);
+    bits &= bits - 1ull;
+    const int y = r.z + idx / rw, x = r.x + idx % rw;
+    const size_t pix = (size_t)y * a.cam.width + x;
+    const int64_t slot = (int64_t)a.off[pix] + atomicSub(&a.cnt[pix], 1) - 1;
+    if (slot < a.cap) a.ent[slot] = rec;
+    else atomicOr(&a.ctr[FC_OVERFLOW], 1);
   }
 }
 

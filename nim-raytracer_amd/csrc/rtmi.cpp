@@ -208,7 +208,7 @@ struct rt_scene {
     DevBuf<int32_t> cnt, off, ent, rect, lean, heavy, ctr, big;
     DevBuf<double> proj;
     DevBuf<uint32_t> info;
-    DevBuf<unsigned long long> omask;
+    DevBuf<unsigned long long> omask, fmask;
     DevBuf<unsigned char> scan_tmp;
     DevBuf<unsigned char> tiles;   // per-tile shadow skips (k_frame_tiles)
     DevBuf<unsigned char> cls;     // the class counts' scratch (k_frame_class_count + scan)
@@ -1252,8 +1252,8 @@ int frame_buffers(rt_scene* s, int w, int h, hipStream_t st) {
       (rc = f.tiles.alloc((size_t)rtmi_frame_tile_bytes(w, h))))
     return rc;
   if (s->objbins && (rc = f.omask.alloc(npx))) return rc;
-  if (nf > 0 && (f.rect.n < 4 * nf || f.proj.n < 6 * nf)) {
-    if ((rc = f.rect.alloc(4 * nf)) || (rc = f.proj.alloc(6 * nf))) return rc;
+  if (nf > 0 && (f.rect.n < 4 * nf || f.proj.n < 6 * nf || f.fmask.n < nf)) {
+    if ((rc = f.rect.alloc(4 * nf)) || (rc = f.proj.alloc(6 * nf)) || (rc = f.fmask.alloc(nf))) return rc;
   }
   if (!f.ent.p && (rc = f.ent.alloc(1 << 16))) return rc;
   // the bin counts are zero between calls (the fill pass counts them down)
@@ -1298,6 +1298,7 @@ int frame_bins(rt_scene* s, const rt_options* o, const Mapping& mp, hipStream_t 
   a.cap = (int64_t)f.ent.n;
   a.ctr = f.ctr.p;
   a.big = f.big.p;
+  a.fmask = f.fmask.p;
   a.pad_rec = s->bin_tris[0].rec;
   const int64_t w = o->width;
   if (mp.mode == 0) {  // the scan covers the launch's rows only
