@@ -78,7 +78,10 @@ enum : int32_t { FC_OVERFLOW = 0, FC_HEAVY = 1, FC_LEAN = 2, FC_DONE = 3, FC_BIG
 // filling a quarter of a 1080p frame, left a handful of threads looping over
 // thousands of pixels each: 3 ms per call); they go to a list of up to
 // kBigCap faces whose pixels the whole grid shares (k_frame_bins_big).
-constexpr int kBigFace = 64, kBigCap = 4096;
+#ifndef RTMI_BIG_FACE
+#define RTMI_BIG_FACE 64
+#endif
+constexpr int kBigFace = RTMI_BIG_FACE, kBigCap = 4096;
 // rect[4 * face] of a face on the big list carries this bit
 constexpr int32_t kRectBig = 1 << 30;
 

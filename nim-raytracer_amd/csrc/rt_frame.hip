@@ -63,8 +63,8 @@ __global__ __launch_bounds__(256) void k_frame_bins_count(const BinsLaunch a) {
   }
   if (r[0] < 0 || big) return;
   const double m = a.cam.margin;
-  // the listed pixels as a bit mask over the rectangle (area <= kBigFace =
-  // 64 here), kept for the fill pass: it scatters without re-testing
+  // the listed pixels as a bit mask over the rectangle, kept for the fill
+  // pass: it scatters without re-testing (faces of <= 64 pixels)
   unsigned long long bits = 0ull;
   for (int idx = q; idx < area; idx += kFaceLanes) {
     const int y = r[2] + idx / rw, x = r[0] + idx % rw;
@@ -168,7 +168,7 @@ __global__ __launch_bounds__(256) void k_frame_bins_fill(const BinsLaunch a) {
   if (r.x < 0 || (r.x & kRectBig)) return;  // off screen / the big fill pass's
   const int32_t rec = a.tris[i].rec;
   const int rw = r.y - r.x + 1, area = rw * (r.w - r.z + 1);
-  if (area > kBigFace) {  // a big face the full big list left here: test again
+  if (area > 64) {  // no mask (a big face the full big list left here, or kBigFace > 64): test again
     double pr[6];
 #pragma unroll
     for (int k = 0; k < 6; ++k) pr[k] = a.proj[6 * (size_t)i + k];
