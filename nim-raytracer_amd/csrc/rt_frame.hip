@@ -270,22 +270,95 @@ __global__ __launch_bounds__(256) void k_frame_tiles(const RecordsLaunch a, int 
 // Per pixel of one tile (block (tile column, tile row)): the pixel record —
 // list length, and for an empty list the shadow skip bits (the tile's, or
 // the pixel's own test).
-__global__ __launch_bounds__(256) void k_frame_records(const RecordsLaunch a, const uint8_t* tile_bits) {
+// tile_cls (split launches in screen order, a.order == nullptr): the tile's
+// lean / general pixel counts (lean << 32 | general) for the tile-ordered
+// lists (k_frame_class_write_tiles), or nullptr.
+__device__ __forceinline__ int pixel_class(const RecordsLaunch& a, const LaunchPix& p, uint32_t info) {
+  if (!p.drawn) return 0;
+  return (info & kPixCount) == 0u && ((info >> 24) & a.full) == a.full ? 1 : 2;
+}
+__global__ __launch_bounds__(256) void k_frame_records(const RecordsLaunch a, const uint8_t* tile_bits,
+                                                       unsigned long long* tile_cls) {
   __shared__ bg::SkipGrid sg[8];
+  __shared__ unsigned long long wsum[4];
   load_skip_grids(a, sg);
   const int j = (int)blockIdx.x * kTileW + (int)(threadIdx.x & 63u);
   const int k = (int)blockIdx.y * kTileH + (int)(threadIdx.x >> 6);
   const LaunchPix p = launch_pixel(a, j, k);
-  if (!p.valid) return;
-  const size_t pix = (size_t)p.y * a.width + p.x;
-  const int32_t n = a.off[pix + 1] - a.off[pix];
-  uint32_t info = n < (int32_t)kPixCount ? (uint32_t)n : kPixCount;
-  if (n == 0 && a.have != 0u) {
-    const bool tile = tile_bits[blockIdx.y * gridDim.x + blockIdx.x] != 0;
-    const unsigned bits = tile ? a.have : bg::pixel_skip_bits(a.cam, a.planes, a.nplanes, sg, a.nl, a.have, p.x, p.y);
-    info |= bits << 24;
+  int c = 0;
+  if (p.valid) {
+    const size_t pix = (size_t)p.y * a.width + p.x;
+    const int32_t n = a.off[pix + 1] - a.off[pix];
+    uint32_t info = n < (int32_t)kPixCount ? (uint32_t)n : kPixCount;
+    if (n == 0 && a.have != 0u) {
+      const bool tile = tile_bits[blockIdx.y * gridDim.x + blockIdx.x] != 0;
+      const unsigned bits = tile ? a.have : bg::pixel_skip_bits(a.cam, a.planes, a.nplanes, sg, a.nl, a.have, p.x, p.y);
+      info |= bits << 24;
+    }
+    a.info[pix] = info;
+    c = pixel_class(a, p, info);
   }
-  a.info[pix] = info;
+  if (!tile_cls) return;
+  const unsigned long long ml = __ballot(c == 1), mh = __ballot(c == 2);
+  if ((threadIdx.x & 63u) == 0) wsum[threadIdx.x >> 6] = ((unsigned long long)__popcll(ml) << 32) | __popcll(mh);
+  __syncthreads();
+  if (threadIdx.x == 0) tile_cls[blockIdx.y * gridDim.x + blockIdx.x] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+}
+
+// Exclusive scan of n packed counts by one block (n = the launch's tiles:
+// 8,100 at 1080p; rocPRIM's scan took two launches, ~10 us).
+__global__ __launch_bounds__(1024) void k_scan_tiles(const unsigned long long* __restrict__ in,
+                                                     unsigned long long* __restrict__ out, int n) {
+  __shared__ unsigned long long part[1024];
+  const int t = (int)threadIdx.x, per = (n + 1023) / 1024, b = t * per;
+  unsigned long long sum = 0ull;
+  for (int i = b; i < min(n, b + per); ++i) sum += in[i];
+  part[t] = sum;
+  __syncthreads();
+  for (int off = 1; off < 1024; off <<= 1) {
+    const unsigned long long v = t >= off ? part[t - off] : 0ull;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  unsigned long long run = t > 0 ? part[t - 1] : 0ull;
+  for (int i = b; i < min(n, b + per); ++i) {
+    const unsigned long long v = in[i];
+    out[i] = run;
+    run += v;
+  }
+}
+
+// The lean / general lists in tile order (the records kernel's tiles, its
+// counts scanned): each tile's groups at its offsets, wave ballots + mbcnt
+// ranks; the last tile writes the lengths and the lean list's -1 padding.
+__global__ __launch_bounds__(256) void k_frame_class_write_tiles(const RecordsLaunch a,
+                                                                 const unsigned long long* tile_cls,
+                                                                 const unsigned long long* tile_off) {
+  __shared__ unsigned long long wsum[4];
+  const int j = (int)blockIdx.x * kTileW + (int)(threadIdx.x & 63u);
+  const int k = (int)blockIdx.y * kTileH + (int)(threadIdx.x >> 6);
+  const LaunchPix p = launch_pixel(a, j, k);
+  const int c = p.valid ? pixel_class(a, p, a.info[(size_t)p.y * a.width + p.x]) : 0;
+  const unsigned long long ml = __ballot(c == 1), mh = __ballot(c == 2);
+  const int w = (int)(threadIdx.x >> 6);
+  if ((threadIdx.x & 63u) == 0) wsum[w] = ((unsigned long long)__popcll(ml) << 32) | __popcll(mh);
+  __syncthreads();
+  const int tile = (int)(blockIdx.y * gridDim.x + blockIdx.x);
+  unsigned long long base = tile_off[tile];
+  for (int i = 0; i < w; ++i) base += wsum[i];
+  const int g = k * a.ncols + j;
+  if (c == 1) a.lean[(int)(base >> 32) + (int)lane_rank(ml)] = g;
+  if (c == 2) a.heavy[(int)(base & 0xffffffffu) + (int)lane_rank(mh)] = g;
+  if (tile != (int)(gridDim.x * gridDim.y) - 1) return;
+  const unsigned long long tot = tile_off[tile] + tile_cls[tile];
+  const int nl = (int)(tot >> 32), nh = (int)(tot & 0xffffffffu);
+  if (threadIdx.x == 0) {
+    a.ctr[FC_LEAN] = nl;
+    a.ctr[FC_HEAVY] = nh;
+  }
+  const int end = nl == 0 ? 64 : (nl + 63) / 64 * 64;
+  for (int e = nl + (int)threadIdx.x; e < end; e += 256) a.lean[e] = -1;
 }
 
 // The class of the gi-th group of the launch order (order, or screen order):
@@ -439,20 +512,34 @@ extern "C" int rtmi_frame_records(const rtmi::RecordsLaunch* a, void* tile_bits,
                                          (unsigned long long*)nullptr, 0ull, (size_t)nblk,
                                          rocprim::plus<unsigned long long>(), st);
   if (e != hipSuccess) return (int)e;
-  if (!scratch) {
-    *scratch_bytes = 2 * cnt_bytes + scan_bytes;
-    return 0;
-  }
-  if (*scratch_bytes < 2 * cnt_bytes + scan_bytes) return (int)hipErrorInvalidValue;
   const int tiles_x = (a->ncols + kTileW - 1) / kTileW, tiles_y = (a->nrows + kTileH - 1) / kTileH;
   const int ntiles = tiles_x * tiles_y;
+  const size_t tile_bytes = ((size_t)std::max(ntiles, 1) * sizeof(unsigned long long) + 255) / 256 * 256;
+  if (!scratch) {
+    *scratch_bytes = std::max(2 * cnt_bytes + scan_bytes, 2 * tile_bytes);
+    return 0;
+  }
+  if (*scratch_bytes < 2 * cnt_bytes + scan_bytes && !(a->split && !a->order)) return (int)hipErrorInvalidValue;
   if (ntiles <= 0) return 0;
   if (a->have != 0u) {
     hipLaunchKernelGGL(k_frame_tiles, dim3((ntiles + 255) / 256), dim3(256), 0, st, *a, tiles_x, ntiles,
                        (uint8_t*)tile_bits);
     if ((e = hipGetLastError()) != hipSuccess) return (int)e;
   }
-  hipLaunchKernelGGL(k_frame_records, dim3(tiles_x, tiles_y), dim3(256), 0, st, *a, (const uint8_t*)tile_bits);
+  if (a->split && !a->order) {  // tile-ordered lists: counts from the records kernel, one-block scan
+    if (*scratch_bytes < 2 * tile_bytes) return (int)hipErrorInvalidValue;
+    unsigned long long* tc = (unsigned long long*)scratch;
+    unsigned long long* to = (unsigned long long*)((char*)scratch + tile_bytes);
+    hipLaunchKernelGGL(k_frame_records, dim3(tiles_x, tiles_y), dim3(256), 0, st, *a, (const uint8_t*)tile_bits, tc);
+    if ((e = hipGetLastError()) != hipSuccess) return (int)e;
+    hipLaunchKernelGGL(k_scan_tiles, dim3(1), dim3(1024), 0, st, (const unsigned long long*)tc, to, ntiles);
+    if ((e = hipGetLastError()) != hipSuccess) return (int)e;
+    hipLaunchKernelGGL(k_frame_class_write_tiles, dim3(tiles_x, tiles_y), dim3(256), 0, st, *a,
+                       (const unsigned long long*)tc, (const unsigned long long*)to);
+    return (int)hipGetLastError();
+  }
+  hipLaunchKernelGGL(k_frame_records, dim3(tiles_x, tiles_y), dim3(256), 0, st, *a, (const uint8_t*)tile_bits,
+                     (unsigned long long*)nullptr);
   if ((e = hipGetLastError()) != hipSuccess || !a->split) return (int)e;
   unsigned long long* blk = (unsigned long long*)scratch;
   unsigned long long* blk_off = (unsigned long long*)((char*)scratch + cnt_bytes);
