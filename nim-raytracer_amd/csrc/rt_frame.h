@@ -138,7 +138,9 @@ struct ObjMaskLaunch {
   double cam_a, cam_c, margin;
   FrameRows rows;
   unsigned long long* masks;  // per pixel
+  int32_t* rects;             // scratch: 4 x 64 rectangle ints, then the 64-bit always mask (kObjRectInts)
 };
+constexpr int kObjRectInts = 4 * 64 + 2;
 
 }  // namespace rtmi
 

@@ -416,13 +416,13 @@ __global__ __launch_bounds__(256) void k_frame_class_write(const RecordsLaunch a
   for (int e = nl + (int)threadIdx.x; e < end; e += 256) a.lean[e] = -1;
 }
 
-// Object masks (rt_bins.cpp build_object_pixel_masks): each block projects
-// every object's world box once into LDS, then its threads walk the launch's
-// pixels.
-__global__ __launch_bounds__(256) void k_frame_obj_masks(const ObjMaskLaunch a) {
-  __shared__ int rect[64][4];
-  __shared__ int alw[64];
+// Object masks (rt_bins.cpp build_object_pixel_masks). k_frame_obj_rects
+// (one wave) projects every object's world box once: its pixel rectangle
+// (x0, x1, y0, y1; -1s: off screen) into rects[4 i ..], and after them the
+// mask of the objects with no bounded projection (in every pixel's mask).
+__global__ __launch_bounds__(64) void k_frame_obj_rects(const ObjMaskLaunch a) {
   const int t = (int)threadIdx.x;
+  bool alw = false;
   if (t < a.nobj) {
     const DevObjBox& b = a.objs[t];
     bool proj = !b.always;
@@ -442,29 +442,40 @@ __global__ __launch_bounds__(256) void k_frame_obj_masks(const ObjMaskLaunch a) 
       ymin = bg::dmin(ymin, py);
       ymax = bg::dmax(ymax, py);
     }
-    alw[t] = proj ? 0 : 1;
-    rect[t][0] = rect[t][1] = rect[t][2] = rect[t][3] = -1;
+    alw = !proj;
+    int4 r = make_int4(-1, -1, -1, -1);
     const double m = a.margin;
-    if (proj && xmax + m >= 0.0 && ymax + m >= 0.0 && xmin - m < a.width && ymin - m < a.height) {
-      rect[t][0] = (int)bg::dmax(0.0, floor(xmin - m));
-      rect[t][1] = (int)bg::dmin((double)a.width - 1, floor(xmax + m));
-      rect[t][2] = (int)bg::dmax(0.0, floor(ymin - m));
-      rect[t][3] = (int)bg::dmin((double)a.height - 1, floor(ymax + m));
-    }
+    if (proj && xmax + m >= 0.0 && ymax + m >= 0.0 && xmin - m < a.width && ymin - m < a.height)
+      r = make_int4((int)bg::dmax(0.0, floor(xmin - m)), (int)bg::dmin((double)a.width - 1, floor(xmax + m)),
+                    (int)bg::dmax(0.0, floor(ymin - m)), (int)bg::dmin((double)a.height - 1, floor(ymax + m)));
+    reinterpret_cast<int4*>(a.rects)[t] = r;
   }
-  __syncthreads();
-  unsigned long long always = 0ull;
-  for (int i = 0; i < a.nobj; ++i) always |= alw[i] ? 1ull << i : 0ull;
-  const long long total = (long long)a.rows.nrows * a.width;
-  for (long long idx = (long long)blockIdx.x * 256 + t; idx < total; idx += (long long)gridDim.x * 256) {
-    const int k = (int)(idx / a.width), x = (int)(idx - (long long)k * a.width);
-    const int y = frame_row(a.rows, k);
-    if (y < 0) continue;
-    unsigned long long mk = always;
-    for (int i = 0; i < a.nobj; ++i)
-      if (rect[i][0] >= 0 && x >= rect[i][0] && x <= rect[i][1] && y >= rect[i][2] && y <= rect[i][3]) mk |= 1ull << i;
-    a.masks[(size_t)y * a.width + x] = mk;
+  const unsigned long long am = __ballot(alw);
+  if (t == 0) *reinterpret_cast<unsigned long long*>(a.rects + 4 * 64) = am;
+}
+
+// Per pixel of one launch row segment (block (segment, launch row)): the
+// row's objects once per block (a uniform loop over the rectangles), then
+// each pixel's x tests against them.
+__global__ __launch_bounds__(256) void k_frame_obj_masks(const ObjMaskLaunch a) {
+  const int y = frame_row(a.rows, (int)blockIdx.y);
+  if (y < 0) return;
+  const int4* __restrict__ rects = (const int4*)a.rects;
+  unsigned long long row = 0ull;
+  for (int i = 0; i < a.nobj; ++i) {
+    const int4 r = rects[i];
+    row |= (r.x >= 0 && y >= r.z && y <= r.w) ? 1ull << i : 0ull;
   }
+  const int x = (int)(blockIdx.x * 256u + threadIdx.x);
+  if (x >= a.width) return;
+  unsigned long long mk = *(const unsigned long long*)(a.rects + 4 * 64);
+  while (row != 0ull) {
+    const int i = (int)__builtin_ctzll(row);
+    row &= row - 1ull;
+    const int4 r = rects[i];
+    mk |= (x >= r.x && x <= r.y) ? 1ull << i : 0ull;
+  }
+  a.masks[(size_t)y * a.width + x] = mk;
 }
 
 }  // namespace
@@ -561,10 +572,11 @@ extern "C" long long rtmi_frame_tile_bytes(int ncols, int nrows) {
 }
 
 extern "C" int rtmi_frame_obj_masks(const rtmi::ObjMaskLaunch* a, void* stream) {
-  if (a->nobj > 64) return (int)hipErrorInvalidValue;
-  const long long total = (long long)a->rows.nrows * a->width;
-  const long long blocks = std::min<long long>(2048, (total + 255) / 256);
-  hipLaunchKernelGGL(rtmi::k_frame_obj_masks, dim3((unsigned)(blocks > 0 ? blocks : 1)), dim3(256), 0,
-                     (hipStream_t)stream, *a);
+  if (a->nobj > 64 || a->rows.nrows <= 0 || a->width <= 0) return a->nobj > 64 ? (int)hipErrorInvalidValue : 0;
+  hipLaunchKernelGGL(rtmi::k_frame_obj_rects, dim3(1), dim3(64), 0, (hipStream_t)stream, *a);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return (int)e;
+  hipLaunchKernelGGL(rtmi::k_frame_obj_masks, dim3((unsigned)((a->width + 255) / 256), (unsigned)a->rows.nrows), dim3(256),
+                     0, (hipStream_t)stream, *a);
   return (int)hipGetLastError();
 }

@@ -205,7 +205,7 @@ struct rt_scene {
   int64_t sat_off[8] = {};
   struct Frame {                   // per-call buffers of one image size
     int w = 0, h = 0;
-    DevBuf<int32_t> cnt, off, ent, rect, lean, heavy, ctr, big;
+    DevBuf<int32_t> cnt, off, ent, rect, lean, heavy, ctr, big, orect;
     DevBuf<double> proj;
     DevBuf<uint32_t> info;
     DevBuf<unsigned long long> omask, fmask;
@@ -1251,7 +1251,7 @@ int frame_buffers(rt_scene* s, int w, int h, hipStream_t st) {
       (rc = f.big.alloc(kBigCap)) ||
       (rc = f.tiles.alloc((size_t)rtmi_frame_tile_bytes(w, h))))
     return rc;
-  if (s->objbins && (rc = f.omask.alloc(npx))) return rc;
+  if (s->objbins && ((rc = f.omask.alloc(npx)) || (rc = f.orect.alloc(kObjRectInts)))) return rc;
   if (nf > 0 && (f.rect.n < 4 * nf || f.proj.n < 6 * nf || f.fmask.n < nf)) {
     if ((rc = f.rect.alloc(4 * nf)) || (rc = f.proj.alloc(6 * nf)) || (rc = f.fmask.alloc(nf))) return rc;
   }
@@ -1413,6 +1413,7 @@ int frame_obj_masks(rt_scene* s, const rt_options* o, const Mapping& mp, hipStre
   a.margin = kPixelMargin;
   a.rows = frame_rows(mp, o->height);
   a.masks = s->fr.omask.p;
+  a.rects = s->fr.orect.p;
   const int e = rtmi_frame_obj_masks(&a, st);
   if (e) return fail(RT_E_DEVICE, "object mask launch failed: %s", hipGetErrorString((hipError_t)e));
   *ok = true;
