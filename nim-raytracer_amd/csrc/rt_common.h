@@ -287,6 +287,13 @@ enum : unsigned {
 };
 // float32 kernel work queue: 64 head words, 128 B apart, zeroed per launch
 constexpr int kQueueShards = 64, kQueueStride = 32;
+// object-binned batches (k_render_fast, analytic scenes with distant lights,
+// no reflection): samples per lane of one batch (rt_fast.h lean_batch<F, S,
+// true>); the host's lane count gives a work item at least one batch
+#ifndef RTMI_OBJ_BATCH
+#define RTMI_OBJ_BATCH 4
+#endif
+constexpr int kObjBatch = RTMI_OBJ_BATCH;
 // k_render_lean work item: a run of this many lean-list entries (the list
 // padded with -1 to a whole number of runs), fetched with one scalar load
 constexpr int kLeanRun = 4;

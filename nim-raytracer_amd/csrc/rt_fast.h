@@ -2399,15 +2399,15 @@ __global__ __launch_bounds__(256) RTMI_OCC void k_render_fast(const FastParams p
       if (it < iters) sample_loop(Bool<true>{}, it);
     } else if constexpr (!(F & (F_MESH | F_REFLECT | F_POINT)) && (F & (F_SPHERE | F_BOX)) != 0) {
       // analytic scenes with distant lights (C2): object-binned batches —
-      // kLeanBatch samples per lane through the wave's pixels' object masks
+      // kObjBatch samples per lane through the wave's pixels' object masks
       // and the shadow rays' light-grid cell masks, so each object visit's
       // scalar work (record load, dispatch, loop control) serves 64 x
-      // kLeanBatch rays; the remaining iterations one sample at a time
+      // kObjBatch rays; the remaining iterations one sample at a time
       unsigned long long cmask = p->nobj >= 64 ? ~0ull : ((1ull << p->nobj) - 1ull);
       if (p->obj_pix) {
         const int pix = gp.valid ? gp.y * p->width + gp.x : -1;
         unsigned long long todo = bal(pix >= 0), m = 0ull;
-        for (int k = 0; k < 4 && todo != 0ull; ++k) {
+        for (int k = 0; k < 8 && todo != 0ull; ++k) {
           const int kp = __builtin_amdgcn_readlane(pix, (int)__builtin_ctzll(todo));
           todo &= ~bal(pix == kp);
           m |= cp(p->obj_pix)[kp];
@@ -2416,7 +2416,7 @@ __global__ __launch_bounds__(256) RTMI_OCC void k_render_fast(const FastParams p
       }
       int it = 0;
       if (!(p->flags & RT_DEV_FLAG_NO_OBJ_BATCH))
-        for (; it + kLeanBatch <= iters; it += kLeanBatch) lean_batch<F, kLeanBatch, true>(p, gp, it, tb, pacc, ws, cmask);
+        for (; it + kObjBatch <= iters; it += kObjBatch) lean_batch<F, kObjBatch, true>(p, gp, it, tb, pacc, ws, cmask);
       if (it < iters) sample_loop(Bool<false>{}, it);
     } else {
       sample_loop(Bool<false>{}, 0);

@@ -306,26 +306,33 @@ __global__ __launch_bounds__(256) void k_frame_records(const RecordsLaunch a, co
 }
 
 // Exclusive scan of n packed counts by one block (n = the launch's tiles:
-// 8,100 at 1080p; rocPRIM's scan took two launches, ~10 us).
+// 8,100 at 1080p; rocPRIM's scan took two launches, ~10 us): chunks of 1024
+// loaded coalesced, each scanned by wave row scans (DPP-free shuffles) and
+// the 16 wave totals, the running total carried from chunk to chunk.
 __global__ __launch_bounds__(1024) void k_scan_tiles(const unsigned long long* __restrict__ in,
                                                      unsigned long long* __restrict__ out, int n) {
-  __shared__ unsigned long long part[1024];
-  const int t = (int)threadIdx.x, per = (n + 1023) / 1024, b = t * per;
-  unsigned long long sum = 0ull;
-  for (int i = b; i < min(n, b + per); ++i) sum += in[i];
-  part[t] = sum;
+  __shared__ unsigned long long wtot[16];
+  __shared__ unsigned long long carry;
+  const int t = (int)threadIdx.x, lane = t & 63, w = t >> 6;
+  if (t == 0) carry = 0ull;
   __syncthreads();
-  for (int off = 1; off < 1024; off <<= 1) {
-    const unsigned long long v = t >= off ? part[t - off] : 0ull;
+  for (int base = 0; base < n; base += 1024) {
+    const int i = base + t;
+    const unsigned long long v = i < n ? in[i] : 0ull;
+    unsigned long long x = v;  // inclusive scan within the wave
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const unsigned lo = (unsigned)__shfl_up((int)(unsigned)x, off), hi = (unsigned)__shfl_up((int)(unsigned)(x >> 32), off);
+      if (lane >= off) x += ((unsigned long long)hi << 32) | lo;
+    }
+    if (lane == 63) wtot[w] = x;
     __syncthreads();
-    part[t] += v;
+    unsigned long long before = carry;
+    for (int k = 0; k < w; ++k) before += wtot[k];
+    if (i < n) out[i] = before + x - v;
     __syncthreads();
-  }
-  unsigned long long run = t > 0 ? part[t - 1] : 0ull;
-  for (int i = b; i < min(n, b + per); ++i) {
-    const unsigned long long v = in[i];
-    out[i] = run;
-    run += v;
+    if (t == 1023) carry = before + x;
+    __syncthreads();
   }
 }
 
@@ -417,65 +424,78 @@ __global__ __launch_bounds__(256) void k_frame_class_write(const RecordsLaunch a
 }
 
 // Object masks (rt_bins.cpp build_object_pixel_masks). k_frame_obj_rects
-// (one wave) projects every object's world box once: its pixel rectangle
-// (x0, x1, y0, y1; -1s: off screen) into rects[4 i ..], and after them the
-// mask of the objects with no bounded projection (in every pixel's mask).
-__global__ __launch_bounds__(64) void k_frame_obj_rects(const ObjMaskLaunch a) {
-  const int t = (int)threadIdx.x;
-  bool alw = false;
-  if (t < a.nobj) {
-    const DevObjBox& b = a.objs[t];
-    bool proj = !b.always;
-    double xmin = INFINITY, xmax = -INFINITY, ymin = INFINITY, ymax = -INFINITY;
-    for (int c = 0; proj && c < 8; ++c) {
-      const double pw[3] = {(c & 1) ? b.hi[0] : b.lo[0], (c & 2) ? b.hi[1] : b.lo[1], (c & 4) ? b.hi[2] : b.lo[2]};
-      double pc[3];
-      bg::xform_point(a.w2c, pw, pc);
-      if (!(pc[2] < -1e-9 * (1.0 + fabs(pc[0]) + fabs(pc[1])))) {
-        proj = false;  // a corner at or behind the camera plane: no bounded projection
-        break;
-      }
-      const double px = 0.5 * a.width + (pc[0] / -pc[2]) / a.cam_a;
-      const double py = 0.5 * a.height - (pc[1] / -pc[2]) / a.cam_c;
-      xmin = bg::dmin(xmin, px);
-      xmax = bg::dmax(xmax, px);
-      ymin = bg::dmin(ymin, py);
-      ymax = bg::dmax(ymax, py);
+// projects every object's world box once, one thread per (object, corner)
+// (the corners' float64 projections in parallel, min / max over each
+// object's 8 lanes): its pixel rectangle (x0, x1, y0, y1; -1s: off screen)
+// into rects[4 i ..], and after them the mask of the objects with no bounded
+// projection (in every pixel's mask).
+__global__ __launch_bounds__(512) void k_frame_obj_rects(const ObjMaskLaunch a) {
+  __shared__ int alw[64];
+  const int t = (int)threadIdx.x, i = t >> 3, c = t & 7;
+  bool proj = false, bad = false;
+  double px = 0.0, py = 0.0;
+  if (i < a.nobj) {
+    const DevObjBox& b = a.objs[i];
+    proj = !b.always;
+    const double pw[3] = {(c & 1) ? b.hi[0] : b.lo[0], (c & 2) ? b.hi[1] : b.lo[1], (c & 4) ? b.hi[2] : b.lo[2]};
+    double pc[3];
+    bg::xform_point(a.w2c, pw, pc);
+    // a corner at or behind the camera plane: no bounded projection
+    bad = !(pc[2] < -1e-9 * (1.0 + fabs(pc[0]) + fabs(pc[1])));
+    if (!bad) {
+      px = 0.5 * a.width + (pc[0] / -pc[2]) / a.cam_a;
+      py = 0.5 * a.height - (pc[1] / -pc[2]) / a.cam_c;
     }
-    alw = !proj;
+  }
+  double xmin = px, xmax = px, ymin = py, ymax = py;
+#pragma unroll
+  for (int k = 1; k < 8; k <<= 1) {  // the object's 8 lanes (aligned groups of one wave)
+    xmin = bg::dmin(xmin, __shfl_xor(xmin, k));
+    xmax = bg::dmax(xmax, __shfl_xor(xmax, k));
+    ymin = bg::dmin(ymin, __shfl_xor(ymin, k));
+    ymax = bg::dmax(ymax, __shfl_xor(ymax, k));
+    bad = bad || __shfl_xor((int)bad, k) != 0;
+  }
+  if (i < a.nobj && c == 0) {
+    proj = proj && !bad;
+    alw[i] = proj ? 0 : 1;
     int4 r = make_int4(-1, -1, -1, -1);
     const double m = a.margin;
     if (proj && xmax + m >= 0.0 && ymax + m >= 0.0 && xmin - m < a.width && ymin - m < a.height)
       r = make_int4((int)bg::dmax(0.0, floor(xmin - m)), (int)bg::dmin((double)a.width - 1, floor(xmax + m)),
                     (int)bg::dmax(0.0, floor(ymin - m)), (int)bg::dmin((double)a.height - 1, floor(ymax + m)));
-    reinterpret_cast<int4*>(a.rects)[t] = r;
+    reinterpret_cast<int4*>(a.rects)[i] = r;
   }
-  const unsigned long long am = __ballot(alw);
-  if (t == 0) *reinterpret_cast<unsigned long long*>(a.rects + 4 * 64) = am;
+  __syncthreads();
+  if (t == 0) {
+    unsigned long long am = 0ull;
+    for (int k = 0; k < a.nobj; ++k) am |= alw[k] ? 1ull << k : 0ull;
+    *reinterpret_cast<unsigned long long*>(a.rects + 4 * 64) = am;
+  }
 }
 
-// Per pixel of one launch row segment (block (segment, launch row)): the
-// row's objects once per block (a uniform loop over the rectangles), then
-// each pixel's x tests against them.
+// Per pixel of a 256-column segment (blockIdx.x) of every gridDim.y-th launch
+// row: lane i of each wave holds object i's rectangle in registers, a ballot
+// gives the row's objects, and each pixel tests its x against theirs
+// (read back from the holding lanes as uniform values).
 __global__ __launch_bounds__(256) void k_frame_obj_masks(const ObjMaskLaunch a) {
-  const int y = frame_row(a.rows, (int)blockIdx.y);
-  if (y < 0) return;
-  const int4* __restrict__ rects = (const int4*)a.rects;
-  unsigned long long row = 0ull;
-  for (int i = 0; i < a.nobj; ++i) {
-    const int4 r = rects[i];
-    row |= (r.x >= 0 && y >= r.z && y <= r.w) ? 1ull << i : 0ull;
-  }
+  const int lane = (int)(threadIdx.x & 63u);
+  const int4 mine = lane < a.nobj ? reinterpret_cast<const int4*>(a.rects)[lane] : make_int4(-1, -1, -1, -1);
+  const unsigned long long always = *reinterpret_cast<const unsigned long long*>(a.rects + 4 * 64);
   const int x = (int)(blockIdx.x * 256u + threadIdx.x);
-  if (x >= a.width) return;
-  unsigned long long mk = *(const unsigned long long*)(a.rects + 4 * 64);
-  while (row != 0ull) {
-    const int i = (int)__builtin_ctzll(row);
-    row &= row - 1ull;
-    const int4 r = rects[i];
-    mk |= (x >= r.x && x <= r.y) ? 1ull << i : 0ull;
+  for (int k = (int)blockIdx.y; k < a.rows.nrows; k += (int)gridDim.y) {
+    const int y = frame_row(a.rows, k);
+    if (y < 0) continue;
+    unsigned long long row = __ballot(mine.x >= 0 && y >= mine.z && y <= mine.w);
+    unsigned long long mk = always;
+    while (row != 0ull) {
+      const int i = (int)__builtin_ctzll(row);
+      row &= row - 1ull;
+      const int x0 = __builtin_amdgcn_readlane(mine.x, i), x1 = __builtin_amdgcn_readlane(mine.y, i);
+      mk |= (x >= x0 && x <= x1) ? 1ull << i : 0ull;
+    }
+    if (x < a.width) a.masks[(size_t)y * a.width + x] = mk;
   }
-  a.masks[(size_t)y * a.width + x] = mk;
 }
 
 }  // namespace
@@ -573,10 +593,11 @@ extern "C" long long rtmi_frame_tile_bytes(int ncols, int nrows) {
 
 extern "C" int rtmi_frame_obj_masks(const rtmi::ObjMaskLaunch* a, void* stream) {
   if (a->nobj > 64 || a->rows.nrows <= 0 || a->width <= 0) return a->nobj > 64 ? (int)hipErrorInvalidValue : 0;
-  hipLaunchKernelGGL(rtmi::k_frame_obj_rects, dim3(1), dim3(64), 0, (hipStream_t)stream, *a);
+  hipLaunchKernelGGL(rtmi::k_frame_obj_rects, dim3(1), dim3(512), 0, (hipStream_t)stream, *a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
-  hipLaunchKernelGGL(rtmi::k_frame_obj_masks, dim3((unsigned)((a->width + 255) / 256), (unsigned)a->rows.nrows), dim3(256),
-                     0, (hipStream_t)stream, *a);
+  const unsigned segs = (unsigned)((a->width + 255) / 256);
+  const unsigned rows = (unsigned)std::min<long long>(a->rows.nrows, std::max<long long>(1, 2048 / segs));
+  hipLaunchKernelGGL(rtmi::k_frame_obj_masks, dim3(segs, rows), dim3(256), 0, (hipStream_t)stream, *a);
   return (int)hipGetLastError();
 }

@@ -1031,9 +1031,9 @@ unsigned f32_subset(const rt_scene* s, const rt_options* o) {
 // Lanes per pixel of a float32 launch (a power of two, <= 64): as many as
 // the samples fill; scenes of spheres / boxes / planes with distant lights
 // and no reflection (k_render_fast's object-binned batches) use fewer, so a
-// work item holds at least one batch of 4 iterations (C2: 64 spp -> 16 lanes,
-// 4 pixels per wave), but not fewer than 16 (the pixel bins' <= 4 pixels per
-// wave). The count does not depend on the binning / batching flags, so
+// work item holds at least one batch of kObjBatch = 4 iterations (C2: 64 spp
+// -> 16 lanes, 4 pixels per wave), but not fewer than 16 (8 for a batch of
+// 8). The count does not depend on the binning / batching flags, so
 // RT_FLAG_NO_BINNING and RT_FLAG_NO_OBJ_BATCH frames stay bit-identical (the
 // same samples per lane, summed in the same order).
 int f32_lanes(const rt_scene* s, const rt_options* o, int spp) {
@@ -1043,7 +1043,8 @@ int f32_lanes(const rt_scene* s, const rt_options* o, int spp) {
   while (L * 2 <= std::min(std::min(spp, 64), std::max(1, max_lanes))) L *= 2;
   const unsigned sub = f32_subset(s, o);
   const bool ob_batch = !(sub & (SUB_MESH | SUB_REFLECT | SUB_POINT)) && (sub & (SUB_SPHERE | SUB_BOX));
-  while (ob_batch && L > 16 && spp / L < 4) L /= 2;
+  const int lmin = kObjBatch > 4 ? 8 : 16;  // <= 8 pixels per wave (the kernel's object-mask union)
+  while (ob_batch && L > lmin && spp / L < kObjBatch) L /= 2;
   return L;
 }
 

@@ -11,5 +11,6 @@ for k in $(seq 0 15); do
   /opt/rocm/bin/hipcc --offload-arch=gfx950 $F -DRTMI_PART=$k -c csrc/rt_kernels_f32_part.hip -o build/var/$1/part$k.o 2> >(grep -v "packed-fp32-ops. is not a recognized" >&2) &
 done
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off $2 -c csrc/rt_frame.hip -o build/var/$1/frame.o &
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-result -ffp-contract=off $2 -c csrc/rtmi.cpp -o build/var/$1/rtmi.o &
 wait
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ../tools/ab/$1.so build/var/$1/main.o build/var/$1/part*.o build/rt_kernels_f64.o build/rt_kernels_io.o build/rtmi.o build/rt_bvh.o build/rt_bvh_gpu.o build/rt_queue.o build/rt_obj.o build/rt_multi.o build/rt_bins.o build/var/$1/frame.o
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ../tools/ab/$1.so build/var/$1/main.o build/var/$1/part*.o build/rt_kernels_f64.o build/rt_kernels_io.o build/var/$1/rtmi.o build/rt_bvh.o build/rt_bvh_gpu.o build/rt_queue.o build/rt_obj.o build/rt_multi.o build/rt_bins.o build/var/$1/frame.o
