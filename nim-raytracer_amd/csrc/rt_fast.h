@@ -2074,6 +2074,9 @@ __device__ __forceinline__ bool gen1_batch(KP p, const GroupPix& gp, int it0, un
           ro[k] = f3(so[k].x + mob.t[0], so[k].y + mob.t[1], so[k].z + mob.t[2]);
           rd[k] = sd;
           pm[k] = bal(lane_in(litm[k]) && mesh_gate(mob, slab_ray(ro[k], rd[k])));
+#ifdef RTMI_DIAG_GEN_NOMESHORIGIN
+          pm[k] &= ~bal(hm[k]);  // diagnostic build only (wrong images): mesh-origin shadow rays skip the mesh
+#endif
           anyp |= pm[k];
         }
         if (anyp == 0ull) return true;

@@ -306,32 +306,58 @@ __global__ __launch_bounds__(256) void k_frame_records(const RecordsLaunch a, co
 }
 
 // Exclusive scan of n packed counts by one block (n = the launch's tiles:
-// 8,100 at 1080p; rocPRIM's scan took two launches, ~10 us): chunks of 1024
-// loaded coalesced, each scanned by wave row scans (DPP-free shuffles) and
-// the 16 wave totals, the running total carried from chunk to chunk.
+// 8,100 at 1080p; rocPRIM's scan took two launches, ~10 us): per round of
+// 8 x 1024 values, every thread loads its 8 (coalesced, all in flight at
+// once), wave scans of each, then one wave scans the 128 wave totals.
+__device__ __forceinline__ unsigned long long shfl_up_u64(unsigned long long x, int off) {
+  const unsigned lo = (unsigned)__shfl_up((int)(unsigned)x, off), hi = (unsigned)__shfl_up((int)(unsigned)(x >> 32), off);
+  return ((unsigned long long)hi << 32) | lo;
+}
 __global__ __launch_bounds__(1024) void k_scan_tiles(const unsigned long long* __restrict__ in,
                                                      unsigned long long* __restrict__ out, int n) {
-  __shared__ unsigned long long wtot[16];
+  constexpr int C = 8;
+  __shared__ unsigned long long wtot[C * 16];
   __shared__ unsigned long long carry;
   const int t = (int)threadIdx.x, lane = t & 63, w = t >> 6;
   if (t == 0) carry = 0ull;
-  __syncthreads();
-  for (int base = 0; base < n; base += 1024) {
-    const int i = base + t;
-    const unsigned long long v = i < n ? in[i] : 0ull;
-    unsigned long long x = v;  // inclusive scan within the wave
+  for (int base = 0; base < n; base += 1024 * C) {
+    unsigned long long v[C], x[C];
 #pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      const unsigned lo = (unsigned)__shfl_up((int)(unsigned)x, off), hi = (unsigned)__shfl_up((int)(unsigned)(x >> 32), off);
-      if (lane >= off) x += ((unsigned long long)hi << 32) | lo;
+    for (int c = 0; c < C; ++c) {
+      const int i = base + c * 1024 + t;
+      v[c] = i < n ? in[i] : 0ull;
+      x[c] = v[c];
     }
-    if (lane == 63) wtot[w] = x;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1)
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        const unsigned long long y = shfl_up_u64(x[c], off);
+        x[c] += lane >= off ? y : 0ull;
+      }
+    if (lane == 63)
+#pragma unroll
+      for (int c = 0; c < C; ++c) wtot[c * 16 + w] = x[c];
     __syncthreads();
-    unsigned long long before = carry;
-    for (int k = 0; k < w; ++k) before += wtot[k];
-    if (i < n) out[i] = before + x - v;
+    if (t < 64) {  // the 128 wave totals in order (chunk-major), two per lane
+      const unsigned long long a0 = wtot[2 * t], a1 = wtot[2 * t + 1];
+      unsigned long long y = a0 + a1;
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) {
+        const unsigned long long z = shfl_up_u64(y, off);
+        y += lane >= off ? z : 0ull;
+      }
+      const unsigned long long ex = carry + y - a0 - a1;  // before wave total 2 t
+      wtot[2 * t] = ex;
+      wtot[2 * t + 1] = ex + a0;
+      if (t == 63) carry += y;
+    }
     __syncthreads();
-    if (t == 1023) carry = before + x;
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      const int i = base + c * 1024 + t;
+      if (i < n) out[i] = wtot[c * 16 + w] + x[c] - v[c];
+    }
     __syncthreads();
   }
 }
