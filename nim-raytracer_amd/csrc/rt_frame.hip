@@ -524,6 +524,81 @@ __global__ __launch_bounds__(256) void k_frame_obj_masks(const ObjMaskLaunch a) 
   }
 }
 
+// The face lists' offsets: an exclusive scan of the per-pixel counts in two
+// launches (rocPRIM's took an init launch and a 14 us scan for 2 M counts):
+// k_scan_sums sums each kScanChunk-count chunk; k_scan_apply gives each
+// chunk its offset (the sum of the earlier chunks' sums, one wave) and scans
+// the chunk through LDS (coalesced loads and stores, 32 consecutive counts
+// per thread, wave scans of the thread sums).
+constexpr int kScanPer = 32, kScanChunk = 256 * kScanPer;
+__global__ __launch_bounds__(256) void k_scan_sums(const int32_t* __restrict__ in, long long n, int32_t* __restrict__ sums) {
+  __shared__ int32_t ws[4];
+  const long long base = (long long)blockIdx.x * kScanChunk;
+  int32_t v = 0;
+#pragma unroll 8
+  for (int j = 0; j < kScanPer; ++j) {
+    const long long i = base + (long long)j * 256 + threadIdx.x;
+    v += i < n ? in[i] : 0;
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
+  if ((threadIdx.x & 63u) == 0) ws[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) sums[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
+}
+__global__ __launch_bounds__(256) void k_scan_apply(const int32_t* __restrict__ in, long long n,
+                                                    const int32_t* __restrict__ sums, int32_t* __restrict__ out) {
+  // the chunk in LDS with one pad word per 32 (P(e) = e + e / 32): the
+  // coalesced passes and the per-thread runs of 32 are both conflict-free
+  __shared__ int32_t buf[kScanChunk + kScanChunk / 32];
+  __shared__ int32_t wtot[4];
+  __shared__ int32_t before;
+  const int t = (int)threadIdx.x, lane = t & 63, w = t >> 6;
+  const long long base = (long long)blockIdx.x * kScanChunk;
+  if (w == 0) {  // this chunk's offset: the earlier chunks' sums
+    int32_t p = 0;
+    for (int i = lane; i < (int)blockIdx.x; i += 64) p += sums[i];
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) p += __shfl_xor(p, off);
+    if (lane == 0) before = p;
+  }
+#pragma unroll 8
+  for (int j = 0; j < kScanPer; ++j) {
+    const int e = j * 256 + t;
+    const long long i = base + e;
+    buf[e + (e >> 5)] = i < n ? in[i] : 0;
+  }
+  __syncthreads();
+  int32_t x[kScanPer], sum = 0;  // this thread's 32 consecutive counts
+#pragma unroll
+  for (int j = 0; j < kScanPer; ++j) {
+    x[j] = buf[t * (kScanPer + 1) + j];
+    sum += x[j];
+  }
+  int32_t inc = sum;  // inclusive scan of the thread sums within the wave
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int32_t y = __shfl_up(inc, off);
+    inc += lane >= off ? y : 0;
+  }
+  if (lane == 63) wtot[w] = inc;
+  __syncthreads();
+  int32_t run = before + inc - sum;
+  for (int k = 0; k < w; ++k) run += wtot[k];
+#pragma unroll
+  for (int j = 0; j < kScanPer; ++j) {
+    buf[t * (kScanPer + 1) + j] = run;
+    run += x[j];
+  }
+  __syncthreads();
+#pragma unroll 8
+  for (int j = 0; j < kScanPer; ++j) {
+    const int e = j * 256 + t;
+    const long long i = base + e;
+    if (i < n) out[i] = buf[e + (e >> 5)];
+  }
+}
+
 }  // namespace
 }  // namespace rtmi
 
@@ -534,18 +609,25 @@ constexpr int kBigBlocks = 512;  // the big-face passes' grid (their blocks exit
 extern "C" int rtmi_frame_bins_count(const rtmi::BinsLaunch* a, void* scan_tmp, size_t* scan_tmp_bytes,
                                      void* stream) {
   hipStream_t st = (hipStream_t)stream;
+  const long long nchunk = ((long long)a->scan_n + rtmi::kScanChunk - 1) / rtmi::kScanChunk;
   if (!scan_tmp) {
-    return (int)rocprim::exclusive_scan(nullptr, *scan_tmp_bytes, a->cnt, a->off, 0, (size_t)a->scan_n,
-                                        rocprim::plus<int32_t>(), st);
+    *scan_tmp_bytes = (size_t)std::max(1LL, nchunk) * sizeof(int32_t);
+    return 0;
   }
+  if (*scan_tmp_bytes < (size_t)nchunk * sizeof(int32_t)) return (int)hipErrorInvalidValue;
   const int blocks = (int)(((long long)a->nf * rtmi::kFaceLanes + 255) / 256);
   hipLaunchKernelGGL(rtmi::k_frame_bins_count, dim3(blocks > 0 ? blocks : 1), dim3(256), 0, st, *a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
   hipLaunchKernelGGL(rtmi::k_frame_bins_big<false>, dim3(kBigBlocks), dim3(256), 0, st, *a);
   if ((e = hipGetLastError()) != hipSuccess) return (int)e;
-  return (int)rocprim::exclusive_scan(scan_tmp, *scan_tmp_bytes, a->cnt + a->scan_lo, a->off + a->scan_lo, 0,
-                                      (size_t)a->scan_n, rocprim::plus<int32_t>(), st);
+  if (nchunk == 0) return 0;
+  hipLaunchKernelGGL(rtmi::k_scan_sums, dim3((unsigned)nchunk), dim3(256), 0, st, a->cnt + a->scan_lo, (long long)a->scan_n,
+                     (int32_t*)scan_tmp);
+  if ((e = hipGetLastError()) != hipSuccess) return (int)e;
+  hipLaunchKernelGGL(rtmi::k_scan_apply, dim3((unsigned)nchunk), dim3(256), 0, st, a->cnt + a->scan_lo,
+                     (long long)a->scan_n, (const int32_t*)scan_tmp, a->off + a->scan_lo);
+  return (int)hipGetLastError();
 }
 
 extern "C" int rtmi_frame_bins_fill(const rtmi::BinsLaunch* a, void* stream) {
