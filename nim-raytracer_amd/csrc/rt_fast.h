@@ -1273,6 +1273,9 @@ __device__ __forceinline__ void lean_batch(KP p, const GroupPix& gp, int it0, co
   F3 oc[S];
 #pragma unroll
   for (int k = 0; k < S; ++k) oc[k] = o;
+#ifdef RTMI_DIAG_OB_NOCAM
+  cmask &= 1ull;  // diagnostic build only (wrong images): camera rays test object 0 alone
+#endif
   masked_objects(cmask, [&](const int i) {
     const FObj ob = at(objs, i);
     analytic_t_batch<F, S>(p, ob, i, oc, d, [&](int k, float t) {
@@ -1404,6 +1407,9 @@ __device__ __forceinline__ void lean_batch(KP p, const GroupPix& gp, int it0, co
           smask = every ? smask : m;
         }
       }
+#ifdef RTMI_DIAG_OB_NOSHADOW
+      smask = 0ull;  // diagnostic build only (wrong images): the shadow rays' object tests' share
+#endif
       masked_objects(smask, [&](const int i) {
         const FObj ob = at(objs, i);
         if constexpr (kPlanesOnly) {
