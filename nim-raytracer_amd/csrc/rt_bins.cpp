@@ -735,6 +735,54 @@ bool build_object_pixel_masks(const std::vector<ObjBox>& objs, const double c2w[
   return true;
 }
 
+// Convex hull of 2D points (Andrew's monotone chain), counter-clockwise,
+// collinear points dropped.
+std::vector<std::array<double, 2>> convex_hull_2d(std::vector<std::array<double, 2>> p) {
+  std::sort(p.begin(), p.end());
+  p.erase(std::unique(p.begin(), p.end()), p.end());
+  if (p.size() < 3) return p;
+  auto cross = [](const std::array<double, 2>& o, const std::array<double, 2>& a, const std::array<double, 2>& b) {
+    return (a[0] - o[0]) * (b[1] - o[1]) - (a[1] - o[1]) * (b[0] - o[0]);
+  };
+  std::vector<std::array<double, 2>> h(2 * p.size());
+  size_t k = 0;
+  for (size_t i = 0; i < p.size(); ++i) {
+    while (k >= 2 && cross(h[k - 2], h[k - 1], p[i]) <= 0.0) --k;
+    h[k++] = p[i];
+  }
+  for (size_t i = p.size() - 1, t = k + 1; i-- > 0;) {
+    while (k >= t && cross(h[k - 2], h[k - 1], p[i]) <= 0.0) --k;
+    h[k++] = p[i];
+  }
+  h.resize(k - 1);
+  return h;
+}
+
+// Whether a convex polygon (counter-clockwise) meets the box [u0, u1] x
+// [v0, v1]: separating axis test over the box's axes and the polygon's edge
+// normals (touching counts as meeting).
+bool hull_meets_box(const std::vector<std::array<double, 2>>& h, double u0, double v0, double u1, double v1) {
+  double pu0 = INFINITY, pu1 = -INFINITY, pv0 = INFINITY, pv1 = -INFINITY;
+  for (const auto& q : h) {
+    pu0 = std::min(pu0, q[0]);
+    pu1 = std::max(pu1, q[0]);
+    pv0 = std::min(pv0, q[1]);
+    pv1 = std::max(pv1, q[1]);
+  }
+  if (pu1 < u0 || pu0 > u1 || pv1 < v0 || pv0 > v1) return false;
+  const size_t n = h.size();
+  for (size_t i = 0; i < n; ++i) {
+    const auto& a = h[i];
+    const auto& b = h[(i + 1) % n];
+    const double nx = b[1] - a[1], ny = a[0] - b[0];  // outward normal of a CCW edge
+    const double lim = nx * a[0] + ny * a[1];
+    // the box lies wholly outside this edge when its nearest corner does
+    const double m = std::min(std::min(nx * u0 + ny * v0, nx * u1 + ny * v0), std::min(nx * u0 + ny * v1, nx * u1 + ny * v1));
+    if (m > lim) return false;
+  }
+  return true;
+}
+
 bool build_object_light_grid(const std::vector<ObjBox>& objs, const double dir[3], ObjGridHost* out,
                              const char** why) {
   *why = "";
@@ -768,6 +816,7 @@ bool build_object_light_grid(const std::vector<ObjBox>& objs, const double dir[3
       for (int k = 0; k < 3; ++k) scale = std::max(scale, std::max(std::fabs(b.lo[k]), std::fabs(b.hi[k])));
   const double delta = 1e-5 * scale;
   std::vector<std::array<double, 4>> box(objs.size());
+  std::vector<std::vector<std::array<double, 2>>> hull(objs.size());
   double umin = INFINITY, umax = -INFINITY, vmin = INFINITY, vmax = -INFINITY;
   for (size_t i = 0; i < objs.size(); ++i) {
     const ObjBox& b = objs[i];
@@ -775,6 +824,11 @@ bool build_object_light_grid(const std::vector<ObjBox>& objs, const double dir[3
       out->off_grid |= 1ull << i;
       continue;
     }
+    hull[i] = convex_hull_2d([&] {
+      std::vector<std::array<double, 2>> q(8);
+      for (int c = 0; c < 8; ++c) q[(size_t)c] = {dot3(b.corner[c], e1), dot3(b.corner[c], e2)};
+      return q;
+    }());
     double bu0 = INFINITY, bu1 = -INFINITY, bv0 = INFINITY, bv1 = -INFINITY;
     for (int c = 0; c < 8; ++c) {
       const double p[3] = {(c & 1) ? b.hi[0] : b.lo[0], (c & 2) ? b.hi[1] : b.lo[1], (c & 4) ? b.hi[2] : b.lo[2]};
@@ -820,8 +874,16 @@ bool build_object_light_grid(const std::vector<ObjBox>& objs, const double dir[3
     const int c1 = std::min(gu - 1, (int)std::floor((box[i][1] - (double)g.u0) * ih));
     const int r0 = std::max(0, (int)std::floor((box[i][2] - (double)g.v0) * ih));
     const int r1 = std::min(gv - 1, (int)std::floor((box[i][3] - (double)g.v0) * ih));
+    // cells meeting the projected hull of the object box's world corners
+    // (grown by delta): a shadow ray can only reach the object through its
+    // projection, which the hull of the box's projection contains
+    const double hc = 1.0 / ih;
     for (int rr = r0; rr <= r1; ++rr)
-      for (int cc = c0; cc <= c1; ++cc) out->masks[(size_t)rr * (size_t)gu + (size_t)cc] |= 1ull << i;
+      for (int cc = c0; cc <= c1; ++cc) {
+        const double cu0 = (double)g.u0 + cc * hc - delta, cv0 = (double)g.v0 + rr * hc - delta;
+        if (hull[i].size() < 3 || hull_meets_box(hull[i], cu0, cv0, cu0 + hc + 2 * delta, cv0 + hc + 2 * delta))
+          out->masks[(size_t)rr * (size_t)gu + (size_t)cc] |= 1ull << i;
+      }
   }
   return true;
 }

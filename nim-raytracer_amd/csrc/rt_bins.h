@@ -130,6 +130,10 @@ namespace rtmi {
 struct ObjBox {
   bool always;       // in every bin (planes, boxes that cannot be projected)
   double lo[3], hi[3];  // world-space bounding box
+  // the object box's 8 corners in world space (through the inverse of the
+  // world_to_object the kernel transforms rays with); the light grids bin
+  // the convex hull of their projection instead of its bounding rectangle
+  double corner[8][3];
 };
 bool build_object_pixel_masks(const std::vector<ObjBox>& objs, const double c2w[16], double fov_deg, int width,
                               int height, std::vector<unsigned long long>* masks, const char** why);

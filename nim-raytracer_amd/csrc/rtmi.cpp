@@ -897,6 +897,7 @@ extern "C" int rt_scene_create(const rt_scene_desc* d, rt_scene** out_scene) {
         const double q[3] = {(c & 1) ? hi[0] : lo[0], (c & 2) ? hi[1] : lo[1], (c & 4) ? hi[2] : lo[2]};
         for (int r = 0; r < 3; ++r) {
           const double w = o2w[0 * 4 + r] * q[0] + o2w[1 * 4 + r] * q[1] + o2w[2 * 4 + r] * q[2] + o2w[3 * 4 + r];
+          b.corner[c][r] = w;
           b.lo[r] = std::min(b.lo[r], w);
           b.hi[r] = std::max(b.hi[r], w);
         }
