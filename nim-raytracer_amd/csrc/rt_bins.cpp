@@ -577,12 +577,12 @@ bool build_shadow_skips(const std::vector<int32_t>& pix_off, const std::vector<S
             vmin = std::min(vmin, v);
             vmax = std::max(vmax, v);
           }
-          // float32 hit points, transforms and cell coordinates: far inside
-          // 1e-4 of the magnitudes, plus one whole cell
+          // the footprint as rt_bins_geom.h rect_skip_bits forms it (float32
+          // margins far inside 1e-4 of the magnitudes; no extra cell)
           const double mw = 1e-4 * (1.0 + qmax) + 1e-4 * std::fabs(bias);
           const double ih = g.inv_h;
-          const double fu0 = (umin - mw - g.u0) * ih - 1.0, fu1 = (umax + mw - g.u0) * ih + 1.0;
-          const double fv0 = (vmin - mw - g.v0) * ih - 1.0, fv1 = (vmax + mw - g.v0) * ih + 1.0;
+          const double fu0 = (umin - mw - g.u0) * ih - RTMI_SKIP_CELL_PAD, fu1 = (umax + mw - g.u0) * ih + RTMI_SKIP_CELL_PAD;
+          const double fv0 = (vmin - mw - g.v0) * ih - RTMI_SKIP_CELL_PAD, fv1 = (vmax + mw - g.v0) * ih + RTMI_SKIP_CELL_PAD;
           if (!(fu1 >= 0.0 && fv1 >= 0.0 && fu0 < g.gu && fv0 < g.gv)) continue;  // off the grid
           if (!std::isfinite(fu0 + fu1 + fv0 + fv1)) {
             bits &= ~(1u << l);

@@ -182,12 +182,18 @@ __host__ __device__ inline unsigned rect_skip_bits(const SkipCam& c, const SkipP
         vmin = dmin(vmin, v);
         vmax = dmax(vmax, v);
       }
-      // float32 hit points, transforms and cell coordinates: far inside
-      // 1e-4 of the magnitudes, plus one whole cell
+      // float32 hit points, transforms, shadow rays and triangle tests: far
+      // inside 1e-4 of the magnitudes. A face a shadow ray of the footprint
+      // can meet overlaps the grown footprint, so it is listed in a cell
+      // the footprint's cell range holds (cells list every face whose grown
+      // projection meets them): no cell beyond that range is needed.
+#ifndef RTMI_SKIP_CELL_PAD
+#define RTMI_SKIP_CELL_PAD 0.0
+#endif
       const double mw = 1e-4 * (1.0 + qmax) + 1e-4 * fabs(c.bias);
       const double ih = g.inv_h;
-      const double fu0 = (umin - mw - g.u0) * ih - 1.0, fu1 = (umax + mw - g.u0) * ih + 1.0;
-      const double fv0 = (vmin - mw - g.v0) * ih - 1.0, fv1 = (vmax + mw - g.v0) * ih + 1.0;
+      const double fu0 = (umin - mw - g.u0) * ih - RTMI_SKIP_CELL_PAD, fu1 = (umax + mw - g.u0) * ih + RTMI_SKIP_CELL_PAD;
+      const double fv0 = (vmin - mw - g.v0) * ih - RTMI_SKIP_CELL_PAD, fv1 = (vmax + mw - g.v0) * ih + RTMI_SKIP_CELL_PAD;
       if (!(fu1 >= 0.0 && fv1 >= 0.0 && fu0 < g.gu && fv0 < g.gv)) continue;  // off the grid
       if (!isfinite(fu0 + fu1 + fv0 + fv1)) {
         bits &= ~(1u << l);
