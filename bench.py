@@ -168,6 +168,7 @@ def main():
     import torch.distributed as dist
 
     from rtmi import Antialias, Options, Precision, akGrid, scenes
+    from rtmi._lib import kernel_source_hash, library_source_hash
     from rtmi.dist import band_rows, gather_bands
     from rtmi.renderer import DeviceScene
 
@@ -405,6 +406,9 @@ def main():
             },
             "roofline": roof,
             "cpu_baseline": None,
+            # build provenance: the library's embedded source hash against this tree's
+            "build": {"library_sources": library_source_hash(), "tree_sources": kernel_source_hash(),
+                      "match": library_source_hash() == kernel_source_hash()},
         }
         if frame_check is not None:
             out["frame_check"] = frame_check

@@ -256,6 +256,11 @@ typedef struct rt_scene rt_scene; /* opaque, owns device buffers */
 /* ABI version of the loaded library (RTMI_ABI_VERSION). */
 int rt_version(void);
 
+/* Hash of the native sources the library was built from (16 hex digits:
+ * sha256 of csrc/, the Makefile and this header, nim-raytracer_amd/rtmi/
+ * srchash.py): build provenance for benchmarks and profiles. */
+const char *rt_build_source_hash(void);
+
 /* Message of the last failed call on this thread ("" if none). */
 const char *rt_last_error(void);
 

@@ -270,6 +270,11 @@ extern "C" {
 
 int rt_version(void) { return RTMI_ABI_VERSION; }
 
+#ifndef RTMI_SOURCE_HASH
+#define RTMI_SOURCE_HASH "unknown"
+#endif
+const char* rt_build_source_hash(void) { return RTMI_SOURCE_HASH; }
+
 const char* rt_last_error(void) { return g_err.c_str(); }
 
 int rt_device_count(void) {

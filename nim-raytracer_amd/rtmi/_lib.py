@@ -50,15 +50,10 @@ def kernel_source_hash():
     """sha256 (first 16 hex digits) of the native sources (csrc/, the
     Makefile, include/rtmi.h): PMC summaries record it, and bench.py uses a
     committed summary only for the sources it was measured on."""
-    import hashlib
-    here = os.path.dirname(os.path.abspath(__file__))
-    pkg = os.path.dirname(here)
-    files = [os.path.join(pkg, "Makefile"), os.path.join(os.path.dirname(pkg), "include", "rtmi.h")]
-    csrc = os.path.join(pkg, "csrc")
-    files += [os.path.join(csrc, f) for f in sorted(os.listdir(csrc)) if f.endswith((".h", ".hip", ".cpp"))]
-    h = hashlib.sha256()
-    for f in files:
-        h.update(os.path.basename(f).encode())
-        with open(f, "rb") as fh:
-            h.update(fh.read())
-    return h.hexdigest()[:16]
+    from .srchash import source_hash
+    return source_hash()
+
+
+def library_source_hash():
+    """The source hash librtmi.so was built from (rt_build_source_hash)."""
+    return lib().rt_build_source_hash().decode()

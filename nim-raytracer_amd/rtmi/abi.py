@@ -163,6 +163,7 @@ class rt_scene_info(C.Structure):
 _P = C.c_void_p
 SIGNATURES = {
     "rt_version": (C.c_int, []),
+    "rt_build_source_hash": (C.c_char_p, []),
     "rt_last_error": (C.c_char_p, []),
     "rt_init": (C.c_int, [C.c_int]),
     "rt_device_count": (C.c_int, []),

@@ -37,6 +37,15 @@ def test_version_and_error_channel():
     assert b"null" in L.rt_last_error()
 
 
+def test_library_built_from_these_sources():
+    """Build provenance: librtmi.so carries the hash of the native sources it
+    was compiled from (rt_build_source_hash, the Makefile computes it); a
+    library left over from other sources fails here instead of being
+    measured as if it were this tree's."""
+    from rtmi._lib import kernel_source_hash, library_source_hash
+    assert library_source_hash() == kernel_source_hash()
+
+
 def test_no_gpu_is_an_error_not_a_crash():
     L = lib()
     if L.rt_device_count() > 0:
