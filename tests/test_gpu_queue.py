@@ -116,3 +116,36 @@ def test_failed_line_reports_its_error(gpu):
         time.sleep(0.001)
     q.shutdown()
     q.close()
+
+
+def test_queue_progressive_frame_matches_oracle(gpu, oracle_mod):
+    """The queue-driven gui.nim loop against the oracle itself (not only against
+    direct calls): float64 parity mode, maxStep 4 -> 2 -> 1 over every
+    countup(0, h-1, step) line, the oracle's renderLine (renderer.nim:162-211)
+    called for the same lines in the same order — frames bit-identical after
+    every level, Stats equal in total."""
+    scene = scenes.mesh_mix()
+    w, h, max_step = 80, 56, 4
+    opts = Options(width=w, height=h, antialias=Antialias(akGrid, 2), bias=1e-4, maxRayDepth=5,
+                   precision=Precision.fp64)
+    ds = DeviceScene(scene)
+    q = initRenderWorkers(ds, numActiveWorkers=4, poolSize=8)
+    q.waitForReady()
+    assert q.start()
+    o = oracle_mod.OracleScene(scene)
+    fb = np.zeros((h, w, 3), np.float32)
+    ref = np.zeros_like(fb)
+    tot_g, tot_r = Stats(), Stats()
+    step = max_step
+    while step >= 1:
+        lines = list(range(0, h, step))
+        for y in lines:
+            q.queueWork(opts, fb, y, step, max_step)
+        _, st = _drain(q, len(lines))
+        tot_g += st
+        for y in lines:
+            tot_r += o.render_line(opts, ref, y, step, max_step)
+        assert np.array_equal(fb, ref), step
+        step //= 2
+    assert tot_g == tot_r
+    assert q.stop() and q.shutdown() and q.close()
