@@ -2282,7 +2282,15 @@ __device__ __forceinline__ void finish_item(KP p, const GroupPix& gp, F3 acc, in
   if (L == 64) {  // one pixel per wave: DPP row scans + row broadcasts, total in lane 63
     acc = f3(wave_total(acc.x), wave_total(acc.y), wave_total(acc.z));
   } else {
-    for (int off = 1; off < L; off <<= 1) {
+    // the xor butterfly over the pixel's L lanes; inside a 16-lane row it is
+    // DPP (quad_perm 1,0,3,2 / 2,3,0,1, row_ror:12 = lane i + 4, row_ror:8):
+    // lane sub == 0 adds the butterfly's partners in its order, so its sum is
+    // bit-identical (the other lanes' sums are not used)
+    if (L >= 2) acc = f3(dpp_add<0xB1, 0xf>(acc.x), dpp_add<0xB1, 0xf>(acc.y), dpp_add<0xB1, 0xf>(acc.z));
+    if (L >= 4) acc = f3(dpp_add<0x4E, 0xf>(acc.x), dpp_add<0x4E, 0xf>(acc.y), dpp_add<0x4E, 0xf>(acc.z));
+    if (L >= 8) acc = f3(dpp_add<0x12C, 0xf>(acc.x), dpp_add<0x12C, 0xf>(acc.y), dpp_add<0x12C, 0xf>(acc.z));
+    if (L >= 16) acc = f3(dpp_add<0x128, 0xf>(acc.x), dpp_add<0x128, 0xf>(acc.y), dpp_add<0x128, 0xf>(acc.z));
+    for (int off = 16; off < L; off <<= 1) {
       acc.x += __shfl_xor(acc.x, off);
       acc.y += __shfl_xor(acc.y, off);
       acc.z += __shfl_xor(acc.z, off);
