@@ -200,3 +200,39 @@ def test_object_batches_identical(gpu, name, m):
         fb, sb = _render(ds, _opts(200, 120, m, flags))
         assert sa == sb, (name, m, flags)
         assert torch.equal(fa, fb), (name, m, flags, float((fa - fb).abs().max()))
+
+
+def _boxes2_variant(kind):
+    """boxes2 variants: scaled boxes and a non-uniformly scaled ball (the
+    sphere test's `/ 2*a` quirk then scales t, geom.nim:215-233), low suns
+    from other azimuths, two suns, a non-unit light direction."""
+    from rtmi.glm import normalize, vec
+    s = scenes.boxes2()
+    if kind == "scaled":
+        for i, o in enumerate(s.objects[1:], start=1):
+            g = o.geometry
+            f = vec3(2.0, 0.5, 1.0) if i == 2 else vec3(1.0 + 0.1 * (i % 4), 0.7 + 0.2 * (i % 3), 1.3)
+            g.objectToWorld = scale(g.objectToWorld, f)
+            g.worldToObject = inverse(g.objectToWorld)
+        s.lights[0].dir = normalize(vec(-2.0, -0.35, 3.0))
+    elif kind == "two_suns":
+        s.lights[0].dir = normalize(vec(-4.0, -0.6, -1.0))
+        s.lights.append(type(s.lights[0])(color=vec3(0.9, 0.8, 0.6), intensity=0.4,
+                                          dir=normalize(vec(1.0, -0.2, 5.0))))
+    elif kind == "nonunit":
+        s.lights[0].dir = vec(3.0, -0.5, -4.0)
+    return s
+
+
+@pytest.mark.parametrize("kind", ["plain", "scaled", "two_suns", "nonunit"])
+def test_object_batches_full_frame_variants(gpu, kind):
+    """C2's full 1080p / 64 spp frame and variants of it: the object-binned
+    batches' frames and Stats equal the one-sample loop's
+    (RT_FLAG_NO_OBJ_BATCH), which test_gpu_configs.py pins to the oracle."""
+    import torch
+    from rtmi.abi import RT_FLAG_NO_OBJ_BATCH
+    ds = DeviceScene(_boxes2_variant(kind))
+    fa, sa = _render(ds, _opts(1920, 1080, 8))
+    fb, sb = _render(ds, _opts(1920, 1080, 8, RT_FLAG_NO_OBJ_BATCH))
+    assert sa == sb, (kind, sa, sb)
+    assert torch.equal(fa, fb), (kind, float((fa - fb).abs().max()))
