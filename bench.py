@@ -315,6 +315,23 @@ def main():
         render_ms.append(b_ms)
     setup_ms = sum(setup_ms) / len(setup_ms)
     render_ms = sum(render_ms) / len(render_ms)
+    # after the timed region: frames that each follow a camera change
+    # (rt_scene_set_camera, alternating two cameras 0.05 apart), so every call
+    # also re-reads its list size and may grow the entry buffer — what an
+    # interactive caller moving the camera every frame pays
+    camera_change_ms = None
+    if not distributed:
+        from rtmi.glm import translate, vec3
+        cams = [translate(scene.cameraToWorld, vec3(0.05, 0.0, 0.0)), scene.cameraToWorld]
+        n_cam = max(4, args.steps)
+        torch.cuda.synchronize()
+        t_cam = time.perf_counter()
+        for k in range(n_cam):
+            ds.set_camera(cams[k % 2], scene.fov)
+            ds.render_device(opts, fb, stream=stream, stats=False)
+        torch.cuda.synchronize()
+        camera_change_ms = (time.perf_counter() - t_cam) * 1e3 / n_cam
+        ds.set_camera(scene.cameraToWorld, scene.fov)
     # outside the timed region: one more launch with Stats, for how many of
     # the batched general pixels fell back to the one-sample loop
     ds.render_bands_device(opts, local_bufs[0], BAND_H, rank, world, stream=stream, stats=True)
@@ -400,6 +417,7 @@ def main():
                 "shadow_rays_per_frame": shadow_frame, "parallelism": f"bands{world}",
                 "scene_setup_s": round(setup_s, 3), "scene_setup_ms_lib": round(info["build_ms"], 1),
                 "first_frame_ms": None if first_frame_ms is None else round(first_frame_ms, 3),
+                "camera_change_frame_ms": None if camera_change_ms is None else round(camera_change_ms, 3),
                 "lean_pixel_groups": lean_groups, "general_pixel_groups": general_groups,
                 "batched_general_groups": batched_groups, "batch_fallback_groups": batch_fallback,
                 "bvh_builder": {"sah": "host binned SAH", "ploc": "device PLOC"}[args.bvh],

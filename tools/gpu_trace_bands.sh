@@ -23,6 +23,8 @@ for name, dur, s, e in seq:
 for name, v in stats.items():
     print(name, "n", len(v), "dur_us(median)", sorted(d for d, _ in v)[len(v)//2])
 # last 30 entries
-for name, dur, s, e in seq[-12:]:
-    print(f"{name:40s} {dur:9.1f} us")
+last = None
+for name, dur, s, e in seq[-32:]:
+    print(f"{name:40s} {dur:9.1f} us  gap {((s - last) / 1e3 if last else 0):7.1f} us")
+    last = e
 PY
