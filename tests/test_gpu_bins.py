@@ -236,3 +236,23 @@ def test_object_batches_full_frame_variants(gpu, kind):
     fb, sb = _render(ds, _opts(1920, 1080, 8, RT_FLAG_NO_OBJ_BATCH))
     assert sa == sb, (kind, sa, sb)
     assert torch.equal(fa, fb), (kind, float((fa - fb).abs().max()))
+
+
+def test_counters_not_stale_after_no_stats_call(gpu):
+    """rt_scene_last_counters after a call that set RT_FLAG_NO_STATS fails
+    (that call reduced nothing) instead of returning the previous
+    RT_FLAG_COUNT_TRAVERSAL call's counters (include/rtmi.h); a new counting
+    call makes them readable again."""
+    from rtmi._lib import RtmiError
+    from rtmi.abi import RT_FLAG_NO_STATS
+    ds = DeviceScene(scenes.mesh_bunny())
+    _render(ds, _opts(160, 90, 8, RT_FLAG_COUNT_TRAVERSAL))
+    first = ds.last_counters()
+    assert first["lane_node_visits"] + first["lane_tri_tests"] > 0
+    import torch
+    fb = torch.zeros(160 * 90 * 3, dtype=torch.float32, device="cuda")
+    ds.render_device(_opts(160, 90, 8, RT_FLAG_NO_STATS), fb, stats=False)
+    with pytest.raises(RtmiError):
+        ds.last_counters()
+    _render(ds, _opts(160, 90, 8, RT_FLAG_COUNT_TRAVERSAL))
+    assert ds.last_counters() == first

@@ -215,11 +215,10 @@ def test_lean1_light_sides(gpu, dirs):
 
 @pytest.mark.parametrize("cam_y,bias", [(5.5, 1e-4), (5.5, 1e-7), (5.5, 0.0), (-3.0, 1e-4), (0.5, 1e-4)])
 def test_lean1_camera_side_and_bias(gpu, cam_y, bias):
-    """Lights above the plane: with a bias the shadow origin's rounding
-    cannot cancel the lean kernels skip the occlusion test (rtmi.cpp
-    lean_no_occ, rt_fast.h lean1q_loop MODE 2; its lit test is sg dy > 1e-6
-    with sg the side of the camera), otherwise they keep it (bias 1e-7, 0):
-    equal to the general kernels either way, camera above or below the plane."""
+    """Camera above or below the ground plane and biases down to 0: every
+    lean sample tests each light's shadow ray against the plane (round 3
+    removed the host-proved shortcuts of lean modes 1 / 2), and the merged
+    one-plane kernel renders the general kernels' frame and Stats."""
     import torch
     s = scenes.mesh_bunny()
     s.cameraToWorld = scenes._std_camera(0.0, cam_y, 1.5)
@@ -229,6 +228,8 @@ def test_lean1_camera_side_and_bias(gpu, cam_y, bias):
     for flags in (0, RT_FLAG_NO_MIX):
         fb = torch.zeros_like(ref)
         st = ds.render_device(_opts(256, 144, 16, flags, bias=bias), fb)
+        if flags == 0 and ds.last_split()[0] > 0:
+            assert ds.last_lean_kernel() == 15, (cam_y, bias, ds.last_lean_kernel())  # k_render_mix1
         assert st == st_ref and torch.equal(fb, ref), (cam_y, bias, flags, float((fb - ref).abs().max()))
 
 
