@@ -123,6 +123,7 @@ struct RecordsLaunch {
   int32_t* lean;            // capacity ngroups + 64
   int32_t* heavy;           // capacity ngroups
   int32_t* ctr;
+  int32_t tiles_done;       // host: the tile bits were written by the count launch
 };
 
 // object bins (rt_bins.h build_object_pixel_masks): world boxes of the objects
@@ -146,7 +147,11 @@ constexpr int kObjRectInts = 4 * 64 + 2;
 
 extern "C" {
 // count + scan; *scan_tmp_bytes in/out: the scan's scratch size (query with scan_tmp == nullptr)
-int rtmi_frame_bins_count(const rtmi::BinsLaunch* a, void* scan_tmp, size_t* scan_tmp_bytes, void* stream);
+// tr / tile_bits (optional): the call's pixel-record launch; its tiles
+// (k_frame_tiles) then run in the count launch and *tiles_done = 1
+int rtmi_frame_bins_count(const rtmi::BinsLaunch* a, void* scan_tmp, size_t* scan_tmp_bytes, void* stream,
+                          const rtmi::RecordsLaunch* tr = nullptr, void* tile_bits = nullptr,
+                          int* tiles_done = nullptr);
 int rtmi_frame_bins_fill(const rtmi::BinsLaunch* a, void* stream);
 // records (+ lists); tile_bits: rtmi_frame_tile_bytes(ncols, nrows) bytes;
 // scratch: *scratch_bytes (query with scratch == nullptr)

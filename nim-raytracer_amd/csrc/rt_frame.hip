@@ -25,8 +25,7 @@ constexpr int kFaceLanes = 4;
 // Per face: its pixel rectangle and projected vertices (kept for the fill
 // pass), and one count per pixel of the launch's rows that the face's grown
 // projection meets (rt_bins.cpp build_pixel_bins, the same bounds).
-__global__ __launch_bounds__(256) void k_frame_bins_count(const BinsLaunch a) {
-  const int t = (int)(blockIdx.x * 256u + threadIdx.x);
+__device__ __forceinline__ void bins_count_body(const BinsLaunch& a, const int t) {
   if (t == 0) {  // (not FC_BIG: other blocks append to it now; k_frame_bins_fill zeroes it)
 #pragma unroll
     for (int k = 0; k < FC_BIG; ++k) a.ctr[k] = 0;
@@ -79,6 +78,9 @@ __global__ __launch_bounds__(256) void k_frame_bins_count(const BinsLaunch a) {
     bits |= ((unsigned long long)hi << 32) | lo;
   }
   if (q == 0) a.fmask[i] = bits;  // (unused for a face of more than 64 pixels: the fill pass tests again)
+}
+__global__ __launch_bounds__(256) void k_frame_bins_count(const BinsLaunch a) {
+  bins_count_body(a, (int)(blockIdx.x * 256u + threadIdx.x));
 }
 
 // The big faces' pixels (FILL false: counted, true: filled), spread over the
@@ -248,10 +250,8 @@ __device__ __forceinline__ void load_skip_grids(const RecordsLaunch& a, bg::Skip
 constexpr int kTileW = 64, kTileH = 4;
 
 // One thread per tile: the tile's skip bits (0 when not every light is skipped).
-__global__ __launch_bounds__(256) void k_frame_tiles(const RecordsLaunch a, int tiles_x, int ntiles, uint8_t* tile_bits) {
-  __shared__ bg::SkipGrid sg[8];
-  load_skip_grids(a, sg);
-  const int t = (int)(blockIdx.x * 256u + threadIdx.x);
+__device__ __forceinline__ void tiles_body(const RecordsLaunch& a, const int t, int tiles_x, int ntiles,
+                                           uint8_t* tile_bits, const bg::SkipGrid* sg) {
   if (t >= ntiles) return;
   const int tj = t % tiles_x, tk = t / tiles_x;
   const int j0 = tj * kTileW, j1 = min(j0 + kTileW, a.ncols) - 1;
@@ -265,6 +265,28 @@ __global__ __launch_bounds__(256) void k_frame_tiles(const RecordsLaunch a, int 
   unsigned bits = 0u;
   if (yhi >= 0) bits = bg::rect_skip_bits(a.cam, a.planes, a.nplanes, sg, a.nl, a.have, j0 * a.step, ylo, j1 * a.step, yhi);
   tile_bits[t] = (uint8_t)(bits == a.have ? 1u : 0u);
+}
+__global__ __launch_bounds__(256) void k_frame_tiles(const RecordsLaunch a, int tiles_x, int ntiles, uint8_t* tile_bits) {
+  __shared__ bg::SkipGrid sg[8];
+  load_skip_grids(a, sg);
+  tiles_body(a, (int)(blockIdx.x * 256u + threadIdx.x), tiles_x, ntiles, tile_bits, sg);
+}
+
+// k_frame_bins_count and k_frame_tiles in one launch (the tiles depend on
+// the camera and the light grids only): blocks [0, face_blocks) count the
+// faces' pixels, the rest test the 64 x 4 tiles — one launch fewer per call
+// (each costs 4-10 us however little it does; 8 ranks' band sets are
+// dominated by such fixed costs).
+__global__ __launch_bounds__(256) void k_frame_bins_count_tiles(const BinsLaunch a, const RecordsLaunch r,
+                                                                int face_blocks, int tiles_x, int ntiles,
+                                                                uint8_t* tile_bits) {
+  __shared__ bg::SkipGrid sg[8];
+  if ((int)blockIdx.x < face_blocks) {
+    bins_count_body(a, (int)(blockIdx.x * 256u + threadIdx.x));
+    return;
+  }
+  load_skip_grids(r, sg);
+  tiles_body(r, (int)((blockIdx.x - (unsigned)face_blocks) * 256u + threadIdx.x), tiles_x, ntiles, tile_bits, sg);
 }
 
 // Per pixel of one tile (block (tile column, tile row)): the pixel record —
@@ -607,7 +629,7 @@ constexpr int kBigBlocks = 512;  // the big-face passes' grid (their blocks exit
 }
 
 extern "C" int rtmi_frame_bins_count(const rtmi::BinsLaunch* a, void* scan_tmp, size_t* scan_tmp_bytes,
-                                     void* stream) {
+                                     void* stream, const rtmi::RecordsLaunch* tr, void* tile_bits, int* tiles_done) {
   hipStream_t st = (hipStream_t)stream;
   const long long nchunk = ((long long)a->scan_n + rtmi::kScanChunk - 1) / rtmi::kScanChunk;
   if (!scan_tmp) {
@@ -615,8 +637,17 @@ extern "C" int rtmi_frame_bins_count(const rtmi::BinsLaunch* a, void* scan_tmp, 
     return 0;
   }
   if (*scan_tmp_bytes < (size_t)nchunk * sizeof(int32_t)) return (int)hipErrorInvalidValue;
-  const int blocks = (int)(((long long)a->nf * rtmi::kFaceLanes + 255) / 256);
-  hipLaunchKernelGGL(rtmi::k_frame_bins_count, dim3(blocks > 0 ? blocks : 1), dim3(256), 0, st, *a);
+  const int blocks = std::max(1, (int)(((long long)a->nf * rtmi::kFaceLanes + 255) / 256));
+  const int tiles_x = tr ? (tr->ncols + rtmi::kTileW - 1) / rtmi::kTileW : 0;
+  const int ntiles = tr ? tiles_x * ((tr->nrows + rtmi::kTileH - 1) / rtmi::kTileH) : 0;
+  if (tiles_done) *tiles_done = 0;
+  if (tr && tile_bits && tiles_done && tr->have != 0u && ntiles > 0) {
+    hipLaunchKernelGGL(rtmi::k_frame_bins_count_tiles, dim3(blocks + (ntiles + 255) / 256), dim3(256), 0, st, *a, *tr,
+                       blocks, tiles_x, ntiles, (uint8_t*)tile_bits);
+    *tiles_done = 1;
+  } else {
+    hipLaunchKernelGGL(rtmi::k_frame_bins_count, dim3(blocks), dim3(256), 0, st, *a);
+  }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
   hipLaunchKernelGGL(rtmi::k_frame_bins_big<false>, dim3(kBigBlocks), dim3(256), 0, st, *a);
@@ -660,7 +691,7 @@ extern "C" int rtmi_frame_records(const rtmi::RecordsLaunch* a, void* tile_bits,
   }
   if (*scratch_bytes < 2 * cnt_bytes + scan_bytes && !(a->split && !a->order)) return (int)hipErrorInvalidValue;
   if (ntiles <= 0) return 0;
-  if (a->have != 0u) {
+  if (a->have != 0u && !a->tiles_done) {
     hipLaunchKernelGGL(k_frame_tiles, dim3((ntiles + 255) / 256), dim3(256), 0, st, *a, tiles_x, ntiles,
                        (uint8_t*)tile_bits);
     if ((e = hipGetLastError()) != hipSuccess) return (int)e;

@@ -1274,7 +1274,13 @@ int frame_buffers(rt_scene* s, int w, int h, hipStream_t st) {
 // The mesh's camera-ray lists for the launch's rows (k_frame_bins_count /
 // scan / k_frame_bins_fill). *ok = false: no lists for this camera (a mesh
 // vertex may lie at or behind the camera plane), the kernels traverse the BVH.
-int frame_bins(rt_scene* s, const rt_options* o, const Mapping& mp, hipStream_t st, bool* ok) {
+void records_launch(rt_scene* s, const rt_options* o, const Mapping& mp, const FastParams& p, bool split,
+                    RecordsLaunch& r);
+
+// rp (optional): the call's pixel-record parameters; the record tiles then
+// run inside the count launch and *rl holds the record launch (tiles_done)
+int frame_bins(rt_scene* s, const rt_options* o, const Mapping& mp, hipStream_t st, bool* ok,
+               const FastParams* rp = nullptr, bool split = false, RecordsLaunch* rl = nullptr) {
   *ok = false;
   if (!s->binnable) return RT_OK;
   BinsLaunch a;
@@ -1324,8 +1330,11 @@ int frame_bins(rt_scene* s, const rt_options* o, const Mapping& mp, hipStream_t 
     if ((rc = f.scan_tmp.alloc(bytes))) return rc;
   }
   bytes = f.scan_tmp.n;
-  if ((rc = rtmi_frame_bins_count(&a, f.scan_tmp.p, &bytes, st)))
+  int tiles_done = 0;
+  if (rp && rl) records_launch(s, o, mp, *rp, split, *rl);
+  if ((rc = rtmi_frame_bins_count(&a, f.scan_tmp.p, &bytes, st, rp && rl ? rl : nullptr, f.tiles.p, &tiles_done)))
     return fail(RT_E_DEVICE, "bin count launch failed: %s", hipGetErrorString((hipError_t)rc));
+  if (rp && rl) rl->tiles_done = tiles_done;
   // the first call of a row set under this camera reads its entry count and
   // sizes the entry buffer; later calls of the same set list the same faces
   const std::array<int64_t, 9> key = {w, o->height, mp.mode, mp.y0, mp.nrows, mp.step, mp.band_h, mp.rank, mp.world};
@@ -1350,9 +1359,8 @@ int frame_bins(rt_scene* s, const rt_options* o, const Mapping& mp, hipStream_t 
 
 // Pixel records of the launch's one-pixel groups and, with split, the lean /
 // general lists (k_frame_records).
-int frame_records(rt_scene* s, const rt_options* o, const Mapping& mp, const FastParams& p, bool split,
-                  hipStream_t st) {
-  RecordsLaunch r;
+void records_launch(rt_scene* s, const rt_options* o, const Mapping& mp, const FastParams& p, bool split,
+                    RecordsLaunch& r) {
   std::memset(&r, 0, sizeof r);
   r.mode = mp.mode;
   r.y0 = mp.y0;
@@ -1386,6 +1394,14 @@ int frame_records(rt_scene* s, const rt_options* o, const Mapping& mp, const Fas
   r.lean = s->fr.lean.p;
   r.heavy = s->fr.heavy.p;
   r.ctr = s->fr.ctr.p;
+}
+
+// rl: the launch frame_bins already started the tiles of (or nullptr)
+int frame_records(rt_scene* s, const rt_options* o, const Mapping& mp, const FastParams& p, bool split,
+                  hipStream_t st, const RecordsLaunch* rl) {
+  RecordsLaunch r;
+  if (rl) r = *rl;
+  else records_launch(s, o, mp, p, split, r);
   size_t bytes = 0;
   int e = rtmi_frame_records(&r, s->fr.tiles.p, nullptr, &bytes, st);
   if (e) return fail(RT_E_DEVICE, "pixel record scratch query failed: %s", hipGetErrorString((hipError_t)e));
@@ -1561,7 +1577,18 @@ int fill_fast(rt_scene* s, const rt_options* o, const Mapping& mp, float* fb, Fa
   // this call's camera-dependent data (nothing of it is kept from earlier calls)
   int rc;
   bool lists = false, masks = false;
-  if ((rc = frame_bins(s, o, mp, st, &lists))) return rc;
+  // two-class launch (one pixel per wave): the lean pixels — no camera ray
+  // can hit the mesh, every light a distant light whose shadow rays from the
+  // pixel provably miss it, no reflection — get a kernel of their own; not
+  // for the measuring launch of a launch order or instrumented launches
+  static const char* cost_dump = std::getenv("RTMI_COST_DUMP");
+  const unsigned sub = f32_subset(s, o);
+  const bool want_split = !(o->flags & (RT_FLAG_NO_SPLIT | RT_FLAG_COUNT_TRAVERSAL)) && !p.cost && !cost_dump &&
+                          s->nlight <= 8 && rtmi_lean_f32_blocks_per_cu(sub, f32_table_lds(s, o)) > 0;
+  RecordsLaunch rl;
+  rl.tiles_done = 0;
+  const bool records = pl.L == 64;  // records follow the lists (below)
+  if ((rc = frame_bins(s, o, mp, st, &lists, records ? &p : nullptr, want_split, records ? &rl : nullptr))) return rc;
   if (lists) {
     p.pix_off = s->fr.off.p;
     p.pix_ent = s->fr.ent.p;
@@ -1571,15 +1598,8 @@ int fill_fast(rt_scene* s, const rt_options* o, const Mapping& mp, float* fb, Fa
     if (masks) p.obj_pix = s->fr.omask.p;
   }
   if (!lists || pl.L != 64) return RT_OK;
-  // two-class launch (one pixel per wave): the lean pixels — no camera ray
-  // can hit the mesh, every light a distant light whose shadow rays from the
-  // pixel provably miss it, no reflection — get a kernel of their own; not
-  // for the measuring launch of a launch order or instrumented launches
-  static const char* cost_dump = std::getenv("RTMI_COST_DUMP");
-  const unsigned sub = f32_subset(s, o);
-  *split = !(o->flags & (RT_FLAG_NO_SPLIT | RT_FLAG_COUNT_TRAVERSAL)) && !p.cost && !cost_dump && s->nlight <= 8 &&
-           rtmi_lean_f32_blocks_per_cu(sub, f32_table_lds(s, o)) > 0;
-  if ((rc = frame_records(s, o, mp, p, *split, st))) return rc;
+  *split = want_split;
+  if ((rc = frame_records(s, o, mp, p, *split, st, rl.tiles_done ? &rl : nullptr))) return rc;
   p.pix_info = s->fr.info.p;
   return RT_OK;
 }
