@@ -124,6 +124,7 @@ struct RecordsLaunch {
   int32_t* heavy;           // capacity ngroups
   int32_t* ctr;
   int32_t tiles_done;       // host: the tile bits were written by the count launch
+  int32_t records_done;     // host: the records (+ tile class counts) were written by the fill launch
 };
 
 // object bins (rt_bins.h build_object_pixel_masks): world boxes of the objects
@@ -152,7 +153,11 @@ extern "C" {
 int rtmi_frame_bins_count(const rtmi::BinsLaunch* a, void* scan_tmp, size_t* scan_tmp_bytes, void* stream,
                           const rtmi::RecordsLaunch* tr = nullptr, void* tile_bits = nullptr,
                           int* tiles_done = nullptr);
-int rtmi_frame_bins_fill(const rtmi::BinsLaunch* a, void* stream);
+// r (optional): the call's pixel-record launch (its tiles done); the
+// records then run in the fill launch (tile_cls: the tile-ordered lists'
+// class counts, or nullptr) and *records_done = 1
+int rtmi_frame_bins_fill(const rtmi::BinsLaunch* a, void* stream, const rtmi::RecordsLaunch* r = nullptr,
+                         const void* tile_bits = nullptr, void* tile_cls = nullptr, int* records_done = nullptr);
 // records (+ lists); tile_bits: rtmi_frame_tile_bytes(ncols, nrows) bytes;
 // scratch: *scratch_bytes (query with scratch == nullptr)
 int rtmi_frame_records(const rtmi::RecordsLaunch* a, void* tile_bits, void* scratch, size_t* scratch_bytes,

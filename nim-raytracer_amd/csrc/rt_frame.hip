@@ -154,8 +154,7 @@ __global__ __launch_bounds__(256) void k_frame_bins_big(const BinsLaunch a) {
 // Per face again: its record offset into each listed pixel's list. The
 // slot comes from counting the pixel's count back down, so the counts are
 // zero again for the next call (no clearing pass).
-__global__ __launch_bounds__(256) void k_frame_bins_fill(const BinsLaunch a) {
-  const int t = (int)(blockIdx.x * 256u + threadIdx.x);
+__device__ __forceinline__ void bins_fill_body(const BinsLaunch& a, const int t) {
   if (t == 0) {  // read-ahead padding after the last list (rt_bins.h kBinPad)
     const int64_t total = a.off[a.scan_lo + a.scan_n - 1];
     for (int k = 0; k < kBinPad; ++k)
@@ -197,6 +196,9 @@ __global__ __launch_bounds__(256) void k_frame_bins_fill(const BinsLaunch a) {
     if (slot < a.cap) a.ent[slot] = rec;
     else atomicOr(&a.ctr[FC_OVERFLOW], 1);
   }
+}
+__global__ __launch_bounds__(256) void k_frame_bins_fill(const BinsLaunch a) {
+  bins_fill_body(a, (int)(blockIdx.x * 256u + threadIdx.x));
 }
 
 // The launch's pixel at launch column j, launch row k (rt_fast.h lane_pixel
@@ -299,13 +301,12 @@ __device__ __forceinline__ int pixel_class(const RecordsLaunch& a, const LaunchP
   if (!p.drawn) return 0;
   return (info & kPixCount) == 0u && ((info >> 24) & a.full) == a.full ? 1 : 2;
 }
-__global__ __launch_bounds__(256) void k_frame_records(const RecordsLaunch a, const uint8_t* tile_bits,
-                                                       unsigned long long* tile_cls) {
-  __shared__ bg::SkipGrid sg[8];
-  __shared__ unsigned long long wsum[4];
-  load_skip_grids(a, sg);
-  const int j = (int)blockIdx.x * kTileW + (int)(threadIdx.x & 63u);
-  const int k = (int)blockIdx.y * kTileH + (int)(threadIdx.x >> 6);
+// (bx, by): the block's tile; tiles_x tiles per launch row
+__device__ __forceinline__ void records_body(const RecordsLaunch& a, const uint8_t* tile_bits,
+                                             unsigned long long* tile_cls, int bx, int by, int tiles_x,
+                                             const bg::SkipGrid* sg, unsigned long long* wsum) {
+  const int j = bx * kTileW + (int)(threadIdx.x & 63u);
+  const int k = by * kTileH + (int)(threadIdx.x >> 6);
   const LaunchPix p = launch_pixel(a, j, k);
   int c = 0;
   if (p.valid) {
@@ -313,7 +314,7 @@ __global__ __launch_bounds__(256) void k_frame_records(const RecordsLaunch a, co
     const int32_t n = a.off[pix + 1] - a.off[pix];
     uint32_t info = n < (int32_t)kPixCount ? (uint32_t)n : kPixCount;
     if (n == 0 && a.have != 0u) {
-      const bool tile = tile_bits[blockIdx.y * gridDim.x + blockIdx.x] != 0;
+      const bool tile = tile_bits[by * tiles_x + bx] != 0;
       const unsigned bits = tile ? a.have : bg::pixel_skip_bits(a.cam, a.planes, a.nplanes, sg, a.nl, a.have, p.x, p.y);
       info |= bits << 24;
     }
@@ -324,7 +325,32 @@ __global__ __launch_bounds__(256) void k_frame_records(const RecordsLaunch a, co
   const unsigned long long ml = __ballot(c == 1), mh = __ballot(c == 2);
   if ((threadIdx.x & 63u) == 0) wsum[threadIdx.x >> 6] = ((unsigned long long)__popcll(ml) << 32) | __popcll(mh);
   __syncthreads();
-  if (threadIdx.x == 0) tile_cls[blockIdx.y * gridDim.x + blockIdx.x] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+  if (threadIdx.x == 0) tile_cls[by * tiles_x + bx] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+}
+__global__ __launch_bounds__(256) void k_frame_records(const RecordsLaunch a, const uint8_t* tile_bits,
+                                                       unsigned long long* tile_cls) {
+  __shared__ bg::SkipGrid sg[8];
+  __shared__ unsigned long long wsum[4];
+  load_skip_grids(a, sg);
+  records_body(a, tile_bits, tile_cls, (int)blockIdx.x, (int)blockIdx.y, (int)gridDim.x, sg, wsum);
+}
+
+// k_frame_bins_fill and k_frame_records in one launch: the records read the
+// list offsets and the tile bits (both written by earlier launches), never
+// the entries the fill pass writes, so the two are independent. Blocks
+// [0, fill_blocks) fill, the rest build one tile's records each.
+__global__ __launch_bounds__(256) void k_frame_fill_records(const BinsLaunch a, const RecordsLaunch r, int fill_blocks,
+                                                            int tiles_x, const uint8_t* tile_bits,
+                                                            unsigned long long* tile_cls) {
+  __shared__ bg::SkipGrid sg[8];
+  __shared__ unsigned long long wsum[4];
+  if ((int)blockIdx.x < fill_blocks) {
+    bins_fill_body(a, (int)(blockIdx.x * 256u + threadIdx.x));
+    return;
+  }
+  load_skip_grids(r, sg);
+  const int b = (int)blockIdx.x - fill_blocks;
+  records_body(r, tile_bits, tile_cls, b % tiles_x, b / tiles_x, tiles_x, sg, wsum);
 }
 
 // Exclusive scan of n packed counts by one block (n = the launch's tiles:
@@ -661,9 +687,19 @@ extern "C" int rtmi_frame_bins_count(const rtmi::BinsLaunch* a, void* scan_tmp, 
   return (int)hipGetLastError();
 }
 
-extern "C" int rtmi_frame_bins_fill(const rtmi::BinsLaunch* a, void* stream) {
-  const int blocks = (int)(((long long)a->nf * rtmi::kFaceLanes + 255) / 256);
-  hipLaunchKernelGGL(rtmi::k_frame_bins_fill, dim3(blocks > 0 ? blocks : 1), dim3(256), 0, (hipStream_t)stream, *a);
+extern "C" int rtmi_frame_bins_fill(const rtmi::BinsLaunch* a, void* stream, const rtmi::RecordsLaunch* r,
+                                    const void* tile_bits, void* tile_cls, int* records_done) {
+  const int blocks = std::max(1, (int)(((long long)a->nf * rtmi::kFaceLanes + 255) / 256));
+  const int tiles_x = r ? (r->ncols + rtmi::kTileW - 1) / rtmi::kTileW : 0;
+  const int ntiles = r ? tiles_x * ((r->nrows + rtmi::kTileH - 1) / rtmi::kTileH) : 0;
+  if (records_done) *records_done = 0;
+  if (r && records_done && ntiles > 0) {
+    hipLaunchKernelGGL(rtmi::k_frame_fill_records, dim3(blocks + ntiles), dim3(256), 0, (hipStream_t)stream, *a, *r,
+                       blocks, tiles_x, (const uint8_t*)tile_bits, (unsigned long long*)tile_cls);
+    *records_done = 1;
+  } else {
+    hipLaunchKernelGGL(rtmi::k_frame_bins_fill, dim3(blocks), dim3(256), 0, (hipStream_t)stream, *a);
+  }
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
   hipLaunchKernelGGL(rtmi::k_frame_bins_big<true>, dim3(kBigBlocks), dim3(256), 0, (hipStream_t)stream, *a);
@@ -700,17 +736,22 @@ extern "C" int rtmi_frame_records(const rtmi::RecordsLaunch* a, void* tile_bits,
     if (*scratch_bytes < 2 * tile_bytes) return (int)hipErrorInvalidValue;
     unsigned long long* tc = (unsigned long long*)scratch;
     unsigned long long* to = (unsigned long long*)((char*)scratch + tile_bytes);
-    hipLaunchKernelGGL(k_frame_records, dim3(tiles_x, tiles_y), dim3(256), 0, st, *a, (const uint8_t*)tile_bits, tc);
-    if ((e = hipGetLastError()) != hipSuccess) return (int)e;
+    if (!a->records_done) {
+      hipLaunchKernelGGL(k_frame_records, dim3(tiles_x, tiles_y), dim3(256), 0, st, *a, (const uint8_t*)tile_bits, tc);
+      if ((e = hipGetLastError()) != hipSuccess) return (int)e;
+    }
     hipLaunchKernelGGL(k_scan_tiles, dim3(1), dim3(1024), 0, st, (const unsigned long long*)tc, to, ntiles);
     if ((e = hipGetLastError()) != hipSuccess) return (int)e;
     hipLaunchKernelGGL(k_frame_class_write_tiles, dim3(tiles_x, tiles_y), dim3(256), 0, st, *a,
                        (const unsigned long long*)tc, (const unsigned long long*)to);
     return (int)hipGetLastError();
   }
-  hipLaunchKernelGGL(k_frame_records, dim3(tiles_x, tiles_y), dim3(256), 0, st, *a, (const uint8_t*)tile_bits,
-                     (unsigned long long*)nullptr);
-  if ((e = hipGetLastError()) != hipSuccess || !a->split) return (int)e;
+  if (!a->records_done) {
+    hipLaunchKernelGGL(k_frame_records, dim3(tiles_x, tiles_y), dim3(256), 0, st, *a, (const uint8_t*)tile_bits,
+                       (unsigned long long*)nullptr);
+    if ((e = hipGetLastError()) != hipSuccess) return (int)e;
+  }
+  if (!a->split) return 0;
   unsigned long long* blk = (unsigned long long*)scratch;
   unsigned long long* blk_off = (unsigned long long*)((char*)scratch + cnt_bytes);
   void* tmp = (char*)scratch + 2 * cnt_bytes;

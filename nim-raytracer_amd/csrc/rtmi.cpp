@@ -1351,8 +1351,22 @@ int frame_bins(rt_scene* s, const rt_options* o, const Mapping& mp, hipStream_t 
     }
     f.sized.push_back(key);
   }
-  if ((rc = rtmi_frame_bins_fill(&a, st)))
+  // the pixel records read the list offsets (ready now), not the entries:
+  // they share the fill launch when their tiles are done and their scratch
+  // is already sized (every call after a scene's first at this size)
+  const RecordsLaunch* fr = nullptr;
+  void* tile_cls = nullptr;
+  if (rp && rl && (rl->tiles_done || rl->have == 0u)) {
+    size_t need = 0;
+    if (rtmi_frame_records(rl, f.tiles.p, nullptr, &need, st) == 0 && f.cls.p && f.cls.n >= need) {
+      fr = rl;
+      tile_cls = rl->split && !rl->order ? (void*)f.cls.p : nullptr;
+    }
+  }
+  int records_done = 0;
+  if ((rc = rtmi_frame_bins_fill(&a, st, fr, f.tiles.p, tile_cls, &records_done)))
     return fail(RT_E_DEVICE, "bin fill launch failed: %s", hipGetErrorString((hipError_t)rc));
+  if (rl) rl->records_done = records_done;
   *ok = true;
   return RT_OK;
 }
@@ -1586,7 +1600,7 @@ int fill_fast(rt_scene* s, const rt_options* o, const Mapping& mp, float* fb, Fa
   const bool want_split = !(o->flags & (RT_FLAG_NO_SPLIT | RT_FLAG_COUNT_TRAVERSAL)) && !p.cost && !cost_dump &&
                           s->nlight <= 8 && rtmi_lean_f32_blocks_per_cu(sub, f32_table_lds(s, o)) > 0;
   RecordsLaunch rl;
-  rl.tiles_done = 0;
+  rl.tiles_done = rl.records_done = 0;
   const bool records = pl.L == 64;  // records follow the lists (below)
   if ((rc = frame_bins(s, o, mp, st, &lists, records ? &p : nullptr, want_split, records ? &rl : nullptr))) return rc;
   if (lists) {
@@ -1599,7 +1613,7 @@ int fill_fast(rt_scene* s, const rt_options* o, const Mapping& mp, float* fb, Fa
   }
   if (!lists || pl.L != 64) return RT_OK;
   *split = want_split;
-  if ((rc = frame_records(s, o, mp, p, *split, st, rl.tiles_done ? &rl : nullptr))) return rc;
+  if ((rc = frame_records(s, o, mp, p, *split, st, &rl))) return rc;  // (rl filled by frame_bins: lists)
   p.pix_info = s->fr.info.p;
   return RT_OK;
 }
