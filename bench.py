@@ -85,6 +85,9 @@ def parse():
     ap.add_argument("--bvh", default="sah", choices=["sah", "ploc"],
                     help="mesh BVH builder: host binned SAH (default) or device PLOC")
     ap.add_argument("--flags", type=int, default=0, help="rt_options.flags (1 = any-hit shadows)")
+    ap.add_argument("--precision", default="fp32", choices=["fp32", "fp64"],
+                    help="fp32 = the performance kernels (the headline); fp64 = the parity mode the Nim "
+                         "binding defaults to (bit-exact against the oracle): the cost of exactness")
     return ap.parse_args()
 
 
@@ -200,8 +203,9 @@ def main():
     ds = DeviceScene(scene, device=local, bvh_builder=RT_BVH_PLOC if args.bvh == "ploc" else RT_BVH_SAH)
     info = ds.info()
     setup_s = time.time() - t0
+    fp64 = args.precision == "fp64"
     opts = Options(width=W, height=H, antialias=Antialias(akGrid, m), bias=1e-4,
-                   precision=Precision.fp32, flags=args.flags)
+                   precision=Precision.fp64 if fp64 else Precision.fp32, flags=args.flags)
     stream = torch.cuda.current_stream()
     # the first frame of this scene and image size also allocates the
     # per-call buffers and reads the camera-ray list size once (every frame
@@ -262,7 +266,8 @@ def main():
     # node visits / triangle tests of one instrumented launch of the BVH path
     # (k_render_fast<true>, RT_FLAG_COUNT_TRAVERSAL | RT_FLAG_NO_BINNING) —
     # a model of what a per-ray BVH tracer would read, not the timed kernels
-    copts = dataclasses.replace(opts, flags=opts.flags | RT_FLAG_COUNT_TRAVERSAL | RT_FLAG_NO_BINNING)
+    copts = dataclasses.replace(opts, flags=opts.flags | RT_FLAG_COUNT_TRAVERSAL | RT_FLAG_NO_BINNING,
+                                precision=Precision.fp32)
     ds.render_bands_device(copts, local_buf, BAND_H, rank, world, stream=stream, stats=True)
     counters = ds.last_counters()
     for _ in range(max(0, args.warmup)):
@@ -301,7 +306,8 @@ def main():
     lean_k = {0: None, 1: "k_render_lean", 2: "k_render_lean1q (one-plane lean pixels)", 3: None}[kinds & 3]
     gen_k = {0: "k_render_fast<false>", 1: "k_render_gen", 2: "k_render_gen1 (one-plane general pixels)",
              3: None}[kinds >> 2 & 3]
-    kernel_desc = ("k_render_mix1 (one-plane scene: general pixels, then lean pixels, one merged kernel)"
+    kernel_desc = ("k_render<double> (fp64 parity kernel, one lane per pixel, BVH for every ray)" if fp64 else
+                   "k_render_mix1 (one-plane scene: general pixels, then lean pixels, one merged kernel)"
                    if kinds == 15 else f"{gen_k} + {lean_k} (two-class launch)" if lean_k else gen_k)
     # after the timed region, the same steps once more with RT_FLAG_TIMING:
     # HIP events inside the library split each call into its per-call
@@ -350,7 +356,7 @@ def main():
     # per-ray BVH tracer would read; these kernels skip most of it)
     bvh_model_bytes = (counters["lane_node_visits"] * 2 * SURVEY_BOX_BYTES
                        + counters["lane_tri_tests"] * SURVEY_TRI_BYTES + rows * W * PIXEL_BYTES)
-    workload_key = f"{args.config.lower()}_{W}x{H}_m{m}_world{world}"
+    workload_key = f"{args.config.lower()}_{W}x{H}_m{m}_world{world}" + ("_fp64" if fp64 else "")
     pmc = load_pmc(workload_key)
     roof = {"bound": "issue", "achieved": None, "peak": VALU_PEAK_GINST, "unit": "G wave64 VALU inst/s",
             "frac": None, "traffic": None}
@@ -403,12 +409,14 @@ def main():
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
-            "dtype": "f32",
+            "dtype": "f64" if fp64 else "f32",
             "data": {"bunny": "synthetic rays over the reference's bunny.geom fixture (69,451 triangles)",
                      "boxes2": "synthetic rays over the reference's boxes2.nim scene",
                      "torus": "synthetic rays over a deterministic procedural 1M-triangle torus"}[scene_name],
             "config": {
-                "workload": (f"{desc}, {W}x{H}, akGrid {m}x{m} = {m * m} spp, fp32, "
+                "workload": (f"{desc}, {W}x{H}, akGrid {m}x{m} = {m * m} spp, "
+                             + ("fp64 parity mode (k_render<double>: the reference's arithmetic, bit-exact "
+                                "against the oracle), " if fp64 else "fp32, ")
                              + (f"{BAND_H}-row bands round-robin over {world} ranks (one GPU each) + RCCL gather "
                                 "to rank 0" if distributed else "one whole-frame call per step on one GPU")
                              + "; every step builds its camera-dependent data on the device"),

@@ -300,6 +300,11 @@ int rt_scene_set_camera(rt_scene *scene, const double camera_to_world[16],
  * step and max_step must be powers of two with max_step >= step.
  * `out` receives the summed Stats of the call (may be NULL for the _device
  * forms, which then do not synchronise the stream).
+ * A call whose per-call camera-ray lists ran out of entry capacity (never
+ * expected: the capacity is sized from the device count) rendered an
+ * incomplete frame: the call that reads Stats (this one, or the next one
+ * that does when `out` is NULL) returns RT_E_DEVICE instead of RT_OK, and
+ * the next call rebuilds its buffers.
  */
 
 /* Host framebuffer form: fb_rgb is caller memory of fb_w*fb_h*3 floats with
@@ -478,7 +483,10 @@ int rt_scene_last_batch(rt_scene *scene, int64_t *batched_groups, int64_t *fallb
  * (0 the one-sample kernel, 1 the general batched kernel, 2 the one-plane
  * batched kernel, RT_FLAG_NO_GEN1); 3 in both: the merged one-plane kernel
  * (RT_FLAG_NO_MIX); bit 4: reflected rays compacted per wave (reflective
- * scenes, RT_FLAG_COMPACT). Host-side bookkeeping, no wait. */
+ * scenes, RT_FLAG_COMPACT); bits 8-15: lanes per lean pixel of a two-class
+ * call (4 or 16 for the one-plane lean kernels, 64 for one pixel per wave;
+ * 0 otherwise) — mask with 0x1f to compare the kernel kinds. Host-side
+ * bookkeeping, no wait. */
 int rt_scene_last_lean_kernel(rt_scene *scene, int32_t *kind);
 
 /* ---- helpers ----------------------------------------------------------- */

@@ -26,9 +26,11 @@ constexpr int kFaceLanes = 4;
 // pass), and one count per pixel of the launch's rows that the face's grown
 // projection meets (rt_bins.cpp build_pixel_bins, the same bounds).
 __device__ __forceinline__ void bins_count_body(const BinsLaunch& a, const int t) {
-  if (t == 0) {  // (not FC_BIG: other blocks append to it now; k_frame_bins_fill zeroes it)
+  if (t == 0) {  // (not FC_BIG: other blocks append to it now; k_frame_bins_fill zeroes it;
+                 // not FC_OVERFLOW: kept until the host reports it, rtmi.cpp report_overflow)
 #pragma unroll
-    for (int k = 0; k < FC_BIG; ++k) a.ctr[k] = 0;
+    for (int k = 0; k < FC_BIG; ++k)
+      if (k != FC_OVERFLOW) a.ctr[k] = 0;
   }
   const int i = t / kFaceLanes, q = t % kFaceLanes;
   if (i >= a.nf) return;

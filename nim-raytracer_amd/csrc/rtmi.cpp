@@ -18,6 +18,7 @@
 #include <cstring>
 #include <memory>
 #include <mutex>
+#include <set>
 #include <thread>
 #include <string>
 #include <vector>
@@ -213,14 +214,28 @@ struct rt_scene {
     DevBuf<unsigned char> tiles;   // per-tile shadow skips (k_frame_tiles)
     DevBuf<unsigned char> cls;     // the class counts' scratch (k_frame_class_count + scan)
     // launch row sets whose list entries `ent` is known to hold for the
-    // current camera (the first call of a row set reads its entry count)
-    std::vector<std::array<int64_t, 9>> sized;
+    // current camera (the first call of a row set reads its entry count);
+    // `full_sized`: a whole-frame row set was sized, and every row set's
+    // lists are a subset of the whole frame's (a pixel's list does not
+    // depend on which other rows a call covers), so no further reads
+    std::set<std::array<int64_t, 9>> sized;
+    bool full_sized = false;
     bool counted = false;          // the last launch's lean / general lists were counted on the device
+    bool listed = false;           // the last launch built camera-ray lists (its FC_OVERFLOW is meaningful)
+    int64_t test_cap = 0;          // test hook (rtmi_test_entry_cap): > 0 caps the entry capacity
+    // forget everything a call left: the next call re-zeroes the counts and
+    // re-reads its entry count (after a failed or overflowed call)
+    void invalidate() {
+      w = h = 0;
+      sized.clear();
+      full_sized = false;
+    }
     void release() {
       cnt.release(); off.release(); ent.release(); rect.release(); lean.release(); heavy.release(); ctr.release();
       proj.release(); info.release(); omask.release(); scan_tmp.release(); tiles.release();
       cls.release();
       sized.clear();
+      full_sized = false;
     }
   } fr;
   // object bins (rt_bins.h ObjBox), scenes of 4..64 objects
@@ -996,6 +1011,7 @@ extern "C" int rt_scene_set_camera(rt_scene* s, const double c2w[16], double fov
   std::memcpy(s->c2w, c2w, sizeof s->c2w);
   s->fov = fov_deg;
   s->fr.sized.clear();  // list entry counts change with the camera
+  s->fr.full_sized = false;
   s->orders.clear();    // measured per-group costs (launch order) too
   if (prev >= 0 && prev != s->device) (void)hipSetDevice(prev);
   if (e != hipSuccess) return fail(RT_E_DEVICE, "waiting for the scene's earlier calls: %s", hipGetErrorString(e));
@@ -1246,13 +1262,14 @@ FrameRows frame_rows(const Mapping& mp, int height) {
 int frame_buffers(rt_scene* s, int w, int h, hipStream_t st) {
   rt_scene::Frame& f = s->fr;
   if (f.w == w && f.h == h) return RT_OK;
-  HIP_TRY(hipStreamSynchronize(st));  // an earlier call may still read the old buffers
-  HIP_TRY(hipDeviceSynchronize());
+  // an earlier call may still read the old buffers: the call's stream waits
+  // on the scene's last call (render_device), whose aux-stream kernels are
+  // joined into its done event, so this one wait covers them all
+  HIP_TRY(hipStreamSynchronize(st));
   const size_t npx = (size_t)w * (size_t)h;
   const size_t nf = s->bin_tris.size();
   int rc;
-  f.w = f.h = 0;
-  f.sized.clear();
+  f.invalidate();
   if ((rc = f.cnt.alloc(npx + 1)) || (rc = f.off.alloc(npx + 1)) || (rc = f.info.alloc(npx)) ||
       (rc = f.lean.alloc(npx + 64)) || (rc = f.heavy.alloc(npx)) || (rc = f.ctr.alloc(FC_WORDS)) ||
       (rc = f.big.alloc(kBigCap)) ||
@@ -1308,7 +1325,7 @@ int frame_bins(rt_scene* s, const rt_options* o, const Mapping& mp, hipStream_t 
   a.cnt = f.cnt.p;
   a.off = f.off.p;
   a.ent = f.ent.p;
-  a.cap = (int64_t)f.ent.n;
+  a.cap = f.test_cap > 0 ? std::min<int64_t>(f.test_cap, (int64_t)f.ent.n) : (int64_t)f.ent.n;
   a.ctr = f.ctr.p;
   a.big = f.big.p;
   a.fmask = f.fmask.p;
@@ -1332,13 +1349,27 @@ int frame_bins(rt_scene* s, const rt_options* o, const Mapping& mp, hipStream_t 
   bytes = f.scan_tmp.n;
   int tiles_done = 0;
   if (rp && rl) records_launch(s, o, mp, *rp, split, *rl);
+  // From the count launch until the fill launch is queued, the per-pixel
+  // counts are non-zero (the fill pass counts them back down): any failure
+  // in between leaves the frame buffers invalid, so the next call re-zeroes
+  // them and re-reads its entry count.
+  struct Invalidate {
+    rt_scene::Frame& f;
+    bool armed = true;
+    ~Invalidate() {
+      if (armed) f.invalidate();
+    }
+  } guard{f};
   if ((rc = rtmi_frame_bins_count(&a, f.scan_tmp.p, &bytes, st, rp && rl ? rl : nullptr, f.tiles.p, &tiles_done)))
     return fail(RT_E_DEVICE, "bin count launch failed: %s", hipGetErrorString((hipError_t)rc));
+  f.listed = true;
   if (rp && rl) rl->tiles_done = tiles_done;
   // the first call of a row set under this camera reads its entry count and
-  // sizes the entry buffer; later calls of the same set list the same faces
+  // sizes the entry buffer; later calls of the same set list the same faces,
+  // and once the whole frame is sized every row set is (a subset of it)
   const std::array<int64_t, 9> key = {w, o->height, mp.mode, mp.y0, mp.nrows, mp.step, mp.band_h, mp.rank, mp.world};
-  if (std::find(f.sized.begin(), f.sized.end(), key) == f.sized.end()) {
+  const bool whole = mp.mode == 0 ? (mp.y0 == 0 && mp.step == 1 && mp.nrows == o->height) : mp.world == 1;
+  if (!f.full_sized && !f.sized.count(key)) {
     int32_t total = 0;
     HIP_TRY(hipMemcpyAsync(&total, f.off.p + a.scan_lo + a.scan_n - 1, sizeof total, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
@@ -1347,9 +1378,10 @@ int frame_bins(rt_scene* s, const rt_options* o, const Mapping& mp, hipStream_t 
     if (f.ent.n < need) {
       if ((rc = f.ent.alloc(need + need / 4))) return rc;
       a.ent = f.ent.p;
-      a.cap = (int64_t)f.ent.n;
+      a.cap = f.test_cap > 0 ? std::min<int64_t>(f.test_cap, (int64_t)f.ent.n) : (int64_t)f.ent.n;
     }
-    f.sized.push_back(key);
+    if (whole) f.full_sized = true;
+    else f.sized.insert(key);
   }
   // the pixel records read the list offsets (ready now), not the entries:
   // they share the fill launch when their tiles are done and their scratch
@@ -1366,6 +1398,7 @@ int frame_bins(rt_scene* s, const rt_options* o, const Mapping& mp, hipStream_t 
   int records_done = 0;
   if ((rc = rtmi_frame_bins_fill(&a, st, fr, f.tiles.p, tile_cls, &records_done)))
     return fail(RT_E_DEVICE, "bin fill launch failed: %s", hipGetErrorString((hipError_t)rc));
+  guard.armed = false;
   if (rl) rl->records_done = records_done;
   *ok = true;
   return RT_OK;
@@ -1720,10 +1753,19 @@ bool lean1_ok(const rt_scene* s, const rt_options* o, const FastParams& p, unsig
 
 int launch(rt_scene* s, const rt_options* o, const Mapping& mp, float* d_out, hipStream_t st, bool reduce) {
   int blocks = 1;
+  // what rt_scene_last_split / _last_batch report describes THIS call, even
+  // when it returns early or runs the float64 kernel
+  s->fr.counted = false;
+  s->fr.listed = false;
+  s->last_lean = 0;
+  s->last_lean_kind = 0;
+  s->last_general = 0;
+  s->last_batched = 0;
   if (o->precision == RT_FP64) {
     RenderParams<double> p;
     fill_params<double>(s, s->f64, o, mp, d_out, p, &blocks);
     if (o->flags & RT_FLAG_TIMING) HIP_TRY(hipEventRecord(s->tev[1], st));
+    s->last_general = p.ngroups;
     if (p.ngroups == 0) return RT_OK;
     if (p.aa_kind >= RT_AA_JITTERED) {
       const size_t need = (size_t)blocks * 256 * 2 * (size_t)p.spp;
@@ -1748,6 +1790,7 @@ int launch(rt_scene* s, const rt_options* o, const Mapping& mp, float* d_out, hi
     int rc = fill_fast(s, o, mp, d_out, p, &blocks, &measuring, st, &split);
     if (rc) return rc;
     if (o->flags & RT_FLAG_TIMING) HIP_TRY(hipEventRecord(s->tev[1], st));
+    s->last_general = p.ngroups;
     if (p.ngroups == 0) return RT_OK;
     // diagnostic (tools/cost_map.py): RTMI_COST_DUMP=<file> records every
     // pixel group's duration (s_memtime cycles) of this launch into <file>
@@ -1923,10 +1966,28 @@ int launch(rt_scene* s, const rt_options* o, const Mapping& mp, float* d_out, hi
   return RT_OK;
 }
 
+// A camera-ray list fill that ran out of entry capacity (FC_OVERFLOW, set by
+// rt_frame.hip's fill passes, kept until reported here) left lists with
+// unwritten entries: the frame of that call is wrong, so the call that reads
+// Stats fails (RT_E_DEVICE) instead of returning RT_OK, and the frame
+// buffers are invalidated so the next call re-reads its entry count.
+// Reported once: the flag is cleared here (the caller has waited for the
+// scene's calls; the scene mutex is held).
+int report_overflow(rt_scene* s, int32_t flag) {
+  if (!flag) return RT_OK;
+  s->fr.invalidate();
+  const int32_t zero = 0;
+  HIP_TRY(hipMemcpy(s->fr.ctr.p + FC_OVERFLOW, &zero, sizeof zero, hipMemcpyHostToDevice));
+  return fail(RT_E_DEVICE, "camera-ray list entries overflowed their buffer (the frame is incomplete)");
+}
+
 int read_stats(rt_scene* s, hipStream_t st, rt_stats* out) {
   unsigned long long h[kStatSlots];
+  int32_t ovf = 0;
   HIP_TRY(hipMemcpyAsync(h, s->acc(), sizeof h, hipMemcpyDeviceToHost, st));
+  if (s->fr.ctr.p) HIP_TRY(hipMemcpyAsync(&ovf, s->fr.ctr.p + FC_OVERFLOW, sizeof ovf, hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
+  if (int rc = report_overflow(s, ovf)) return rc;
   out->num_primary_rays = h[STAT_PRIMARY];
   // renderer.nim:54-56 counts one test per object per trace call, and every
   // trace call is a primary, shadow or reflection ray: the float32 kernel
@@ -2145,7 +2206,7 @@ int last_lists(rt_scene* s, int64_t* lean, int64_t* general) {
   int32_t c[FC_WORDS];
   HIP_TRY(hipEventSynchronize(s->done));
   HIP_TRY(hipMemcpy(c, s->fr.ctr.p, sizeof c, hipMemcpyDeviceToHost));
-  if (c[FC_OVERFLOW]) return fail(RT_E_DEVICE, "camera-ray list entries overflowed their buffer");
+  if (int rc = report_overflow(s, c[FC_OVERFLOW])) return rc;
   *lean = c[FC_LEAN];
   *general = c[FC_HEAVY];
   return RT_OK;
@@ -2196,6 +2257,15 @@ extern "C" int rt_scene_last_counters(rt_scene* s, rt_traversal_counters* out) {
 }
 
 // ---- test hooks (tests/test_gpu_frame.py; not part of include/rtmi.h) ----
+
+// Caps the camera-ray list entry capacity the fill passes may use (0: no
+// cap), so a test can force FC_OVERFLOW and check that the call fails.
+extern "C" int rtmi_test_entry_cap(rt_scene* s, int64_t cap) {
+  if (!s || cap < 0) return fail(RT_E_INVALID, "bad argument");
+  std::lock_guard<std::mutex> lk(s->mu);
+  s->fr.test_cap = cap;
+  return RT_OK;
+}
 
 // The last render call's device-built camera-ray lists and pixel records
 // (image-sized arrays; only the call's pixels are defined). off: w*h + 1,

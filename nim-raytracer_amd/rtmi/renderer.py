@@ -5,10 +5,12 @@
                                                  renderer.nim:162-211
 plus the whole-frame and multi-GPU forms that replace the scanline worker
 pool (src/raytracer.nim:25-109, src/concurrency/workerpool.nim) with one GPU
-dispatch. `scene` here is a DeviceScene: the reference's Scene flattened and
+dispatch. `scene` is the reference's Scene (renderLine caches its device copy,
+as the Nim binding in INTEGRATION.md does) or a DeviceScene: the Scene flattened and
 uploaded once (BVH built) — the Nim shim in INTEGRATION.md does the same.
 """
 import ctypes as C
+import threading
 
 import numpy as np
 
@@ -167,9 +169,91 @@ def unshard_bands_device(d_gathered, d_fb, width, height, band_h, world, stream=
                                         int(height), int(band_h), int(world), _stream(stream)))
 
 
-def renderLine(scene: DeviceScene, opts: Options, fb, y, step=1, maxStep=1) -> Stats:
-    """renderer.nim:162-211 — one scanline (and its step x step blocks)."""
-    return scene.render_lines(opts, fb, y, y + 1, step, maxStep)
+def _shape_key(scene: Scene):
+    """Everything of a Scene except the camera that the device copy holds:
+    object transforms, materials, sphere radii, the FULL box bounds (all of
+    vmin / vmax, geom.nim:169-170), mesh sizes, lights, background — the
+    fingerprint INTEGRATION.md's Nim binding (shapeHash) keeps. Mesh vertices
+    edited in place (same sizes) are not hashed per call: invalidateScene."""
+    from .scene import Box, DistantLight, Sphere, TriangleMesh
+    parts = []
+    for o in scene.objects:
+        g = o.geometry
+        parts += [type(g).__name__, np.asarray(g.objectToWorld, np.float64).tobytes(),
+                  np.asarray(g.worldToObject, np.float64).tobytes(),
+                  np.asarray(o.material.albedo, np.float64).tobytes(), float(o.material.reflection)]
+        if isinstance(g, Sphere):
+            parts.append(g.r)
+        elif isinstance(g, Box):
+            parts += [g.vmin.tobytes(), g.vmax.tobytes()]
+        elif isinstance(g, TriangleMesh):
+            parts += [g.vertices.shape[0], g.faces.shape[0], id(g.vertices), id(g.faces)]
+    for li in scene.lights:
+        parts += [type(li).__name__, np.asarray(li.color, np.float64).tobytes(), float(li.intensity),
+                  np.asarray(li.dir if isinstance(li, DistantLight) else li.pos, np.float64).tobytes()]
+    parts.append(np.asarray(scene.bgColor, np.float64).tobytes())
+    return tuple(parts)
+
+
+class _DeviceCache:
+    """The Nim binding's `deviceScene` in Python: one device
+    copy per Scene, created on first use, re-created when the shape key
+    changes, its camera pushed (rt_scene_set_camera) when Scene.cameraToWorld
+    / fov moved — renderLine re-reads them on every call (renderer.nim:135-136,
+    150-153). Re-entrant like renderLine (the pool calls it from
+    countProcessors() threads at once, workerpool.nim:72-99): lookups,
+    creation and camera pushes hold one lock; the render call itself runs
+    outside it (the library serialises calls per scene)."""
+
+    def __init__(self):
+        self._lock = threading.Lock()
+        self._entries = {}  # id(scene) -> [scene, DeviceScene, shape key, camera bytes, fov]
+
+    def get(self, scene: Scene, device=0) -> "DeviceScene":
+        shape = _shape_key(scene)
+        cam = np.asarray(scene.cameraToWorld, np.float64).tobytes()
+        fov = float(scene.fov)
+        with self._lock:
+            e = self._entries.get(id(scene))
+            if e is not None and e[0] is scene:
+                if e[2] != shape:  # geometry / materials / lights changed
+                    e[1].close()
+                    e[1] = DeviceScene(scene, device)
+                    e[2], e[3], e[4] = shape, cam, fov
+                elif e[3] != cam or e[4] != fov:  # the camera moved: the next call renders it
+                    e[1].set_camera(scene.cameraToWorld, fov)
+                    e[3], e[4] = cam, fov
+                return e[1]
+            ds = DeviceScene(scene, device)
+            self._entries[id(scene)] = [scene, ds, shape, cam, fov]
+            return ds
+
+    def invalidate(self, scene: Scene):
+        with self._lock:
+            e = self._entries.pop(id(scene), None)
+        if e is not None:
+            e[1].close()
+
+
+_cache = _DeviceCache()
+
+
+def deviceScene(scene: Scene, device=0) -> "DeviceScene":
+    """The cached device copy of `scene` (INTEGRATION.md deviceScene)."""
+    return _cache.get(scene, device)
+
+
+def invalidateScene(scene: Scene):
+    """After editing mesh vertices / faces in place (same sizes)."""
+    _cache.invalidate(scene)
+
+
+def renderLine(scene, opts: Options, fb, y, step=1, maxStep=1) -> Stats:
+    """renderer.nim:162-211 — one scanline (and its step x step blocks).
+    `scene` is the reference's Scene (its device copy is cached and kept in
+    step with the Scene's camera, as the Nim binding does) or a DeviceScene."""
+    ds = scene if isinstance(scene, DeviceScene) else deviceScene(scene)
+    return ds.render_lines(opts, fb, y, y + 1, step, maxStep)
 
 
 def render_frame(scene: DeviceScene, opts: Options, fb=None):
@@ -392,5 +476,5 @@ def _stream(stream):
     return C.c_void_p(int(stream.cuda_stream) or None)
 
 
-__all__ = ["DeviceScene", "RtmiError", "band_rows", "device_count", "initRenderer", "ppm_encode_device",
-           "renderLine", "render_frame", "unshard_bands_device", "write_ppm_device"]
+__all__ = ["DeviceScene", "RtmiError", "band_rows", "device_count", "deviceScene", "initRenderer", "invalidateScene",
+           "ppm_encode_device", "renderLine", "render_frame", "unshard_bands_device", "write_ppm_device"]
