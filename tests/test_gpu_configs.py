@@ -6,9 +6,11 @@ float64 BVH whose answers — closest t, lowest face on ties, every Stats count
 geom.nim:339-358; tests/test_oracle_bvh.py proves the equality), so the
 frames below are the reference algorithm's at the benchmark's sample counts.
 
-Tolerance (float32 performance path, DESIGN.md "Parity"): per pixel the
-largest channel error |gpu - oracle| <= 2e-3 on >= 99.5 % of the pixels and a
-mean <= 2e-4; primary-ray counts exact; shadow-ray and hit counts within
+Tolerance (float32 performance path, DESIGN.md "Parity"; per config below,
+set from the measured error distributions): per pixel the largest channel
+error |gpu - oracle| <= 2e-3 on >= 99.95 % of the pixels (99.99 % at
+256+ spp), <= 1e-4 on >= 98-99.95 %, mean <= 1e-5 (1e-6 for C3);
+primary-ray counts exact; shadow-ray, hit and intersection-test counts within
 1e-4 relative (a float32 camera ray that lands on the other side of a
 silhouette than the float64 one changes one hit and its two shadow rays).
 
@@ -52,11 +54,22 @@ def _log(what, err):
                                 "within_1e-4": float((err <= 1e-4).mean())}) + "\n")
 
 
-def _check(got, ref, what, frac=0.995, tol=2e-3, mean_tol=2e-4):
+def _check(got, ref, what, frac=0.9995, tol=2e-3, mean_tol=1e-5, fine_frac=None, fine_tol=1e-4):
+    """Per pixel the largest channel error |gpu - oracle|: at least `frac` of
+    the pixels within `tol`, at least `fine_frac` within `fine_tol`, and the
+    mean at most `mean_tol`. The defaults are set from the measured error
+    distributions (RTMI_PARITY_LOG, round 4 on MI355X: the 256-spp 1080p C3
+    frame has 99.998 % of its pixels within 2e-3, 99.978 % within 1e-4, mean
+    1.9e-7); the remaining pixels are silhouettes and shadow edges where a
+    float32 sample lands on the other side of an edge than the float64 one
+    (one flipped sample of m*m moves a pixel by up to ~1/(m*m))."""
     err = np.abs(got.astype(np.float64) - ref.astype(np.float64)).max(axis=-1)
     _log(what, err)
     ok = float((err <= tol).mean())
     assert ok >= frac, f"{what}: only {ok:.5f} of pixels within {tol} (max {err.max():.3g})"
+    if fine_frac is not None:
+        fine = float((err <= fine_tol).mean())
+        assert fine >= fine_frac, f"{what}: only {fine:.5f} of pixels within {fine_tol}"
     assert err.mean() <= mean_tol, f"{what}: mean abs err {err.mean():.3g}"
     return ok, float(err.max())
 
@@ -107,7 +120,7 @@ def test_c1_512_every_pixel(gpu):
     got64, st64 = _gpu(ds, _opts(512, 512, 1, Precision.fp64))
     assert np.array_equal(got64, ref) and st64 == rst
     got32, st32 = _gpu(ds, _opts(512, 512, 1))
-    _check(got32, ref, "C1 fp32")
+    _check(got32, ref, "C1 fp32", fine_frac=0.9995)
     _counts_close(st32, rst, rel=2e-3)
 
 
@@ -121,7 +134,7 @@ def test_c2_1080p_64spp_rows(gpu):
     assert st.numPrimaryRays == 1920 * 1080 * 64
     rows = [120, 300, 420, 540, 600, 700, 820, 1000]
     ref, rst = _oracle_rows(sc, o, rows, bvh=False)
-    _check(got[rows], ref[rows], "C2 rows")
+    _check(got[rows], ref[rows], "C2 rows", fine_frac=0.998)
     _counts_close(_row_stats(ds, o, rows), rst)
 
 
@@ -137,7 +150,7 @@ def test_c3_256spp_whole_frame(gpu):
     lean, general = ds.last_split()
     assert lean > 0 and general > 0 and lean + general == 480 * 270
     ref, rst = _oracle_rows(sc, o, list(range(270)))
-    _check(got, ref, "C3 480x270")
+    _check(got, ref, "C3 480x270", frac=0.9999, fine_frac=0.999, mean_tol=1e-6)
     _counts_close(st, rst)
 
 
@@ -153,7 +166,7 @@ def test_c3_1080p_whole_frame(gpu):
     assert ds.last_lean_kernel() == 3 | 3 << 2, ds.last_lean_kernel()
     assert st.numPrimaryRays == 1920 * 1080 * 256
     ref, rst = _oracle_rows(sc, o, list(range(1080)))
-    _check(got, ref, "C3 1080p whole frame")
+    _check(got, ref, "C3 1080p whole frame", frac=0.9999, fine_frac=0.999, mean_tol=1e-6)
     _counts_close(st, rst)
 
 
@@ -169,7 +182,7 @@ def test_c3_1080p_rows(gpu):
     assert st.numPrimaryRays == 1920 * 1080 * 256
     rows = [200, 380, 470, 520, 560, 610, 680, 900]
     ref, rst = _oracle_rows(sc, o, rows)
-    _check(got[rows], ref[rows], "C3 rows")
+    _check(got[rows], ref[rows], "C3 rows", frac=0.9999, fine_frac=0.999, mean_tol=1e-6)
     _counts_close(_row_stats(ds, o, rows), rst)
 
 
@@ -199,7 +212,7 @@ def test_c4_4k_1024spp(gpu):
     img, st = _properties(ds, o, 3840 * 2160 * 1024)
     rows = [1000, 1240]
     ref, rst = _oracle_rows(sc, o, rows)
-    _check(img[rows], ref[rows], "C4 rows")
+    _check(img[rows], ref[rows], "C4 rows", frac=0.9999, fine_frac=0.998, mean_tol=2e-6)
     _counts_close(_row_stats(ds, o, rows), rst)
 
 
@@ -213,5 +226,5 @@ def test_c5_torus_4k_4096spp(gpu):
     img, st = _properties(ds, o, 3840 * 2160 * 4096)
     rows = [1150]
     ref, rst = _oracle_rows(sc, o, rows)
-    _check(img[rows], ref[rows], "C5 row")
+    _check(img[rows], ref[rows], "C5 row", frac=0.9999, fine_frac=0.98)
     _counts_close(_row_stats(ds, o, rows), rst)
