@@ -213,8 +213,12 @@ struct FastParams {
   const FLight* lights;
   const BvhNode* tree;              // nodes (child refs = byte offsets into tree) then TriFast records
   const float* normals;
-  const int32_t* pix_off;          // pixel lists of the mesh (rt_bins.h): y * width + x -> [off, off+1)
-  const int32_t* pix_ent;          //   ... of TriFast byte offsets; nullptr: BVH for camera rays
+  // pixel lists of the mesh (rt_frame.h): pixel y * width + x lists
+  // min(n, 2^slot_lg) TriFast byte offsets at pix_slots[pix << slot_lg ..],
+  // n = pix_cnt[pix] & kPixCount (n > 2^slot_lg: the list overflowed, the
+  // pixel's camera rays take the BVH); pix_slots nullptr: BVH for camera rays
+  const int32_t* pix_slots;
+  const uint32_t* pix_cnt;
   const LightGrid* grids;          // per light, or nullptr: BVH for shadow rays
   const int32_t* grid_off;
   const int32_t* grid_ent;
@@ -248,6 +252,7 @@ struct FastParams {
   uint32_t tx_magic;               // g / tiles_x == (g * tx_magic) >> tx_shift for 0 <= g < 2^31
   int32_t tx_shift;
   int32_t stat_flush;              // work items between flushes of the 32-bit wave Stats counters
+  int32_t slot_lg;                 // pixel list slots per pixel: 2^slot_lg
   // per-pixel shadow lists (rt_bins.h build_shadow_skips): pix_sl[2 (pixel *
   // pix_sl_nl + light)] = start in pix_sl_ent, [.. + 1] = count (-1: none)
   const int32_t* pix_sl;
@@ -257,7 +262,7 @@ struct FastParams {
   const int32_t* order2;
   int32_t ngroups2, shards2;
   // two-class launches: the entry counts of the lists at order / order2,
-  // counted on the device by this call's k_frame_records (rt_frame.h), or
+  // counted on the device by this call's k_frame_build2 (rt_frame.h), or
   // nullptr (the lists' lengths are ngroups / ngroups2, items of the kernel)
   const int32_t* list_n;
   const int32_t* list_n2;

@@ -554,15 +554,22 @@ __device__ __forceinline__ unsigned long long mesh_search(KP p, const FObj& ob, 
     boff = p->grid_off;
     bent = p->grid_ent + G.ent_base;
   }
-  if (boff) {  // up to 4 distinct bins per wave; lanes left over take the BVH
-    unsigned long long todo = bal(part && bin >= 0);
+  if (bent) {  // up to 4 distinct bins per wave; lanes left over take the BVH
+    unsigned long long todo = bal(part && bin >= 0), ovf = 0ull;
     for (int it = 0; it < 4 && todo != 0ull; ++it) {
       const int kb = __builtin_amdgcn_readlane(bin, (int)__builtin_ctzll(todo));
-      todo &= ~bal(bin == kb);
-      list_search<COUNT>(p, bent, cp(boff)[kb], cp(boff)[kb + 1], ro, rd, ex, stop, key, tc, ws);
+      const unsigned long long mk = bal(bin == kb);
+      todo &= ~mk;
+      if (boff) {  // a light-grid cell
+        list_search<COUNT>(p, bent, cp(boff)[kb], cp(boff)[kb + 1], ro, rd, ex, stop, key, tc, ws);
+      } else {     // a pixel list (rt_frame.h slots); past its slots the BVH serves the pixel
+        const int n = (int)(at(p->pix_cnt, kb) & kPixCount), b = kb << p->slot_lg;
+        if (n > (1 << p->slot_lg)) ovf |= mk;
+        else list_search<COUNT>(p, bent, b, b + n, ro, rd, ex, stop, key, tc, ws);
+      }
     }
     // done: binned lanes (their bin was searched) and lanes off the grid
-    tc = (lane_in(todo) || !(bin >= 0 || nohit)) ? tc : -1.0f;
+    tc = (lane_in(todo | ovf) || !(bin >= 0 || nohit)) ? tc : -1.0f;
   }
   traverse<COUNT>(p, ob.root, ro, rd, sr, ex, stop, key, tc, ws);
   return key;
@@ -634,13 +641,12 @@ __device__ __forceinline__ Hit trace(KP p, F3 o, F3 d, float tmax, bool active, 
       // pixel's shadow skip bit for this light is set) the mesh is skipped
       // before the AABB gate (the gate's verdict cannot matter).
       int bin = -1;                        // this lane's bin, -1: none
-      const int32_t* boff = nullptr;
+      const int32_t* boff = nullptr;       // light-grid cells: CSR offsets; pixel lists: slots (boff == nullptr)
       const int32_t* bent = nullptr;
       bool nohit = false;                  // off every listed face
-      if ((F & F_MESH) && !shadow && p->pix_off && pix >= 0) {
+      if ((F & F_MESH) && !shadow && p->pix_slots && pix >= 0) {
         bin = pix;
-        boff = p->pix_off;
-        bent = p->pix_ent;
+        bent = p->pix_slots;
       }
       // no_mesh (wave-uniform, the caller's pixel record): no lane can hit the mesh
       const bool skip = no_mesh;
@@ -1681,9 +1687,11 @@ __device__ __forceinline__ bool gen_batch(KP p, const GroupPix& gp, int it0, con
         nomask[k] = 0ull;
         anyp |= bal(part);
       }
-      if (anyp != 0ull) {  // the wave's one pixel: one list for every sample
+      if (anyp != 0ull) {  // the wave's one pixel: one list for every sample (gen_batch's caller
+                           // sends a pixel whose list overflowed its slots to the one-sample loop)
         const int pu = __builtin_amdgcn_readfirstlane(gp.y * p->width + gp.x);
-        list_search_batch<S, true>(p, p->pix_ent, cp(p->pix_off)[pu], cp(p->pix_off)[pu + 1], (1u << S) - 1u,
+        const int b = pu << p->slot_lg;
+        list_search_batch<S, true>(p, p->pix_slots, b, b + (int)(pinfo & kPixCount), (1u << S) - 1u,
                                    ro, rd, unused, nomask, key, unused, tc);
       }
 #pragma unroll
@@ -1989,7 +1997,8 @@ __device__ __forceinline__ bool gen1_batch(KP p, const GroupPix& gp, int it0, un
     if (anyp != 0ull) {
       const KP q = params();
       const int pu = __builtin_amdgcn_readfirstlane(gp.y * q->width + gp.x);
-      list_search_batch<S, true>(q, q->pix_ent, cp(q->pix_off)[pu], cp(q->pix_off)[pu + 1], (1u << S) - 1u,
+      const int b = pu << q->slot_lg;
+      list_search_batch<S, true>(q, q->pix_slots, b, b + (int)(pinfo & kPixCount), (1u << S) - 1u,
                                  ro, rd, unused, nomask, key, unused, tc);
     }
 #pragma unroll
@@ -3203,7 +3212,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RTMI_GEN_WA
     Stats32 wi;
 #pragma unroll
     for (int k = 0; k < kStatSlots; ++k) wi.v[k] = 0u;
-    bool ok = true;
+    // a pixel list past its slots (rt_frame.h): the one-sample loop, whose
+    // camera rays take the BVH for this pixel
+    bool ok = (pinfo & kPixCount) <= (1u << p->slot_lg);
     int it = 0;
     for (; ok && it + kGenBatch <= iters; it += kGenBatch) ok = gen_batch<F, kGenBatch>(p, gp, it, tb, pinfo, ls, acc, wi);
     for (; ok && it < iters; ++it) ok = gen_batch<F, 1>(p, gp, it, tb, pinfo, ls, acc, wi);
@@ -3277,7 +3288,9 @@ __device__ __forceinline__ void gen1_loop(KP p, LdsF* ls, Stats32& ws, unsigned 
     Stats32 wi;
 #pragma unroll
     for (int k = 0; k < kStatSlots; ++k) wi.v[k] = 0u;
-    bool ok = true;
+    // a pixel list past its slots (rt_frame.h): the one-sample loop, whose
+    // camera rays take the BVH for this pixel
+    bool ok = (pinfo & kPixCount) <= (1u << p->slot_lg);
     for (int it = 0; ok && it < iters; it += kGenBatch) ok = gen1_batch<kGenBatch, NL>(p, gp, it, pinfo, acc, wi);
     if (params()->flags & RT_DEV_FLAG_FALLBACK) ok = false;  // test hook (RT_FLAG_BATCH_FALLBACK)
     if (ok) {

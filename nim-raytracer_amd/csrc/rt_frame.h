@@ -8,25 +8,32 @@
 // camera is kept from one render call to the next. What is built once per
 // scene (rt_scene_create) depends only on the scene's geometry and lights:
 // the BVH, the light grids and their occupancy prefix sums, the faces'
-// float64 vertices. Each render call runs, on its own stream, in order:
-//   k_frame_bins_count   per face: its pixel rectangle, a SAT test per pixel
-//                        of the launch's rows, one atomic count per listed pixel
-//                        (faces of more than kBigFace pixels: onto the big list)
-//   k_frame_bins_big     the big faces' pixels spread over the whole grid
-//   rocprim exclusive scan of the counts -> per-pixel list offsets
-//   k_frame_bins_fill    per face again: scatter its record offset into each
-//                        listed pixel's list (the pixels are the count pass's
-//                        per-face bit mask; the counts return to zero)
-//   k_frame_bins_big     the same for the big faces
-//   k_frame_tiles        per 64 x 4 tile of the launch: the shadow skips the
-//                        tile's pixels share (one test for the whole tile)
-//   k_frame_records      per pixel of the launch: the record (the tile's skip
-//                        bits, or the pixel's own test)
-//   k_frame_class_count  per block of groups in launch order: its lean and
-//                        general counts; a rocprim scan of them; then
-//   k_frame_class_write  the groups written to the lean and general lists at
-//                        their blocks' offsets (wave ballot + mbcnt ranks) —
-//                        the lists in launch order, no global atomics
+// float64 vertices. Each render call runs, on its own stream, TWO build
+// launches before its render kernels (round 4; round 3 took ten):
+//   k_frame_build1   blocks [0, face_blocks): per face (kFaceLanes threads)
+//                    its pixel rectangle and, for a face of <= kBigFace
+//                    pixels, a SAT test per pixel of the launch; a listed
+//                    pixel's counter hands out its slot (atomicAdd) and the
+//                    face's record offset goes straight into the pixel's
+//                    fixed block of 2^slot_lg slots — no count / scan / fill
+//                    passes. Larger faces go onto the huge list.
+//                    the other blocks: per 64 x 4 tile of the launch, the
+//                    shadow skips its pixels share (one test for the tile) and
+//                    the tile's look-back status word zeroed; block 0 also
+//                    zeroes the render kernels' queue heads + Stats words.
+//   k_frame_build2   persistent blocks over the launch's tiles in order: per
+//                    pixel its huge faces (the tile's share of the huge list,
+//                    a SAT test each, appended after the small faces), its
+//                    record (list length + skip bits: the tile's, or the
+//                    pixel's own test), its counter zeroed for the next call;
+//                    then the lean / general lists in tile order by a
+//                    single-pass decoupled look-back over the tiles (one 8-byte
+//                    status granule per tile, agent-scope sc1 stores / polls:
+//                    no global atomic counter, no scan launch).
+// A pixel with more listed faces than its 2^slot_lg slots keeps its true
+// count in the record; the render kernels then traverse the BVH for that
+// pixel's camera rays (the same answers, rt_fast.h mesh_search) — exact, no
+// failure mode.
 //   k_frame_obj_masks    (scenes of 4..64 objects) per pixel: 64-bit object mask
 // Every geometric bound is rt_bins_geom.h's, shared with the host builders
 // the tests compare against (float64, no FMA contraction on either side).
@@ -41,7 +48,8 @@ namespace rtmi {
 constexpr int kFrameMaxPlanes = 8;
 
 // The image rows of one launch (rtmi.cpp Mapping): mode 0 rows
-// y0 + k * step (k < nrows), mode 1 the rank's round-robin bands.
+// y0 + k * step (k < nrows) and columns x = j * step, mode 1 the rank's
+// round-robin bands (every column).
 struct FrameRows {
   int32_t mode, y0, nrows, step, band_h, rank, world, height;
 };
@@ -52,6 +60,10 @@ __host__ __device__ inline bool frame_has_row(const FrameRows& r, int y) {
     return d >= 0 && d < r.nrows * r.step && d % r.step == 0;
   }
   return (y / r.band_h) % r.world == r.rank;
+}
+// a column of the launch (its pixels: launch rows x launch columns)
+__host__ __device__ inline bool frame_has_col(const FrameRows& r, int x) {
+  return r.mode != 0 || x % r.step == 0;
 }
 // image row of launch row k (k < nrows), or -1 past the image
 __host__ __device__ inline int frame_row(const FrameRows& r, int k) {
@@ -67,48 +79,43 @@ struct DevBinTri {
   int32_t pad;
 };
 
-// frame counters (one small device array; cleared by k_frame_bins_count,
-// the list lengths written by k_frame_class_write)
-// (FC_BIG: the big-face list's length, appended by k_frame_bins_count,
-// moved to FC_BIG_N and cleared by k_frame_bins_fill)
-enum : int32_t { FC_OVERFLOW = 0, FC_HEAVY = 1, FC_LEAN = 2, FC_DONE = 3, FC_BIG = 4, FC_BIG_N = 5, FC_WORDS = 6 };
+// frame counters (one small device array). FC_HUGE0 / FC_HUGE1: the huge-face
+// list's length of calls of even / odd parity (k_frame_build1 appends to its
+// call's word and zeroes the other one, which the next call uses).
+// FC_OVERFLOW: kept for a build that could not complete (a look-back that
+// timed out); reported by the host (rtmi.cpp report_overflow).
+enum : int32_t { FC_OVERFLOW = 0, FC_HEAVY = 1, FC_LEAN = 2, FC_HUGE0 = 3, FC_HUGE1 = 4, FC_WORDS = 8 };
 
 // Faces whose pixel rectangle holds more than kBigFace pixels are not walked
 // by their own kFaceLanes threads (a few large faces, e.g. a 576-face torus
 // filling a quarter of a 1080p frame, left a handful of threads looping over
-// thousands of pixels each: 3 ms per call); they go to a list of up to
-// kBigCap faces whose pixels the whole grid shares (k_frame_bins_big).
+// thousands of pixels each: 3 ms per call); they go to the huge list, whose
+// faces k_frame_build2 tests per tile (each tile culls the list against its
+// pixel rectangle, then each pixel tests the tile's share). Past kHugeCap
+// faces the rest are walked by their own threads (slow, exact).
 #ifndef RTMI_BIG_FACE
 #define RTMI_BIG_FACE 64
 #endif
-constexpr int kBigFace = RTMI_BIG_FACE, kBigCap = 4096;
-// rect[4 * face] of a face on the big list carries this bit
-constexpr int32_t kRectBig = 1 << 30;
+constexpr int kBigFace = RTMI_BIG_FACE, kHugeCap = 4096;
 
-struct BinsLaunch {
-  const DevBinTri* tris;
-  int32_t nf;
-  bg::PixCam cam;
-  FrameRows rows;
-  int32_t* rect;   // 4 per face (scratch)
-  double* proj;    // 6 per face (scratch)
-  int32_t* cnt;    // per pixel + 1: zero between calls (the fill pass counts back down)
-  int32_t* off;    // per pixel + 1: list offsets (the scan of cnt over [scan_lo, scan_lo + scan_n))
-  int32_t* ent;    // list entries (TriFast byte offsets), capacity cap
-  int64_t cap;
-  int32_t* ctr;    // FC_* counters
-  int32_t* big;    // the big-face list (kBigCap faces)
-  unsigned long long* fmask;  // per face (not big): its listed pixels, bit = index in its rectangle
-  int64_t scan_lo, scan_n;
-  int32_t pad_rec; // a valid record offset for the read-ahead padding
+// Per-pixel list slots: 2^kSlotLg record offsets per pixel (32: C3 at 1080p
+// lists at most 28 faces per pixel, p99 11; the 1M-face torus at 4K 99, p999
+// 34 — its 1,490 pixels past 32 take the BVH).
+#ifndef RTMI_SLOT_LG
+#define RTMI_SLOT_LG 5
+#endif
+constexpr int kSlotLg = RTMI_SLOT_LG;
+
+struct HugeFace {
+  int32_t rec, pad;
+  int32_t r[4];    // pixel rectangle x0, x1, y0, y1
+  double pr[6];    // projected vertices (rt_bins_geom.h tri_meets_box)
 };
 
 struct RecordsLaunch {
   // the launch's one-pixel groups (rt_fast.h lane_pixel / group_pixel, tile 1 x 1)
   int32_t mode, y0, nrows, ncols, step, max_step, band_h, rank, world, width, height, ngroups;
-  const int32_t* order;     // launch order (group_order), or nullptr
-  const int32_t* off;       // pixel lists (per pixel + 1)
-  uint32_t* info;           // out: FastParams.pix_info records
+  uint32_t* info;           // out: per pixel min(list length, kPixCount) | skip bits << 24
   // shadow skips (have == 0: none)
   int32_t nplanes, nl;
   uint32_t have;
@@ -117,14 +124,33 @@ struct RecordsLaunch {
   const LightGrid* grids;   // per light (rt_scene::grids)
   const int32_t* sat;       // occupancy prefix sums of every light's grid, back to back
   int64_t sat_off[8];
+  int32_t records;          // 1: skip bits (one-pixel launches); 0: list lengths only
   // two-class split (split == 0: records only)
   int32_t split;
   uint32_t full;            // every light's bit: (1 << nlight) - 1
   int32_t* lean;            // capacity ngroups + 64
   int32_t* heavy;           // capacity ngroups
   int32_t* ctr;
-  int32_t tiles_done;       // host: the tile bits were written by the count launch
-  int32_t records_done;     // host: the records (+ tile class counts) were written by the fill launch
+};
+
+struct FrameLaunch {
+  // faces (k_frame_build1)
+  const DevBinTri* tris;
+  int32_t nf;
+  bg::PixCam cam;
+  FrameRows rows;
+  int32_t* cnt;             // per pixel: zero between calls (k_frame_build2 zeroes the launch's)
+  int32_t* slots;           // per pixel 2^slot_lg list entries (TriFast byte offsets), + kBinPad
+  int32_t slot_lg;
+  HugeFace* huge;           // kHugeCap
+  int32_t parity;           // the call's FC_HUGE word: FC_HUGE0 + parity
+  // tiles / records / lists (k_frame_build1 tile blocks, k_frame_build2)
+  RecordsLaunch r;
+  uint8_t* tile_bits;       // per tile: 1 = every light skipped for the whole tile
+  unsigned long long* status;  // per tile: the look-back granule
+  int32_t tiles_x, ntiles;
+  unsigned int* zero;       // words k_frame_build1 zeroes (queue heads + Stats), or nullptr
+  int32_t nzero;
 };
 
 // object bins (rt_bins.h build_object_pixel_masks): world boxes of the objects
@@ -147,21 +173,10 @@ constexpr int kObjRectInts = 4 * 64 + 2;
 }  // namespace rtmi
 
 extern "C" {
-// count + scan; *scan_tmp_bytes in/out: the scan's scratch size (query with scan_tmp == nullptr)
-// tr / tile_bits (optional): the call's pixel-record launch; its tiles
-// (k_frame_tiles) then run in the count launch and *tiles_done = 1
-int rtmi_frame_bins_count(const rtmi::BinsLaunch* a, void* scan_tmp, size_t* scan_tmp_bytes, void* stream,
-                          const rtmi::RecordsLaunch* tr = nullptr, void* tile_bits = nullptr,
-                          int* tiles_done = nullptr);
-// r (optional): the call's pixel-record launch (its tiles done); the
-// records then run in the fill launch (tile_cls: the tile-ordered lists'
-// class counts, or nullptr) and *records_done = 1
-int rtmi_frame_bins_fill(const rtmi::BinsLaunch* a, void* stream, const rtmi::RecordsLaunch* r = nullptr,
-                         const void* tile_bits = nullptr, void* tile_cls = nullptr, int* records_done = nullptr);
-// records (+ lists); tile_bits: rtmi_frame_tile_bytes(ncols, nrows) bytes;
-// scratch: *scratch_bytes (query with scratch == nullptr)
-int rtmi_frame_records(const rtmi::RecordsLaunch* a, void* tile_bits, void* scratch, size_t* scratch_bytes,
-                       void* stream);
+// The call's two build launches (k_frame_build1, k_frame_build2) on `stream`;
+// build2_blocks: the persistent grid of k_frame_build2 (<= the launch's
+// tiles, far below what stays resident).
+int rtmi_frame_build(const rtmi::FrameLaunch* a, int build2_blocks, void* stream);
 long long rtmi_frame_tile_bytes(int ncols, int nrows);
 int rtmi_frame_obj_masks(const rtmi::ObjMaskLaunch* a, void* stream);
 }

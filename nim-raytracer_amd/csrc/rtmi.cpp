@@ -134,6 +134,15 @@ int device_of_current() {
 
 }  // namespace
 
+// Pixel-list slots per pixel, 2^lg (rt_frame.h kSlotLg; RTMI_SLOT_LG: A/B knob).
+inline int slot_lg_env() {
+  static const int v = [] {
+    const char* e = std::getenv("RTMI_SLOT_LG");
+    return e ? std::min(10, std::max(0, std::atoi(e))) : rtmi::kSlotLg;
+  }();
+  return v;
+}
+
 struct rt_scene {
   std::mutex mu;
   int device = 0;
@@ -206,36 +215,23 @@ struct rt_scene {
   int64_t sat_off[8] = {};
   struct Frame {                   // per-call buffers of one image size
     int w = 0, h = 0;
-    DevBuf<int32_t> cnt, off, ent, rect, lean, heavy, ctr, big, orect;
-    DevBuf<double> proj;
+    DevBuf<int32_t> cnt, slots, lean, heavy, ctr, orect;
     DevBuf<uint32_t> info;
-    DevBuf<unsigned long long> omask, fmask;
-    DevBuf<unsigned char> scan_tmp;
-    DevBuf<unsigned char> tiles;   // per-tile shadow skips (k_frame_tiles)
-    DevBuf<unsigned char> cls;     // the class counts' scratch (k_frame_class_count + scan)
-    // launch row sets whose list entries `ent` is known to hold for the
-    // current camera (the first call of a row set reads its entry count);
-    // `full_sized`: a whole-frame row set was sized, and every row set's
-    // lists are a subset of the whole frame's (a pixel's list does not
-    // depend on which other rows a call covers), so no further reads
-    std::set<std::array<int64_t, 9>> sized;
-    bool full_sized = false;
+    DevBuf<unsigned long long> omask, status;
+    DevBuf<HugeFace> huge;
+    DevBuf<unsigned char> tiles;   // per-tile shadow skips (k_frame_build1)
+    int slot_lg = -1;              // slots allocated for 2^slot_lg entries per pixel (-1: none)
+    int want_lg = slot_lg_env();   // test hook (rtmi_test_slot_lg) / RTMI_SLOT_LG
+    uint32_t calls = 0;            // build launches (their parity picks the huge-list counter)
     bool counted = false;          // the last launch's lean / general lists were counted on the device
-    bool listed = false;           // the last launch built camera-ray lists (its FC_OVERFLOW is meaningful)
-    int64_t test_cap = 0;          // test hook (rtmi_test_entry_cap): > 0 caps the entry capacity
-    // forget everything a call left: the next call re-zeroes the counts and
-    // re-reads its entry count (after a failed or overflowed call)
-    void invalidate() {
-      w = h = 0;
-      sized.clear();
-      full_sized = false;
-    }
+    bool listed = false;           // the last launch built camera-ray lists
+    // forget the buffers: the next call re-allocates and re-zeroes them
+    void invalidate() { w = h = 0; }
     void release() {
-      cnt.release(); off.release(); ent.release(); rect.release(); lean.release(); heavy.release(); ctr.release();
-      proj.release(); info.release(); omask.release(); scan_tmp.release(); tiles.release();
-      cls.release();
-      sized.clear();
-      full_sized = false;
+      cnt.release(); slots.release(); lean.release(); heavy.release(); ctr.release(); orect.release();
+      info.release(); omask.release(); status.release(); huge.release(); tiles.release();
+      slot_lg = -1;
+      w = h = 0;
     }
   } fr;
   // object bins (rt_bins.h ObjBox), scenes of 4..64 objects
@@ -1010,8 +1006,6 @@ extern "C" int rt_scene_set_camera(rt_scene* s, const double c2w[16], double fov
   const hipError_t e = hipEventSynchronize(s->done);
   std::memcpy(s->c2w, c2w, sizeof s->c2w);
   s->fov = fov_deg;
-  s->fr.sized.clear();  // list entry counts change with the camera
-  s->fr.full_sized = false;
   s->orders.clear();    // measured per-group costs (launch order) too
   if (prev >= 0 && prev != s->device) (void)hipSetDevice(prev);
   if (e != hipSuccess) return fail(RT_E_DEVICE, "waiting for the scene's earlier calls: %s", hipGetErrorString(e));
@@ -1261,26 +1255,31 @@ FrameRows frame_rows(const Mapping& mp, int height) {
 // The per-call buffers of one image size (contents are rebuilt by each call).
 int frame_buffers(rt_scene* s, int w, int h, hipStream_t st) {
   rt_scene::Frame& f = s->fr;
-  if (f.w == w && f.h == h) return RT_OK;
+  const bool lists = s->binnable && !s->bin_tris.empty();
+  if (f.w == w && f.h == h && (!lists || f.slot_lg == f.want_lg)) return RT_OK;
   // an earlier call may still read the old buffers: the call's stream waits
   // on the scene's last call (render_device), whose aux-stream kernels are
   // joined into its done event, so this one wait covers them all
   HIP_TRY(hipStreamSynchronize(st));
   const size_t npx = (size_t)w * (size_t)h;
-  const size_t nf = s->bin_tris.size();
   int rc;
   f.invalidate();
-  if ((rc = f.cnt.alloc(npx + 1)) || (rc = f.off.alloc(npx + 1)) || (rc = f.info.alloc(npx)) ||
-      (rc = f.lean.alloc(npx + 64)) || (rc = f.heavy.alloc(npx)) || (rc = f.ctr.alloc(FC_WORDS)) ||
-      (rc = f.big.alloc(kBigCap)) ||
-      (rc = f.tiles.alloc((size_t)rtmi_frame_tile_bytes(w, h))))
+  if ((rc = f.cnt.alloc(npx + 1)) || (rc = f.info.alloc(npx)) || (rc = f.lean.alloc(npx + 64)) ||
+      (rc = f.heavy.alloc(npx)) || (rc = f.ctr.alloc(FC_WORDS)) ||
+      (rc = f.tiles.alloc((size_t)rtmi_frame_tile_bytes(w, h))) ||
+      (rc = f.status.alloc((size_t)rtmi_frame_tile_bytes(w, h))))
     return rc;
   if (s->objbins && ((rc = f.omask.alloc(npx)) || (rc = f.orect.alloc(kObjRectInts)))) return rc;
-  if (nf > 0 && (f.rect.n < 4 * nf || f.proj.n < 6 * nf || f.fmask.n < nf)) {
-    if ((rc = f.rect.alloc(4 * nf)) || (rc = f.proj.alloc(6 * nf)) || (rc = f.fmask.alloc(nf))) return rc;
+  if (lists) {
+    // the slots hold valid record offsets from the start (the list search
+    // reads up to kBinPad entries past a list's end)
+    const size_t ns = (npx << f.want_lg) + kBinPad;
+    if ((rc = f.slots.alloc(ns)) || (rc = f.huge.alloc(kHugeCap))) return rc;
+    HIP_TRY(hipMemsetD32(f.slots.p, s->bin_tris[0].rec, ns));
+    f.slot_lg = f.want_lg;
   }
-  if (!f.ent.p && (rc = f.ent.alloc(1 << 16))) return rc;
-  // the bin counts are zero between calls (the fill pass counts them down)
+  // the per-pixel counters are zero between calls (k_frame_build2 zeroes
+  // the ones a call used)
   HIP_TRY(hipMemset(f.cnt.p, 0, f.cnt.bytes()));
   HIP_TRY(hipMemset(f.ctr.p, 0, f.ctr.bytes()));
   f.w = w;
@@ -1288,19 +1287,56 @@ int frame_buffers(rt_scene* s, int w, int h, hipStream_t st) {
   return RT_OK;
 }
 
-// The mesh's camera-ray lists for the launch's rows (k_frame_bins_count /
-// scan / k_frame_bins_fill). *ok = false: no lists for this camera (a mesh
-// vertex may lie at or behind the camera plane), the kernels traverse the BVH.
-void records_launch(rt_scene* s, const rt_options* o, const Mapping& mp, const FastParams& p, bool split,
-                    RecordsLaunch& r);
+// The call's pixel-record / list parameters (RecordsLaunch) for the
+// launch's pixels.
+void records_launch(rt_scene* s, const rt_options* o, const Mapping& mp, const FastParams& p, bool records,
+                    bool split, RecordsLaunch& r) {
+  std::memset(&r, 0, sizeof r);
+  r.mode = mp.mode;
+  r.y0 = mp.y0;
+  r.nrows = mp.nrows;
+  r.ncols = mp.ncols;
+  r.step = mp.step;
+  r.max_step = mp.max_step;
+  r.band_h = mp.band_h;
+  r.rank = mp.rank;
+  r.world = mp.world;
+  r.width = o->width;
+  r.height = o->height;
+  r.ngroups = p.ngroups;
+  r.info = s->fr.info.p;
+  r.records = records ? 1 : 0;
+  if (records && s->skippable && s->skip_planes.size() <= (size_t)kFrameMaxPlanes) {
+    std::vector<bg::SkipPlaneC> pcs;
+    if (skip_camera(s->skip_planes, s->mesh_w2o, s->c2w, s->fov, o->width, o->height, o->bias, &r.cam, &pcs)) {
+      r.nplanes = (int32_t)pcs.size();
+      std::copy(pcs.begin(), pcs.end(), r.planes);
+      r.nl = std::min(8, s->nlight);
+      for (int l = 0; l < r.nl; ++l) r.have |= s->grid_occ[(size_t)l].g.gu > 0 ? 1u << l : 0u;
+      r.grids = s->grids.p;
+      r.sat = s->sat_dev.p;
+      for (int l = 0; l < 8; ++l) r.sat_off[l] = s->sat_off[l];
+    }
+  }
+  r.split = split ? 1 : 0;
+  r.full = s->nlight >= 32 ? ~0u : (1u << s->nlight) - 1u;
+  r.lean = s->fr.lean.p;
+  r.heavy = s->fr.heavy.p;
+  r.ctr = s->fr.ctr.p;
+}
 
-// rp (optional): the call's pixel-record parameters; the record tiles then
-// run inside the count launch and *rl holds the record launch (tiles_done)
-int frame_bins(rt_scene* s, const rt_options* o, const Mapping& mp, hipStream_t st, bool* ok,
-               const FastParams* rp = nullptr, bool split = false, RecordsLaunch* rl = nullptr) {
+// The mesh's camera-ray lists for the launch's pixels, their records
+// (records: one-pixel groups) and with split the lean / general lists — the
+// call's two build launches (rt_frame.h). *ok = false: no lists for this
+// camera (a mesh vertex may lie at or behind the camera plane), the kernels
+// traverse the BVH. zero (words, count): the render kernels' queue heads +
+// Stats words, zeroed by the first build launch (*zeroed = true).
+int frame_build(rt_scene* s, const rt_options* o, const Mapping& mp, const FastParams& p, bool records, bool split,
+                unsigned int* zero, int nzero, hipStream_t st, bool* ok, bool* zeroed) {
   *ok = false;
-  if (!s->binnable) return RT_OK;
-  BinsLaunch a;
+  *zeroed = false;
+  if (!s->binnable || s->bin_tris.empty()) return RT_OK;
+  FrameLaunch a;
   std::memset(&a, 0, sizeof a);
   if (!pixel_camera(s->mesh_o2w, s->mesh_w2o, s->c2w, s->fov, o->width, o->height, &a.cam)) return RT_OK;
   // every vertex strictly in front of the camera plane (face_pixel_rect's
@@ -1320,146 +1356,25 @@ int frame_bins(rt_scene* s, const rt_options* o, const Mapping& mp, hipStream_t 
   a.tris = s->bin_dev.p;
   a.nf = (int32_t)s->bin_tris.size();
   a.rows = frame_rows(mp, o->height);
-  a.rect = f.rect.p;
-  a.proj = f.proj.p;
   a.cnt = f.cnt.p;
-  a.off = f.off.p;
-  a.ent = f.ent.p;
-  a.cap = f.test_cap > 0 ? std::min<int64_t>(f.test_cap, (int64_t)f.ent.n) : (int64_t)f.ent.n;
-  a.ctr = f.ctr.p;
-  a.big = f.big.p;
-  a.fmask = f.fmask.p;
-  a.pad_rec = s->bin_tris[0].rec;
-  const int64_t w = o->width;
-  if (mp.mode == 0) {  // the scan covers the launch's rows only
-    const int64_t last = mp.y0 + (int64_t)(mp.nrows - 1) * mp.step;
-    a.scan_lo = mp.y0 * w;
-    a.scan_n = (last + 1) * w - a.scan_lo + 1;
-  } else {
-    a.scan_lo = 0;
-    a.scan_n = w * o->height + 1;
-  }
-  size_t bytes = 0;
-  if ((rc = rtmi_frame_bins_count(&a, nullptr, &bytes, st)))
-    return fail(RT_E_DEVICE, "bin scan size query failed: %s", hipGetErrorString((hipError_t)rc));
-  if (f.scan_tmp.n < bytes) {
-    HIP_TRY(hipStreamSynchronize(st));
-    if ((rc = f.scan_tmp.alloc(bytes))) return rc;
-  }
-  bytes = f.scan_tmp.n;
-  int tiles_done = 0;
-  if (rp && rl) records_launch(s, o, mp, *rp, split, *rl);
-  // From the count launch until the fill launch is queued, the per-pixel
-  // counts are non-zero (the fill pass counts them back down): any failure
-  // in between leaves the frame buffers invalid, so the next call re-zeroes
-  // them and re-reads its entry count.
-  struct Invalidate {
-    rt_scene::Frame& f;
-    bool armed = true;
-    ~Invalidate() {
-      if (armed) f.invalidate();
-    }
-  } guard{f};
-  if ((rc = rtmi_frame_bins_count(&a, f.scan_tmp.p, &bytes, st, rp && rl ? rl : nullptr, f.tiles.p, &tiles_done)))
-    return fail(RT_E_DEVICE, "bin count launch failed: %s", hipGetErrorString((hipError_t)rc));
+  a.slots = f.slots.p;
+  a.slot_lg = f.slot_lg;
+  a.huge = f.huge.p;
+  a.parity = (int32_t)(f.calls++ & 1u);
+  records_launch(s, o, mp, p, records, split, a.r);
+  a.tile_bits = f.tiles.p;
+  a.status = f.status.p;
+  a.tiles_x = (mp.ncols + 63) / 64;
+  a.ntiles = a.tiles_x * ((mp.nrows + 3) / 4);
+  a.zero = zero;
+  a.nzero = nzero;
+  // k_frame_build2's persistent grid: two blocks per CU, far below what
+  // stays resident (its look-back waits on earlier chunks only)
+  if ((rc = rtmi_frame_build(&a, 2 * s->num_cus, st)))
+    return fail(RT_E_DEVICE, "frame build launch failed: %s", hipGetErrorString((hipError_t)rc));
   f.listed = true;
-  if (rp && rl) rl->tiles_done = tiles_done;
-  // the first call of a row set under this camera reads its entry count and
-  // sizes the entry buffer; later calls of the same set list the same faces,
-  // and once the whole frame is sized every row set is (a subset of it)
-  const std::array<int64_t, 9> key = {w, o->height, mp.mode, mp.y0, mp.nrows, mp.step, mp.band_h, mp.rank, mp.world};
-  const bool whole = mp.mode == 0 ? (mp.y0 == 0 && mp.step == 1 && mp.nrows == o->height) : mp.world == 1;
-  if (!f.full_sized && !f.sized.count(key)) {
-    int32_t total = 0;
-    HIP_TRY(hipMemcpyAsync(&total, f.off.p + a.scan_lo + a.scan_n - 1, sizeof total, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
-    if (total < 0) return fail(RT_E_UNSUPPORTED, "more than 2^31 camera-ray list entries");
-    const size_t need = (size_t)total + kBinPad;
-    if (f.ent.n < need) {
-      if ((rc = f.ent.alloc(need + need / 4))) return rc;
-      a.ent = f.ent.p;
-      a.cap = f.test_cap > 0 ? std::min<int64_t>(f.test_cap, (int64_t)f.ent.n) : (int64_t)f.ent.n;
-    }
-    if (whole) f.full_sized = true;
-    else f.sized.insert(key);
-  }
-  // the pixel records read the list offsets (ready now), not the entries:
-  // they share the fill launch when their tiles are done and their scratch
-  // is already sized (every call after a scene's first at this size)
-  const RecordsLaunch* fr = nullptr;
-  void* tile_cls = nullptr;
-  if (rp && rl && (rl->tiles_done || rl->have == 0u)) {
-    size_t need = 0;
-    if (rtmi_frame_records(rl, f.tiles.p, nullptr, &need, st) == 0 && f.cls.p && f.cls.n >= need) {
-      fr = rl;
-      tile_cls = rl->split && !rl->order ? (void*)f.cls.p : nullptr;
-    }
-  }
-  int records_done = 0;
-  if ((rc = rtmi_frame_bins_fill(&a, st, fr, f.tiles.p, tile_cls, &records_done)))
-    return fail(RT_E_DEVICE, "bin fill launch failed: %s", hipGetErrorString((hipError_t)rc));
-  guard.armed = false;
-  if (rl) rl->records_done = records_done;
+  *zeroed = zero != nullptr;
   *ok = true;
-  return RT_OK;
-}
-
-// Pixel records of the launch's one-pixel groups and, with split, the lean /
-// general lists (k_frame_records).
-void records_launch(rt_scene* s, const rt_options* o, const Mapping& mp, const FastParams& p, bool split,
-                    RecordsLaunch& r) {
-  std::memset(&r, 0, sizeof r);
-  r.mode = mp.mode;
-  r.y0 = mp.y0;
-  r.nrows = mp.nrows;
-  r.ncols = mp.ncols;
-  r.step = mp.step;
-  r.max_step = mp.max_step;
-  r.band_h = mp.band_h;
-  r.rank = mp.rank;
-  r.world = mp.world;
-  r.width = o->width;
-  r.height = o->height;
-  r.ngroups = p.ngroups;
-  r.order = p.order;
-  r.off = s->fr.off.p;
-  r.info = s->fr.info.p;
-  if (s->skippable && s->skip_planes.size() <= (size_t)kFrameMaxPlanes) {
-    std::vector<bg::SkipPlaneC> pcs;
-    if (skip_camera(s->skip_planes, s->mesh_w2o, s->c2w, s->fov, o->width, o->height, o->bias, &r.cam, &pcs)) {
-      r.nplanes = (int32_t)pcs.size();
-      std::copy(pcs.begin(), pcs.end(), r.planes);
-      r.nl = std::min(8, s->nlight);
-      for (int l = 0; l < r.nl; ++l) r.have |= s->grid_occ[(size_t)l].g.gu > 0 ? 1u << l : 0u;
-      r.grids = s->grids.p;
-      r.sat = s->sat_dev.p;
-      for (int l = 0; l < 8; ++l) r.sat_off[l] = s->sat_off[l];
-    }
-  }
-  r.split = split ? 1 : 0;
-  r.full = s->nlight >= 32 ? ~0u : (1u << s->nlight) - 1u;
-  r.lean = s->fr.lean.p;
-  r.heavy = s->fr.heavy.p;
-  r.ctr = s->fr.ctr.p;
-}
-
-// rl: the launch frame_bins already started the tiles of (or nullptr)
-int frame_records(rt_scene* s, const rt_options* o, const Mapping& mp, const FastParams& p, bool split,
-                  hipStream_t st, const RecordsLaunch* rl) {
-  RecordsLaunch r;
-  if (rl) r = *rl;
-  else records_launch(s, o, mp, p, split, r);
-  size_t bytes = 0;
-  int e = rtmi_frame_records(&r, s->fr.tiles.p, nullptr, &bytes, st);
-  if (e) return fail(RT_E_DEVICE, "pixel record scratch query failed: %s", hipGetErrorString((hipError_t)e));
-  if (s->fr.cls.n < bytes) {
-    HIP_TRY(hipStreamSynchronize(st));  // an earlier call may still use the old scratch
-    const int rc = s->fr.cls.alloc(bytes);
-    if (rc) return rc;
-  }
-  bytes = s->fr.cls.n;
-  e = rtmi_frame_records(&r, s->fr.tiles.p, s->fr.cls.p, &bytes, st);
-  if (e) return fail(RT_E_DEVICE, "pixel record launch failed: %s", hipGetErrorString((hipError_t)e));
   return RT_OK;
 }
 
@@ -1511,8 +1426,11 @@ bool sampler_in_pixel(int32_t aa_kind) {
 // kernels: the mesh's camera-ray lists (>= 16 samples per pixel), the object
 // masks, and for one-pixel waves the pixel records — with *split, also the
 // lean / general lists of a two-class launch.
+// zero / nzero: the render kernels' queue heads + Stats words; a call that
+// builds pixel lists zeroes them in its first build launch (*zeroed), else
+// the caller clears them.
 int fill_fast(rt_scene* s, const rt_options* o, const Mapping& mp, float* fb, FastParams& p, int* blocks,
-              rt_scene::Order** measuring, hipStream_t st, bool* split) {
+              rt_scene::Order** measuring, hipStream_t st, bool* split, unsigned int* zero, int nzero, bool* zeroed) {
   std::memset(&p, 0, sizeof p);
   p.objs = s->f32.objs.p;
   p.objx = s->f32.objx.p;
@@ -1620,6 +1538,7 @@ int fill_fast(rt_scene* s, const rt_options* o, const Mapping& mp, float* fb, Fa
   *measuring = ou.entry;
   *blocks = pl.blocks;
   *split = false;
+  *zeroed = false;
   if (!binning || pl.L < 16 || !sampler_in_pixel(o->aa_kind)) return RT_OK;
   // this call's camera-dependent data (nothing of it is kept from earlier calls)
   int rc;
@@ -1632,22 +1551,21 @@ int fill_fast(rt_scene* s, const rt_options* o, const Mapping& mp, float* fb, Fa
   const unsigned sub = f32_subset(s, o);
   const bool want_split = !(o->flags & (RT_FLAG_NO_SPLIT | RT_FLAG_COUNT_TRAVERSAL)) && !p.cost && !cost_dump &&
                           s->nlight <= 8 && rtmi_lean_f32_blocks_per_cu(sub, f32_table_lds(s, o)) > 0;
-  RecordsLaunch rl;
-  rl.tiles_done = rl.records_done = 0;
-  const bool records = pl.L == 64;  // records follow the lists (below)
-  if ((rc = frame_bins(s, o, mp, st, &lists, records ? &p : nullptr, want_split, records ? &rl : nullptr))) return rc;
+  const bool records = pl.L == 64;  // one-pixel groups: records (+ the split)
+  *split = records && want_split && !p.order;
+  if ((rc = frame_build(s, o, mp, p, records, *split, zero, nzero, st, &lists, zeroed))) return rc;
   if (lists) {
-    p.pix_off = s->fr.off.p;
-    p.pix_ent = s->fr.ent.p;
+    p.pix_slots = s->fr.slots.p;
+    p.pix_cnt = s->fr.info.p;
+    p.slot_lg = s->fr.slot_lg;
+    if (records) p.pix_info = s->fr.info.p;
+  } else {
+    *split = false;
   }
   if (s->objbins) {
     if ((rc = frame_obj_masks(s, o, mp, st, &masks))) return rc;
     if (masks) p.obj_pix = s->fr.omask.p;
   }
-  if (!lists || pl.L != 64) return RT_OK;
-  *split = want_split;
-  if ((rc = frame_records(s, o, mp, p, *split, st, &rl))) return rc;  // (rl filled by frame_bins: lists)
-  p.pix_info = s->fr.info.p;
   return RT_OK;
 }
 
@@ -1751,8 +1669,16 @@ bool lean1_ok(const rt_scene* s, const rt_options* o, const FastParams& p, unsig
          p.iters * 64 == p.spp && p.iters % 4 == 0 && s->nobj == 2;
 }
 
-int launch(rt_scene* s, const rt_options* o, const Mapping& mp, float* d_out, hipStream_t st, bool reduce) {
+// zero / nzero: the queue heads and / or Stats words every call clears
+// before its render kernels (a float32 call that builds pixel lists clears
+// them in its first build launch: one launch fewer).
+int launch(rt_scene* s, const rt_options* o, const Mapping& mp, float* d_out, hipStream_t st, bool reduce,
+           unsigned int* zero, int nzero) {
   int blocks = 1;
+  auto clear = [&]() -> int {
+    if (nzero > 0) HIP_TRY(hipMemsetAsync(zero, 0, (size_t)nzero * sizeof(unsigned int), st));
+    return RT_OK;
+  };
   // what rt_scene_last_split / _last_batch report describes THIS call, even
   // when it returns early or runs the float64 kernel
   s->fr.counted = false;
@@ -1762,6 +1688,7 @@ int launch(rt_scene* s, const rt_options* o, const Mapping& mp, float* d_out, hi
   s->last_general = 0;
   s->last_batched = 0;
   if (o->precision == RT_FP64) {
+    if (int rc = clear()) return rc;
     RenderParams<double> p;
     fill_params<double>(s, s->f64, o, mp, d_out, p, &blocks);
     if (o->flags & RT_FLAG_TIMING) HIP_TRY(hipEventRecord(s->tev[1], st));
@@ -1785,10 +1712,11 @@ int launch(rt_scene* s, const rt_options* o, const Mapping& mp, float* d_out, hi
   } else {
     FastParams p;
     rt_scene::Order* measuring = nullptr;
-    bool split = false;
-    if (mp.nrows == 0 || mp.ncols == 0) return RT_OK;
-    int rc = fill_fast(s, o, mp, d_out, p, &blocks, &measuring, st, &split);
+    bool split = false, zeroed = false;
+    if (mp.nrows == 0 || mp.ncols == 0) return clear();
+    int rc = fill_fast(s, o, mp, d_out, p, &blocks, &measuring, st, &split, zero, nzero, &zeroed);
     if (rc) return rc;
+    if (!zeroed && (rc = clear())) return rc;
     if (o->flags & RT_FLAG_TIMING) HIP_TRY(hipEventRecord(s->tev[1], st));
     s->last_general = p.ngroups;
     if (p.ngroups == 0) return RT_OK;
@@ -1801,7 +1729,7 @@ int launch(rt_scene* s, const rt_options* o, const Mapping& mp, float* d_out, hi
     }
     s->fr.counted = split;
     if (split) {  // two-class launch: the general kernel on its list, then the lean kernel on its own
-      // the lists and their entry counts come from this call's k_frame_records
+      // the lists and their entry counts come from this call's k_frame_build2
       // (the host never reads them: grids and items are sized for the launch's
       // groups, the kernels stop at the device counts)
       int32_t* const n_heavy = s->fr.ctr.p + FC_HEAVY;
@@ -1812,7 +1740,7 @@ int launch(rt_scene* s, const rt_options* o, const Mapping& mp, float* d_out, hi
       // the general pixels: the batched kernel (k_render_gen) for scenes of
       // one mesh object with distant lights only, no reflection (the lean
       // kernel's subsets) when both camera lists and light grids exist
-      const int gbpc = (o->flags & RT_FLAG_NO_BATCH) || p.shadow_mesh < 0 || !p.pix_off || !p.pix_ent || !p.grids ||
+      const int gbpc = (o->flags & RT_FLAG_NO_BATCH) || p.shadow_mesh < 0 || !p.pix_slots || !p.grids ||
                                p.has_point_light
                            ? 0
                            : rtmi_gen_f32_blocks_per_cu(sub, shmem);
@@ -2033,8 +1961,7 @@ int render_device(rt_scene* s, const rt_options* o, const Mapping& mp, float* d_
   // one fill: the queue heads (float32) and / or the Stats accumulator behind them
   const size_t q0 = o->precision == RT_FP32 ? 0 : rt_scene::kQueueWords;
   const size_t q1 = rt_scene::kQueueWords + (reduce ? 2 * (size_t)kStatSlots : 0);
-  if (q1 > q0) HIP_TRY(hipMemsetAsync(s->queue.p + q0, 0, (q1 - q0) * sizeof(unsigned int), st));
-  int rc = launch(s, o, mp, d_out, st, reduce);
+  int rc = launch(s, o, mp, d_out, st, reduce, s->queue.p + q0, (int)(q1 - q0));
   if (rc) return rc;
   if (s->timed) HIP_TRY(hipEventRecord(s->tev[2], st));
   HIP_TRY(hipEventRecord(s->done, st));
@@ -2194,7 +2121,7 @@ extern "C" int rt_rgba_encode_device(const float* d_fb, int32_t width, int32_t h
 
 namespace {
 // The last launch's lean / general list lengths: counted on the device by
-// its k_frame_records (read back here, after the call completed), or the
+// its k_frame_build2 (read back here, after the call completed), or the
 // host's (a one-kernel launch: every group general).
 int last_lists(rt_scene* s, int64_t* lean, int64_t* general) {
   if (!s->fr.counted) {
@@ -2258,35 +2185,44 @@ extern "C" int rt_scene_last_counters(rt_scene* s, rt_traversal_counters* out) {
 
 // ---- test hooks (tests/test_gpu_frame.py; not part of include/rtmi.h) ----
 
-// Caps the camera-ray list entry capacity the fill passes may use (0: no
-// cap), so a test can force FC_OVERFLOW and check that the call fails.
-extern "C" int rtmi_test_entry_cap(rt_scene* s, int64_t cap) {
-  if (!s || cap < 0) return fail(RT_E_INVALID, "bad argument");
+// Pixel-list slots per pixel, 2^lg (lg >= 0: used from the next call on; the
+// buffers are re-allocated): a test forces lists past their slots (the
+// pixels' camera rays then take the BVH). Returns the current lg (lg < 0:
+// query only).
+extern "C" int rtmi_test_slot_lg(rt_scene* s, int32_t lg) {
+  if (!s || lg > 10) return fail(RT_E_INVALID, "bad argument");
   std::lock_guard<std::mutex> lk(s->mu);
-  s->fr.test_cap = cap;
-  return RT_OK;
+  if (lg >= 0) s->fr.want_lg = lg;
+  return s->fr.want_lg;
 }
 
 // The last render call's device-built camera-ray lists and pixel records
-// (image-sized arrays; only the call's pixels are defined). off: w*h + 1,
-// info: w*h, ent: up to ent_cap entries. Returns the entry capacity copied,
-// or a negative RT_E_* code.
+// (image-sized arrays; only the call's pixels are defined) as CSR: off:
+// w*h + 1 (a pixel's true list length, overflowed ones included), ent: up to
+// ent_cap entries (a pixel past its 2^lg slots contributes its first 2^lg
+// entries and pads the rest with -1), info: w*h. Returns the entries
+// copied, or a negative RT_E_* code.
 extern "C" int64_t rtmi_test_frame_lists(rt_scene* s, int32_t* off, int32_t* ent, int64_t ent_cap, uint32_t* info) {
   if (!s || !off || !ent || !info) return fail(RT_E_INVALID, "null argument");
   std::lock_guard<std::mutex> lk(s->mu);
   DeviceGuard g(s->device);
   const rt_scene::Frame& f = s->fr;
-  if (!f.off.p || f.w == 0) return fail(RT_E_INVALID, "no per-call lists yet");
+  if (!f.slots.p || f.w == 0 || f.slot_lg < 0) return fail(RT_E_INVALID, "no per-call lists yet");
   const size_t npx = (size_t)f.w * (size_t)f.h;
   HIP_TRY(hipEventSynchronize(s->done));
-  HIP_TRY(hipMemcpy(off, f.off.p, (npx + 1) * sizeof(int32_t), hipMemcpyDeviceToHost));
   HIP_TRY(hipMemcpy(info, f.info.p, npx * sizeof(uint32_t), hipMemcpyDeviceToHost));
-  const size_t n = std::min<size_t>(f.ent.n, (size_t)std::max<int64_t>(0, ent_cap));
-  HIP_TRY(hipMemcpy(ent, f.ent.p, n * sizeof(int32_t), hipMemcpyDeviceToHost));
-  int32_t c[FC_WORDS];
-  HIP_TRY(hipMemcpy(c, f.ctr.p, sizeof c, hipMemcpyDeviceToHost));
-  if (c[FC_OVERFLOW]) return fail(RT_E_DEVICE, "camera-ray list entries overflowed their buffer");
-  return (int64_t)n;
+  std::vector<int32_t> slots(npx << f.slot_lg);
+  HIP_TRY(hipMemcpy(slots.data(), f.slots.p, slots.size() * sizeof(int32_t), hipMemcpyDeviceToHost));
+  const uint32_t K = 1u << f.slot_lg;
+  int64_t n = 0;
+  off[0] = 0;
+  for (size_t p = 0; p < npx; ++p) {
+    const uint32_t c = info[p] & kPixCount;
+    for (uint32_t k = 0; k < c; ++k, ++n)
+      if (n < ent_cap) ent[n] = k < K ? slots[(p << f.slot_lg) + k] : -1;
+    off[p + 1] = (int32_t)n;
+  }
+  return std::min<int64_t>(n, ent_cap);
 }
 
 // The host builders (rt_bins.cpp build_pixel_bins + build_shadow_skips) on

@@ -8,9 +8,10 @@ failure behaviour.
   is cached behind a lock and follows the Scene's camera, as the Nim binding
   in INTEGRATION.md does); a camera move and a box resized in y between
   frames render the oracle's frames for the new Scene.
-* A render call whose camera-ray lists overflowed their entry capacity
-  returns RT_E_DEVICE (never RT_OK with a truncated image): a test hook caps
-  the capacity.
+* A pixel whose camera-ray list outgrows its slots (a test hook shrinks
+  them) renders exactly the same frame and Stats: its camera rays take the
+  BVH. The per-call build has no failure mode that returns RT_OK with a
+  wrong image.
 * rt_scene_last_split describes the last call, including a float64 call
   after a two-class float32 call.
 """
@@ -21,8 +22,7 @@ import numpy as np
 import pytest
 
 from rtmi import Antialias, Options, Precision, akGrid, akNone, scenes
-from rtmi._lib import RtmiError, lib
-from rtmi.abi import RT_E_DEVICE
+from rtmi._lib import lib
 from rtmi.glm import X_AXIS, Y_AXIS, degToRad, mat4, rotate, translate, vec3
 from rtmi.renderer import DeviceScene, deviceScene, invalidateScene, renderLine
 
@@ -127,43 +127,41 @@ def test_threaded_renderline_fp32_c3_scene(gpu):
         invalidateScene(sc)
 
 
-def _entry_cap(ds, cap):
-    f = lib().rtmi_test_entry_cap
+def _slot_lg(ds, lg=-1):
+    f = lib().rtmi_test_slot_lg
     f.restype = C.c_int
-    f.argtypes = [C.c_void_p, C.c_int64]
-    assert f(ds.h, cap) == 0
+    f.argtypes = [C.c_void_p, C.c_int32]
+    r = f(ds.h, lg)
+    assert r >= 0
+    return r
 
 
-def test_entry_overflow_fails_the_call(gpu):
-    """A fill pass that runs out of entry capacity (forced by the test hook)
-    fails the call with RT_E_DEVICE — host path and device path, including a
-    device call without Stats (reported by the next call that reads them) —
-    and the next call after the cap is lifted renders the right frame."""
+@pytest.mark.parametrize("lg", [0, 1, 3])
+def test_list_past_its_slots_takes_the_bvh(gpu, lg):
+    """A pixel whose camera-ray list holds more faces than its 2^lg slots
+    (rt_frame.h) keeps its true length in the record, and its camera rays
+    take the BVH — the same answers: frames and Stats bit-identical to the
+    default slots, host path and device path (no failure mode). With 1 slot
+    most bunny pixels overflow; with 8 a few do."""
     import torch
     sc = scenes.mesh_bunny()
     ds = DeviceScene(sc)
     opts = Options(width=160, height=90, antialias=Antialias(akGrid, 16), bias=BIAS)
     ref = torch.zeros(160 * 90 * 3, dtype=torch.float32, device="cuda")
     sref = ds.render_device(opts, ref)
-    _entry_cap(ds, 16)
-    fb = np.zeros((90, 160, 3), np.float32)
-    with pytest.raises(RtmiError) as e:
-        ds.render_lines(opts, fb, 0, 90)
-    assert e.value.code == RT_E_DEVICE and "overflow" in str(e.value)
-    d = torch.zeros_like(ref)
-    with pytest.raises(RtmiError):
-        ds.render_device(opts, d)
-    ds.render_device(opts, d, stats=False)  # no wait, nothing read yet
-    with pytest.raises(RtmiError):
-        ds.last_split()  # the overflow is reported by the next read
-    ds.last_split()  # ... once
-    _entry_cap(ds, 0)
+    assert ds.last_batch()[1] == 0  # default slots: no general pixel falls back
+    default = _slot_lg(ds)
+    _slot_lg(ds, lg)
     out = torch.zeros_like(ref)
     assert ds.render_device(opts, out) == sref
     assert torch.equal(out, ref)
+    assert ds.last_batch()[1] > 0  # overflowed general pixels took the one-sample loop + BVH
     got = np.zeros((90, 160, 3), np.float32)
-    ds.render_lines(opts, got, 0, 90)
+    assert ds.render_lines(opts, got, 0, 90) == sref
     assert np.array_equal(got, ref.view(90, 160, 3).cpu().numpy())
+    _slot_lg(ds, default)
+    again = torch.zeros_like(ref)
+    assert ds.render_device(opts, again) == sref and torch.equal(again, ref)
 
 
 def test_last_split_describes_the_last_call(gpu):
