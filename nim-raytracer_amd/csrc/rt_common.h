@@ -253,11 +253,6 @@ struct FastParams {
   int32_t tx_shift;
   int32_t stat_flush;              // work items between flushes of the 32-bit wave Stats counters
   int32_t slot_lg;                 // pixel list slots per pixel: 2^slot_lg
-  // per-pixel shadow lists (rt_bins.h build_shadow_skips): pix_sl[2 (pixel *
-  // pix_sl_nl + light)] = start in pix_sl_ent, [.. + 1] = count (-1: none)
-  const int32_t* pix_sl;
-  const int32_t* pix_sl_ent;
-  int32_t pix_sl_nl;
   // k_render_mix1's second list (lean pixels, k_render_lean1q items) and its shard count
   const int32_t* order2;
   int32_t ngroups2, shards2;

@@ -1926,7 +1926,7 @@ __device__ __forceinline__ bool gen_batch(KP p, const GroupPix& gp, int it0, con
 // gen_batch does (a shadow ray that needs the BVH). Frames and Stats
 // bit-identical to gen_batch (tests/test_gpu_split.py, RT_FLAG_NO_GEN1).
 template <int S, int NL>
-__device__ __forceinline__ bool gen1_batch(KP p, const GroupPix& gp, int it0, unsigned pinfo, Acc& acc,
+__device__ __forceinline__ bool gen1_batch(KP p, const GroupPix& gp, int pu, int it0, unsigned pinfo, Acc& acc,
                                            Stats32& wi) {
   p = params();
   const int mesh = p->shadow_mesh, po = 1 - mesh;  // the scene's two objects
@@ -1996,7 +1996,6 @@ __device__ __forceinline__ bool gen1_batch(KP p, const GroupPix& gp, int it0, un
     }
     if (anyp != 0ull) {
       const KP q = params();
-      const int pu = __builtin_amdgcn_readfirstlane(gp.y * q->width + gp.x);
       const int b = pu << q->slot_lg;
       list_search_batch<S, true>(q, q->pix_slots, b, b + (int)(pinfo & kPixCount), (1u << S) - 1u,
                                  ro, rd, unused, nomask, key, unused, tc);
@@ -2107,44 +2106,6 @@ __device__ __forceinline__ bool gen1_batch(KP p, const GroupPix& gp, int it0, un
         for (int k = 0; k < S; ++k) {
           stop[k] = finf();
           if (mesh == 0) stop[k] = tpl[k] >= 0.0f ? fminf(stop[k], tpl[k]) : stop[k];
-        }
-        // the pixel's shadow list for this light (rt_bins.h: built for pixels
-        // whose camera rays only reach planes; every face a shadow ray from
-        // the pixel's footprint can hit, deduplicated): one search for all
-        // the batch's rays instead of the light-grid cells
-        if (q->pix_sl && li < q->pix_sl_nl) {
-          const int pu = __builtin_amdgcn_readfirstlane(gp.y * q->width + gp.x);
-          const int32_t* e = cp(q->pix_sl) + 2 * (pu * q->pix_sl_nl + li);
-          const int lb = e[0], lc = e[1];
-          if (lc >= 0) {
-            unsigned fl = 0u;
-            unsigned long long own[S];
-#pragma unroll
-            for (int k = 0; k < S; ++k) {
-              const bool part = lane_in(pm[k]);
-              stop[k] = fminf(stop[k], __uint_as_float(__float_as_uint(ts[k]) - 1u));
-              tc[k] = part ? ts[k] : -1.0f;
-              best[k] = part ? ts[k] : 0.0f;
-              unused[k] = 0ull;
-              own[k] = pm[k];
-              fl |= pm[k] != 0ull ? (1u << k) : 0u;
-            }
-            const int nt = list_search_batch<S, false>(q, q->pix_sl_ent, lb, lb + lc, fl, ro, rd, stop, own, unused,
-                                                       best, tc);
-#ifdef RTMI_DIAG_GEN_COUNT
-            wi.v[STAT_NODE_FETCH] += 1u;
-            wi.v[STAT_TRI_FETCH] += (unsigned)nt * (unsigned)__builtin_popcount(fl);
-#else
-            (void)nt;
-#endif
-#pragma unroll
-            for (int k = 0; k < S; ++k) {  // found => 0 <= t < ts: the hit counts
-              const bool c = lane_in(pm[k]) && __float_as_uint(best[k]) != __float_as_uint(ts[k]);
-              ts[k] = c ? best[k] : ts[k];
-              hitl += c ? 1u : 0u;
-            }
-            return true;
-          }
         }
         const RT_CONST LightGrid& G = cp(q->grids)[li];
         int cell[S];
@@ -2947,6 +2908,9 @@ __device__ __forceinline__ GroupPix lane_pixel(KP p, int g) {
 // k_render_lean1q's work loop over one list (order: 64 / LP entries per
 // item, ngroups items, dequeued from the shard heads at `queue`); also the
 // second phase of k_render_mix1.
+#ifndef RTMI_LEAN1Q_H
+#define RTMI_LEAN1Q_H 1
+#endif
 template <int NL, int LP>
 __device__ __forceinline__ void lean1q_loop(KP p, const int32_t* order, int ngroups, unsigned int* queue, int shards,
                                             Stats32& ws, unsigned long long* tot, int& nflush) {
@@ -2986,6 +2950,8 @@ __device__ __forceinline__ void lean1q_loop(KP p, const int32_t* order, int ngro
   const float st = p->sample_step, of = p->sample_off;
   static_assert(LP == 4 || LP == 8 || LP == 16, "lanes per pixel");
   constexpr int V = 64 / LP;   // virtual lanes per lane
+  constexpr int H = RTMI_LEAN1Q_H;  // virtual lanes per step (independent sample chains)
+  static_assert(H == 1 || H == 2, "one or two virtual lanes per step");
   constexpr int PPI = 64 / LP; // pixels per work item
   const int q = lane & (LP - 1);  // this lane's share of its pixel's virtual lanes
   // Every lit sample traces each light's shadow ray: against the plane here
@@ -3017,14 +2983,17 @@ __device__ __forceinline__ void lean1q_loop(KP p, const int32_t* order, int ngro
     // the binary-counter stack of the V virtual lanes' partial sums, two
     // virtual lanes at a time (two independent sample chains per step; their
     // sum is the tree's first level)
-    F3 s1 = f3(0.0f, 0.0f, 0.0f), s2 = s1, s3 = s1, sum = s1;
+    F3 s1 = f3(0.0f, 0.0f, 0.0f), s2 = s1, s3 = s1, sum = s1, s0 = s1;
     static_assert(V % 2 == 0, "virtual lanes in pairs");
     // the sample row of virtual lane jv in iteration it: (it * 64 + jv) >> lg
     // == it * (64 >> lg) + (jv >> lg) (m | 64), and jv >> lg == (q V) >> lg
     // for all of this lane's virtual lanes (m >= 16, rtmi.cpp lean1_ok, so V
     // divides 2^lg): one camera y per iteration for the whole lane, formed
     // from exact small-integer floats as k_render_lean1 steps them
-    const float rows = (float)(64 >> lg), sj0 = (float)((q * V) >> lg);
+    float rows = (float)(64 >> lg), sj0 = (float)((q * V) >> lg);
+    // formed per item (opaque): hoisted out of the item loop, the four
+    // per-lane row offsets below lived across every item and spilled
+    asm volatile("" : "+v"(sj0));
     float cyc[4];  // the camera y of four consecutive iterations from it0
     auto cy_rows = [&](int it0) {
 #pragma unroll
@@ -3035,11 +3004,11 @@ __device__ __forceinline__ void lean1q_loop(KP p, const int32_t* order, int ngro
     };
     if (iters == 4) cy_rows(0);  // one chunk (m = 16): once per item
 #pragma unroll 1
-    for (int j = 0; j < V; j += 2) {
-      float q0[2], ay[2];
-      F3 acc[2];
+    for (int j = 0; j < V; j += H) {
+      float q0[H], ay[H];
+      F3 acc[H];
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
+      for (int h = 0; h < H; ++h) {
         const int jv = q * V + j + h;  // the virtual lane (k_render_lean1's lane)
         const float px = pxb + __builtin_fmaf((float)(jv & mm), st, of);
         const float cx = (px - p->cam_b) * p->cam_a;
@@ -3054,7 +3023,7 @@ __device__ __forceinline__ void lean1q_loop(KP p, const int32_t* order, int ngro
 #pragma unroll
       for (int it = 0; it < 4; ++it)
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
+      for (int h = 0; h < H; ++h) {
         const float cy = cyc[it];
         const float rl = rsq(__builtin_fmaf(cy, cy, q0[h]));
         const float dy = __builtin_fmaf(cy, p->cam[7], ay[h]) * rl;
@@ -3086,9 +3055,18 @@ __device__ __forceinline__ void lean1q_loop(KP p, const int32_t* order, int ngro
       }
       }
       // push the pair's sum: pair index P = j / 2 pairs with the stack while
-      // it has trailing ones (uniform branches)
+      // it has trailing ones (uniform branches); one virtual lane per step
+      // (H = 1): the even one waits in s0 for its odd partner (the same sum)
+      F3 lo = acc[0], hi = acc[H - 1];
+      if constexpr (H == 1) {
+        if ((j & 1) == 0) {
+          s0 = acc[0];
+          continue;
+        }
+        lo = s0;
+      }
       const int P = j >> 1;
-      F3 t = f3(acc[0].x + acc[1].x, acc[0].y + acc[1].y, acc[0].z + acc[1].z);
+      F3 t = f3(lo.x + hi.x, lo.y + hi.y, lo.z + hi.z);
       if (P & 1) {
         t = f3(s1.x + t.x, s1.y + t.y, s1.z + t.z);
         if (P & 2) {
@@ -3101,7 +3079,7 @@ __device__ __forceinline__ void lean1q_loop(KP p, const int32_t* order, int ngro
       } else {
         s1 = t;
       }
-      if (j + 2 == V) sum = t;  // the lane's sum
+      if (j + H == V) sum = t;  // the lane's sum
     }
     // the pixel's lanes pairwise: xor 1 and 2 by quad permutes (DPP), then
     // xor 4, 8, ... by shuffles
@@ -3140,8 +3118,11 @@ __device__ __forceinline__ void lean1q_loop(KP p, const int32_t* order, int ngro
   }
 }
 
+#ifndef RTMI_LEAN1Q_WAVES
+#define RTMI_LEAN1Q_WAVES 8
+#endif
 template <int NL, int LP>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k_render_lean1q(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RTMI_LEAN1Q_WAVES))) void k_render_lean1q(
     const FastParams params_by_value) {
   (void)params_by_value;
   const KP p = params();
@@ -3282,7 +3263,15 @@ __device__ __forceinline__ void gen1_loop(KP p, LdsF* ls, Stats32& ws, unsigned 
     const int gg = cp(p->order)[g];
     GroupPix gp = group_pixel(p, gg, lane_id_fresh());
     gp.valid = true;  // the lists hold only pixels of the launch (rtmi.cpp split_lists)
-    const unsigned pinfo = at(p->pix_info, __builtin_amdgcn_readfirstlane(gp.y * p->width + gp.x));
+    // a one-pixel group: its placement is wave-uniform (scalar registers;
+    // per lane it stayed live as 64-bit products across the item and spilled)
+    gp.x = __builtin_amdgcn_readfirstlane(gp.x);
+    gp.y = __builtin_amdgcn_readfirstlane(gp.y);
+    gp.out_row = __builtin_amdgcn_readfirstlane(gp.out_row);
+    // the pixel index once per item, wave-uniform (recomputed per batch from
+    // the lane's placement it kept a 64-bit product live and spilled)
+    const int pu = __builtin_amdgcn_readfirstlane(gp.y * p->width + gp.x);
+    const unsigned pinfo = at(p->pix_info, pu);
     Acc acc;
     acc.v = f3(0.0f, 0.0f, 0.0f);
     Stats32 wi;
@@ -3291,7 +3280,7 @@ __device__ __forceinline__ void gen1_loop(KP p, LdsF* ls, Stats32& ws, unsigned 
     // a pixel list past its slots (rt_frame.h): the one-sample loop, whose
     // camera rays take the BVH for this pixel
     bool ok = (pinfo & kPixCount) <= (1u << p->slot_lg);
-    for (int it = 0; ok && it < iters; it += kGenBatch) ok = gen1_batch<kGenBatch, NL>(p, gp, it, pinfo, acc, wi);
+    for (int it = 0; ok && it < iters; it += kGenBatch) ok = gen1_batch<kGenBatch, NL>(p, gp, pu, it, pinfo, acc, wi);
     if (params()->flags & RT_DEV_FLAG_FALLBACK) ok = false;  // test hook (RT_FLAG_BATCH_FALLBACK)
     if (ok) {
       ws.v[STAT_PRIMARY] += wi.v[STAT_PRIMARY];

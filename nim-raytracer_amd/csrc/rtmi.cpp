@@ -1282,6 +1282,7 @@ int frame_buffers(rt_scene* s, int w, int h, hipStream_t st) {
   // the ones a call used)
   HIP_TRY(hipMemset(f.cnt.p, 0, f.cnt.bytes()));
   HIP_TRY(hipMemset(f.ctr.p, 0, f.ctr.bytes()));
+  HIP_TRY(hipMemset(f.info.p, 0, f.info.bytes()));  // (only read for the call's pixels; defined for the test hook)
   f.w = w;
   f.h = h;
   return RT_OK;
