@@ -1528,17 +1528,27 @@ __device__ __forceinline__ void tri_test_t(const TR& T, F3 o, F3 d, float& best,
 // for — own[k], the lanes whose ray lies in this cell — is left: the other
 // lanes test these faces only as a harmless superset, their own cell is
 // searched in its turn).
+// diag (RTMI_DIAG_LANES builds, else nullptr): += the lanes still searching
+// at each face test of each flagged sample (lane occupancy of the search).
 template <int S, bool KEY>
 __device__ __forceinline__ int list_search_batch(KP p, const int32_t* ent, int b, int e, unsigned fl,
                                                   const F3 (&ro)[S], const F3 (&rd)[S], const float (&stop)[S],
                                                   const unsigned long long (&own)[S], unsigned long long (&key)[S],
-                                                  float (&best)[S], float (&tc)[S]) {
+                                                  float (&best)[S], float (&tc)[S], unsigned* diag = nullptr) {
   const int b_in = b;  // returns the number of faces tested (diagnostics)
+  auto lanes = [&]() {
+    if (diag) {
+#pragma unroll
+      for (int k = 0; k < S; ++k)
+        if ((fl >> k) & 1u) *diag += pc(bal(tc[k] >= 0.0f));
+    }
+  };
   if constexpr (!KEY) {
     // a cell's first face alone: it is the one covering most of the cell
     // (rt_bins.cpp), so lanes in the umbra retire after one test
     if (b < e) {
       const TriRegs T = load_tri(rec<TriFast>(p, cp(ent)[b]));
+      lanes();
       unsigned long long left = 0ull;
 #pragma unroll
       for (int k = 0; k < S; ++k)
@@ -1588,6 +1598,7 @@ __device__ __forceinline__ int list_search_batch(KP p, const int32_t* ent, int b
 #else
       const TriRegs T = load_tri(rec<TriFast>(p, r[j]));
 #endif
+      lanes();
 #pragma unroll
       for (int k = 0; k < S; ++k)
         if ((fl >> k) & 1u) {
@@ -1997,8 +2008,16 @@ __device__ __forceinline__ bool gen1_batch(KP p, const GroupPix& gp, int pu, int
     if (anyp != 0ull) {
       const KP q = params();
       const int b = pu << q->slot_lg;
+#ifdef RTMI_DIAG_LANES  // diagnostic: camera face tests (x samples) and the lanes still searching
+      unsigned dl = 0u;
+      wi.v[STAT_TRI_FETCH] += (unsigned)(pinfo & kPixCount) * (unsigned)S;
+      list_search_batch<S, true>(q, q->pix_slots, b, b + (int)(pinfo & kPixCount), (1u << S) - 1u,
+                                 ro, rd, unused, nomask, key, unused, tc, &dl);
+      wi.v[STAT_LANE_TRIS] += dl;
+#else
       list_search_batch<S, true>(q, q->pix_slots, b, b + (int)(pinfo & kPixCount), (1u << S) - 1u,
                                  ro, rd, unused, nomask, key, unused, tc);
+#endif
     }
 #pragma unroll
     for (int k = 0; k < S; ++k) {
@@ -2151,8 +2170,16 @@ __device__ __forceinline__ bool gen1_batch(KP p, const GroupPix& gp, int pu, int
 #ifdef RTMI_DIAG_GEN_NOTESTS
           continue;  // diagnostic build only (wrong images): the cell loop without its face tests
 #endif
+#ifdef RTMI_DIAG_LANES  // diagnostic: shadow face tests (x flagged samples) and the lanes still searching
+          unsigned dl = 0u;
+          const int nt = list_search_batch<S, false>(q, bent, cp(q->grid_off)[kb], cp(q->grid_off)[kb + 1], fl, ro, rd,
+                                                     stop, own, unused, best, tc, &dl);
+          wi.v[STAT_NODE_FETCH] += (unsigned)nt * (unsigned)__builtin_popcount(fl);
+          wi.v[STAT_LANE_NODES] += dl;
+#else
           const int nt = list_search_batch<S, false>(q, bent, cp(q->grid_off)[kb], cp(q->grid_off)[kb + 1], fl, ro, rd,
                                                      stop, own, unused, best, tc);
+#endif
 #ifdef RTMI_DIAG_GEN_COUNT
           wi.v[STAT_NODE_FETCH] += 1u;                                      // diagnostic: cells searched
           wi.v[STAT_TRI_FETCH] += (unsigned)nt * (unsigned)__builtin_popcount(fl);  // wave face tests
@@ -3204,7 +3231,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RTMI_GEN_WA
       ws.v[STAT_PRIMARY] += wi.v[STAT_PRIMARY];
       ws.v[STAT_SHADOW] += wi.v[STAT_SHADOW];
       ws.v[STAT_HITS] += wi.v[STAT_HITS];
-#ifdef RTMI_DIAG_GEN_COUNT
+#if defined(RTMI_DIAG_GEN_COUNT) || defined(RTMI_DIAG_LANES)
       for (int q = STAT_NODE_FETCH; q <= STAT_LANE_TRIS; ++q) ws.v[q] += wi.v[q];
 #endif
     } else {  // some shadow ray needs the BVH: the whole pixel by the one-sample loop
@@ -3286,7 +3313,7 @@ __device__ __forceinline__ void gen1_loop(KP p, LdsF* ls, Stats32& ws, unsigned 
       ws.v[STAT_PRIMARY] += wi.v[STAT_PRIMARY];
       ws.v[STAT_SHADOW] += wi.v[STAT_SHADOW];
       ws.v[STAT_HITS] += wi.v[STAT_HITS];
-#ifdef RTMI_DIAG_GEN_COUNT
+#if defined(RTMI_DIAG_GEN_COUNT) || defined(RTMI_DIAG_LANES)
       for (int q = STAT_NODE_FETCH; q <= STAT_LANE_TRIS; ++q) ws.v[q] += wi.v[q];
 #endif
     } else {  // some shadow ray needs the BVH: the whole pixel by the one-sample loop

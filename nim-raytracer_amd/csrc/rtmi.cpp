@@ -1510,7 +1510,11 @@ int fill_fast(rt_scene* s, const rt_options* o, const Mapping& mp, float* fb, Fa
     const uint64_t levels = s->any_reflective ? (uint64_t)std::min(kMaxShadeLevels, std::max(1, o->max_ray_depth + 1)) : 1ull;
     const uint64_t per_item = 64ull * (uint64_t)p.iters * levels * (1ull + (uint64_t)s->nlight) *
                               (uint64_t)std::max(1, s->nobj);
-    p.stat_flush = (o->flags & RT_FLAG_COUNT_TRAVERSAL) ? 1 : (int32_t)std::min<uint64_t>(1u << 20, std::max<uint64_t>(1, 0xFFFFFFFFull / per_item));
+    // diagnostic builds with wider counters (RTMI_DIAG_LANES): RTMI_STAT_FLUSH=1 flushes every item
+    static const int flush_env = std::getenv("RTMI_STAT_FLUSH") ? std::atoi(std::getenv("RTMI_STAT_FLUSH")) : 0;
+    p.stat_flush = (o->flags & RT_FLAG_COUNT_TRAVERSAL) ? 1
+                   : flush_env > 0 ? flush_env
+                                   : (int32_t)std::min<uint64_t>(1u << 20, std::max<uint64_t>(1, 0xFFFFFFFFull / per_item));
   }
   // binned searches (rt_bins.h): camera rays when a wave spans at most 4
   // pixels (>= 16 samples per pixel), shadow rays to distant lights

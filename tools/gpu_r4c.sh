@@ -22,3 +22,9 @@ cat $O/scaling_sim.json
 VARIANTS="default r3 h2" SCENES="mesh-bunny:1920x1080:16 mesh-mix:1920x1080:8 boxes2:1920x1080:8" REPS=3 bash tools/gpu_ab_scenes.sh || exit 1
 mkdir -p $O/ab && cp gpurun_out/ab/*.log $O/ab/
 python tools/ab_report.py gpurun_out/ab setup_ms; python tools/ab_report.py gpurun_out/ab call_ms
+RTMI_LIB=$PWD/tools/ab/lanes.so RTMI_STAT_FLUSH=1 timeout -k 10 300 python tools/lanes_probe.py > $O/lanes_probe.json 2> $O/lanes.err || exit 1
+cat $O/lanes_probe.json
+# row n1 on C5 (the scene that overflows L2): LDS-staged face records A/B
+VARIANTS="default lds" SCENES="torus:3840x2160:64" REPS=2 bash tools/gpu_ab_scenes.sh || exit 1
+mkdir -p $O/ab_lds && cp gpurun_out/ab/*.log $O/ab_lds/
+python tools/ab_report.py gpurun_out/ab render_ms
