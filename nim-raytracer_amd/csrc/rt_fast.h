@@ -1201,6 +1201,25 @@ __device__ __forceinline__ void batch_dirs(KP p, const GroupPix& gp, int it0, co
 // irradiance sum), the samples' colours added to the pixel in sample order:
 // frames bit-identical to the one-sample loop (tests: binned vs
 // RT_FLAG_NO_BINNING, which takes no pixel records).
+// trace's hit rule "t >= 0 and t < lim" (renderer.nim:58-62) for a limit lim
+// in [+0, +inf] as ONE unsigned compare of the float bits: non-negative
+// floats order like their bit patterns, a negative t or a NaN has bits above
+// every such lim, and t + 0.0f turns -0.0 (which the rule accepts) into
+// +0.0 and leaves every other value as it is. The float form is two compares
+// and a scalar AND of their lane masks per ray and object (the batches'
+// busiest pipe is the CU's one scalar unit). A sample that takes no part
+// holds lim = +0.0, below which nothing lies. RTMI_HIT_UINT=0: the float form.
+#ifndef RTMI_HIT_UINT
+#define RTMI_HIT_UINT 1
+#endif
+__device__ __forceinline__ bool hit_below(float t, float lim) {
+#if RTMI_HIT_UINT
+  return __float_as_uint(t + 0.0f) < __float_as_uint(lim);
+#else
+  return t >= 0.0f && t < lim;
+#endif
+}
+
 #ifndef RTMI_LEAN_BATCH
 #define RTMI_LEAN_BATCH 4
 #endif
@@ -1238,7 +1257,7 @@ __device__ __forceinline__ void lean_batch(KP p, const GroupPix& gp, int it0, co
 #pragma unroll
   for (int k = 0; k < S; ++k) {
     nprim += pc(bal(sv[k]));
-    th[k] = sv[k] ? finf() : -1.0f;
+    th[k] = sv[k] ? finf() : (RTMI_HIT_UINT ? 0.0f : -1.0f);  // (hit_below: +0 takes no hit)
     hob[k] = -1;
   }
   ws.v[STAT_PRIMARY] += nprim;
@@ -1286,7 +1305,7 @@ __device__ __forceinline__ void lean_batch(KP p, const GroupPix& gp, int it0, co
     const FObj ob = at(objs, i);
     analytic_t_batch<F, S>(p, ob, i, oc, d, [&](int k, float t) {
       // trace's rule (t >= 0 ? t : inf) < th, as two compares (th <= inf)
-      const bool c = t >= 0.0f && t < th[k];
+      const bool c = hit_below(t, th[k]);
       th[k] = c ? t : th[k];
       hob[k] = c ? i : hob[k];
       hitl += c ? 1u : 0u;
@@ -1298,7 +1317,7 @@ __device__ __forceinline__ void lean_batch(KP p, const GroupPix& gp, int it0, co
   F3 N[S], so[S];
 #pragma unroll
   for (int k = 0; k < S; ++k) {
-    litm[k] = m_lt(th[k], finf()) & m_ge(th[k], 0.0f);
+    litm[k] = bal(hob[k] >= 0);  // (a hit beat th's start: +inf, or +0 for a sample that takes no part)
     pend[k] = litm[k];
     N[k] = f3(0.0f, 0.0f, 0.0f);
     so[k] = f3(__builtin_fmaf(d[k].x, th[k], o.x), __builtin_fmaf(d[k].y, th[k], o.y),
@@ -1430,7 +1449,7 @@ __device__ __forceinline__ void lean_batch(KP p, const GroupPix& gp, int it0, co
             F3 ro, rd;
             to_object<F>(p, ob, i, so[k], sd, ro, rd);
             const float t = -ro.y * mulp;
-            const bool c = t >= 0.0f && t < ts[k];
+            const bool c = hit_below(t, ts[k]);
             ts[k] = c ? t : ts[k];
             hitl += c ? 1u : 0u;
           }
@@ -1439,7 +1458,7 @@ __device__ __forceinline__ void lean_batch(KP p, const GroupPix& gp, int it0, co
 #pragma unroll
           for (int k = 0; k < S; ++k) sdk[k] = sd;
           analytic_t_batch<F, S>(p, ob, i, so, sdk, [&](int k, float t) {
-            const bool c = t >= 0.0f && t < ts[k];
+            const bool c = hit_below(t, ts[k]);
             ts[k] = c ? t : ts[k];
             hitl += c ? 1u : 0u;
           });

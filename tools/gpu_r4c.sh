@@ -19,7 +19,7 @@ timeout -k 10 300 python tools/host_overhead.py > $O/host_overhead.json 2> $O/ho
 cat $O/host_overhead.json
 BANDS=4 timeout -k 10 300 python tools/scaling_sim.py > $O/scaling_sim.json 2> $O/ss.err || exit 1
 cat $O/scaling_sim.json
-VARIANTS="default r3 h2" SCENES="mesh-bunny:1920x1080:16 mesh-mix:1920x1080:8 boxes2:1920x1080:8" REPS=3 bash tools/gpu_ab_scenes.sh || exit 1
+VARIANTS="default r3 h2 hitf" SCENES="mesh-bunny:1920x1080:16 mesh-mix:1920x1080:8 boxes2:1920x1080:8" REPS=3 bash tools/gpu_ab_scenes.sh || exit 1
 mkdir -p $O/ab && cp gpurun_out/ab/*.log $O/ab/
 python tools/ab_report.py gpurun_out/ab setup_ms; python tools/ab_report.py gpurun_out/ab call_ms
 RTMI_LIB=$PWD/tools/ab/lanes.so RTMI_STAT_FLUSH=1 timeout -k 10 300 python tools/lanes_probe.py > $O/lanes_probe.json 2> $O/lanes.err || exit 1
