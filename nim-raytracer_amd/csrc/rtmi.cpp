@@ -1371,8 +1371,12 @@ int frame_build(rt_scene* s, const rt_options* o, const Mapping& mp, const FastP
   a.nzero = nzero;
   // k_frame_build2's persistent grid: two blocks per CU, far below what
   // stays resident (its look-back waits on earlier chunks only)
-  if ((rc = rtmi_frame_build(&a, 2 * s->num_cus, st)))
+  if ((rc = rtmi_frame_build(&a, 2 * s->num_cus, st))) {
+    // the first launch may have run (its counters non-zero, zeroed only by
+    // the second): the next call re-allocates and re-zeroes the buffers
+    f.invalidate();
     return fail(RT_E_DEVICE, "frame build launch failed: %s", hipGetErrorString((hipError_t)rc));
+  }
   f.listed = true;
   *zeroed = zero != nullptr;
   *ok = true;
