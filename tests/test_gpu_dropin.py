@@ -149,13 +149,13 @@ def test_list_past_its_slots_takes_the_bvh(gpu, lg):
     opts = Options(width=160, height=90, antialias=Antialias(akGrid, 16), bias=BIAS)
     ref = torch.zeros(160 * 90 * 3, dtype=torch.float32, device="cuda")
     sref = ds.render_device(opts, ref)
-    assert ds.last_batch()[1] == 0  # default slots: no general pixel falls back
+    fb0 = ds.last_batch()[1]  # (at 160x90 the bunny's pixels list many faces: some overflow 32 slots too)
     default = _slot_lg(ds)
     _slot_lg(ds, lg)
     out = torch.zeros_like(ref)
     assert ds.render_device(opts, out) == sref
     assert torch.equal(out, ref)
-    assert ds.last_batch()[1] > 0  # overflowed general pixels took the one-sample loop + BVH
+    assert ds.last_batch()[1] > fb0  # more overflowed general pixels took the one-sample loop + BVH
     got = np.zeros((90, 160, 3), np.float32)
     assert ds.render_lines(opts, got, 0, 90) == sref
     assert np.array_equal(got, ref.view(90, 160, 3).cpu().numpy())
