@@ -1330,6 +1330,10 @@ __device__ __forceinline__ void lean_batch(KP p, const GroupPix& gp, int it0, co
   constexpr bool kPlanesOnly = !(F & (F_SPHERE | F_BOX));
   int nhobj = 0;
   F3 Nu = f3(0.0f, 0.0f, 0.0f), alb_u = f3(0.0f, 0.0f, 0.0f);
+#ifdef RTMI_DIAG_OB_NONORMAL
+#pragma unroll
+  for (int k = 0; k < S; ++k) pend[k] = 0ull;  // diagnostic build only (wrong images): the normal pass's share
+#endif
   for (;;) {
     const int oi = first_pending<S>(pend, hob);
     if (oi < 0) break;

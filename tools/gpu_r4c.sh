@@ -28,3 +28,7 @@ cat $O/lanes_probe.json
 VARIANTS="default lds" SCENES="torus:3840x2160:64" REPS=2 bash tools/gpu_ab_scenes.sh || exit 1
 mkdir -p $O/ab_lds && cp gpurun_out/ab/*.log $O/ab_lds/
 python tools/ab_report.py gpurun_out/ab render_ms
+# C2 (boxes2) cost breakdown: diagnostic builds with parts of the object-binned batch switched off (wrong images, timing only)
+VARIANTS="default hitf obnoshadow obnocam obnonormal nosamples" SCENES="boxes2:1920x1080:8" REPS=2 bash tools/gpu_ab_scenes.sh || exit 1
+mkdir -p $O/ab_c2 && cp gpurun_out/ab/*.log $O/ab_c2/
+python tools/ab_report.py gpurun_out/ab render_ms
