@@ -98,9 +98,10 @@ enum : int32_t { FC_OVERFLOW = 0, FC_HEAVY = 1, FC_LEAN = 2, FC_HUGE0 = 3, FC_HU
 #endif
 constexpr int kBigFace = RTMI_BIG_FACE, kHugeCap = 4096;
 
-// Per-pixel list slots: 2^kSlotLg record offsets per pixel (32: C3 at 1080p
+// Per-pixel list slots: at least 2^kSlotLg record offsets per pixel (the
+// host gives small images more, up to 256: rtmi.cpp slot_lg_for). C3 at 1080p
 // lists at most 28 faces per pixel, p99 11; the 1M-face torus at 4K 99, p999
-// 34 — its 1,490 pixels past 32 take the BVH).
+// 34 — its 1,490 pixels past 32 take the BVH.
 #ifndef RTMI_SLOT_LG
 #define RTMI_SLOT_LG 5
 #endif

@@ -134,13 +134,21 @@ int device_of_current() {
 
 }  // namespace
 
-// Pixel-list slots per pixel, 2^lg (rt_frame.h kSlotLg; RTMI_SLOT_LG: A/B knob).
+// Pixel-list slots per pixel, 2^lg: RTMI_SLOT_LG (A/B knob) or -1 = by image size.
 inline int slot_lg_env() {
   static const int v = [] {
     const char* e = std::getenv("RTMI_SLOT_LG");
-    return e ? std::min(10, std::max(0, std::atoi(e))) : rtmi::kSlotLg;
+    return e ? std::min(10, std::max(0, std::atoi(e))) : -1;
   }();
   return v;
+}
+// by image size: the most slots (a power of two, 2^kSlotLg .. 256) whose
+// block stays within 2^27 entries
+inline int slot_lg_for(int w, int h) {
+  const unsigned long long npx = (unsigned long long)w * (unsigned long long)h;
+  int lg = rtmi::kSlotLg;
+  while (lg < 8 && (npx << (lg + 1)) <= (1ull << 27)) ++lg;
+  return lg;
 }
 
 struct rt_scene {
@@ -221,7 +229,7 @@ struct rt_scene {
     DevBuf<HugeFace> huge;
     DevBuf<unsigned char> tiles;   // per-tile shadow skips (k_frame_build1)
     int slot_lg = -1;              // slots allocated for 2^slot_lg entries per pixel (-1: none)
-    int want_lg = slot_lg_env();   // test hook (rtmi_test_slot_lg) / RTMI_SLOT_LG
+    int want_lg = slot_lg_env();   // test hook (rtmi_test_slot_lg) / RTMI_SLOT_LG; -1: by image size
     uint32_t calls = 0;            // build launches (their parity picks the huge-list counter)
     bool counted = false;          // the last launch's lean / general lists were counted on the device
     bool listed = false;           // the last launch built camera-ray lists
@@ -1256,7 +1264,13 @@ FrameRows frame_rows(const Mapping& mp, int height) {
 int frame_buffers(rt_scene* s, int w, int h, hipStream_t st) {
   rt_scene::Frame& f = s->fr;
   const bool lists = s->binnable && !s->bin_tris.empty();
-  if (f.w == w && f.h == h && (!lists || f.slot_lg == f.want_lg)) return RT_OK;
+  // slots per pixel: 2^want_lg when set (test hook / RTMI_SLOT_LG), else
+  // as many as 2^27 entries (512 MB) allow, 32 to 256: a mesh's per-pixel
+  // lists are longer the fewer pixels it covers (the bunny: 28 faces at most
+  // at 1080p, past 32 for 7 % of its pixels at 320x180); a pixel past its
+  // slots takes the BVH (exact, slower)
+  const int lg = f.want_lg >= 0 ? f.want_lg : slot_lg_for(w, h);
+  if (f.w == w && f.h == h && (!lists || f.slot_lg == lg)) return RT_OK;
   // an earlier call may still read the old buffers: the call's stream waits
   // on the scene's last call (render_device), whose aux-stream kernels are
   // joined into its done event, so this one wait covers them all
@@ -1273,10 +1287,10 @@ int frame_buffers(rt_scene* s, int w, int h, hipStream_t st) {
   if (lists) {
     // the slots hold valid record offsets from the start (the list search
     // reads up to kBinPad entries past a list's end)
-    const size_t ns = (npx << f.want_lg) + kBinPad;
+    const size_t ns = (npx << lg) + kBinPad;
     if ((rc = f.slots.alloc(ns)) || (rc = f.huge.alloc(kHugeCap))) return rc;
     HIP_TRY(hipMemsetD32(f.slots.p, s->bin_tris[0].rec, ns));
-    f.slot_lg = f.want_lg;
+    f.slot_lg = lg;
   }
   // the per-pixel counters are zero between calls (k_frame_build2 zeroes
   // the ones a call used)
@@ -2202,7 +2216,7 @@ extern "C" int rtmi_test_slot_lg(rt_scene* s, int32_t lg) {
   if (!s || lg > 10) return fail(RT_E_INVALID, "bad argument");
   std::lock_guard<std::mutex> lk(s->mu);
   if (lg >= 0) s->fr.want_lg = lg;
-  return s->fr.want_lg;
+  return s->fr.slot_lg;
 }
 
 // The last render call's device-built camera-ray lists and pixel records
