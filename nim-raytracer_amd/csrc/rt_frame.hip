@@ -257,32 +257,55 @@ __device__ __forceinline__ int build2_tile(const FrameLaunch& a, int t, int nhug
   return r.split ? pixel_class(r, p, info) : 0;
 }
 
+// k_frame_build2: one tile per block, all of them at once (a pixel's own
+// skip test is a long float64 chain: tiles taken in turn by a persistent
+// grid serialised those chains, 90 us per C3 call).
 __global__ __launch_bounds__(256) void k_frame_build2(const FrameLaunch a) {
   __shared__ bg::SkipGrid sg[8];
   __shared__ int32_t hl[256];
   __shared__ int hn;
-  __shared__ uint8_t cls[kChunkTiles][256];       // the chunk's pixel classes
+  const RecordsLaunch& r = a.r;
+  if (r.records && r.have != 0u) load_skip_grids(r, sg);
+  const int nhuge = min(r.ctr[FC_HUGE0 + a.parity], kHugeCap);
+  (void)build2_tile(a, (int)blockIdx.x, nhuge, sg, hl, &hn);
+}
+
+// k_frame_lists: the lean / general lists (two-class launches), persistent
+// blocks over chunks of kChunkTiles tiles in order: each thread loads its
+// pixel's record in each of the chunk's tiles (all loads in flight), the
+// per-tile class counts go through LDS, the chunk's granule is published and
+// its predecessors' summed (look-back), and the chunk's pixels are written at
+// their offsets.
+__global__ __launch_bounds__(256) void k_frame_lists(const FrameLaunch a) {
   __shared__ unsigned long long wpart[4];          // per-wave partial counts
   __shared__ unsigned long long wsum[kChunkTiles][4];
   __shared__ int first_s, bad_s;
   const RecordsLaunch& r = a.r;
-  if (r.records && r.have != 0u) load_skip_grids(r, sg);
-  const int nhuge = min(r.ctr[FC_HUGE0 + a.parity], kHugeCap);
   const int tid = (int)threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int nchunks = (a.ntiles + kChunkTiles - 1) / kChunkTiles;
   for (int c = (int)blockIdx.x; c < nchunks; c += (int)gridDim.x) {
-    const int t0 = c * kChunkTiles, t1 = min(t0 + kChunkTiles, a.ntiles);
-    for (int t = t0; t < t1; ++t) {
-      const int cl = build2_tile(a, t, nhuge, sg, hl, &hn);
-      if (!r.split) continue;
-      cls[t - t0][tid] = (uint8_t)cl;
-      const unsigned long long ml = __ballot(cl == 1), mh = __ballot(cl == 2);
-      if (lane == 0) wsum[t - t0][w] = (unsigned long long)__popcll(ml) * kLeanOne + (unsigned long long)__popcll(mh);
+    const int t0 = c * kChunkTiles;
+    uint32_t inf[kChunkTiles];
+    LaunchPix px[kChunkTiles];
+#pragma unroll
+    for (int i = 0; i < kChunkTiles; ++i) {
+      const int t = t0 + i;
+      const int bx = t % a.tiles_x, by = t / a.tiles_x;
+      px[i] = launch_pixel(r, bx * kTileW + lane, by * kTileH + w);
+      px[i].valid = px[i].valid && t < a.ntiles;
+      inf[i] = px[i].valid ? r.info[(size_t)px[i].y * r.width + px[i].x] : 0u;
     }
-    if (!r.split) continue;
-    __syncthreads();
+    int cls[kChunkTiles];
     unsigned long long agg = 0ull;
-    for (int t = t0; t < t1; ++t) agg += wsum[t - t0][0] + wsum[t - t0][1] + wsum[t - t0][2] + wsum[t - t0][3];
+#pragma unroll
+    for (int i = 0; i < kChunkTiles; ++i) {
+      cls[i] = px[i].valid ? pixel_class(r, px[i], inf[i]) : 0;
+      const unsigned long long ml = __ballot(cls[i] == 1), mh = __ballot(cls[i] == 2);
+      if (lane == 0) wsum[i][w] = (unsigned long long)__popcll(ml) * kLeanOne + (unsigned long long)__popcll(mh);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < kChunkTiles; ++i) agg += wsum[i][0] + wsum[i][1] + wsum[i][2] + wsum[i][3];
     // publish, then look back (every thread one predecessor per step)
     if (tid == 0) granule_store(&a.status[c], (c == 0 ? kStIncl : kStAgg) | agg);
     unsigned long long excl = 0ull;
@@ -328,18 +351,19 @@ __global__ __launch_bounds__(256) void k_frame_build2(const FrameLaunch a) {
     }
     // the chunk's pixels into the lists at their offsets (wave ballots, mbcnt ranks)
     unsigned long long base = excl;
-    for (int t = t0; t < t1; ++t) {
-      const int cl = cls[t - t0][tid];
-      const unsigned long long ml = __ballot(cl == 1), mh = __ballot(cl == 2);
+#pragma unroll
+    for (int i = 0; i < kChunkTiles; ++i) {
+      const int t = t0 + i;
+      const unsigned long long ml = __ballot(cls[i] == 1), mh = __ballot(cls[i] == 2);
       unsigned long long b = base;
-      for (int i = 0; i < w; ++i) b += wsum[t - t0][i];
+      for (int q = 0; q < w; ++q) b += wsum[i][q];
       const int bx = t % a.tiles_x, by = t / a.tiles_x;
       const int g = (by * kTileH + w) * r.ncols + bx * kTileW + lane;
-      if (cl == 1) r.lean[(int)(b >> 31) + (int)lane_rank(ml)] = g;
-      if (cl == 2) r.heavy[(int)(b & (kLeanOne - 1ull)) + (int)lane_rank(mh)] = g;
-      base += wsum[t - t0][0] + wsum[t - t0][1] + wsum[t - t0][2] + wsum[t - t0][3];
+      if (cls[i] == 1) r.lean[(int)(b >> 31) + (int)lane_rank(ml)] = g;
+      if (cls[i] == 2) r.heavy[(int)(b & (kLeanOne - 1ull)) + (int)lane_rank(mh)] = g;
+      base += wsum[i][0] + wsum[i][1] + wsum[i][2] + wsum[i][3];
     }
-    if (t1 == a.ntiles) {  // the last chunk: the list lengths, the lean list's -1 padding
+    if (c == nchunks - 1) {  // the last chunk: the list lengths, the lean list's -1 padding
       const int nl = (int)(base >> 31), nh = (int)(base & (kLeanOne - 1ull));
       if (tid == 0) {
         r.ctr[FC_LEAN] = nl;
@@ -348,10 +372,9 @@ __global__ __launch_bounds__(256) void k_frame_build2(const FrameLaunch a) {
       const int end = nl == 0 ? 64 : (nl + 63) / 64 * 64;
       for (int e = nl + tid; e < end; e += 256) r.lean[e] = -1;
     }
-    __syncthreads();  // cls / wsum reused by the next chunk
+    __syncthreads();  // wsum reused by the next chunk
   }
 }
-
 
 // Object masks (rt_bins.cpp build_object_pixel_masks). k_frame_obj_rects
 // projects every object's world box once, one thread per (object, corner)
@@ -440,8 +463,10 @@ extern "C" int rtmi_frame_build(const rtmi::FrameLaunch* a, int build2_blocks, v
   hipLaunchKernelGGL(k_frame_build1, dim3(face_blocks + tile_blocks), dim3(256), 0, st, *a, face_blocks);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || a->ntiles <= 0) return (int)e;
+  hipLaunchKernelGGL(k_frame_build2, dim3((unsigned)a->ntiles), dim3(256), 0, st, *a);
+  if ((e = hipGetLastError()) != hipSuccess || !a->r.split) return (int)e;
   const int nchunks = (a->ntiles + kChunkTiles - 1) / kChunkTiles;
-  hipLaunchKernelGGL(k_frame_build2, dim3((unsigned)std::max(1, std::min(build2_blocks, nchunks))), dim3(256), 0, st,
+  hipLaunchKernelGGL(k_frame_lists, dim3((unsigned)std::max(1, std::min(build2_blocks, nchunks))), dim3(256), 0, st,
                      *a);
   return (int)hipGetLastError();
 }
