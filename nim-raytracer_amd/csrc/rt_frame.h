@@ -8,7 +8,7 @@
 // camera is kept from one render call to the next. What is built once per
 // scene (rt_scene_create) depends only on the scene's geometry and lights:
 // the BVH, the light grids and their occupancy prefix sums, the faces'
-// float64 vertices. Each render call runs, on its own stream, TWO build
+// float64 vertices. Each render call runs, on its own stream, three build
 // launches before its render kernels (round 4; round 3 took ten):
 //   k_frame_build1   blocks [0, face_blocks): per face (kFaceLanes threads)
 //                    its pixel rectangle and, for a face of <= kBigFace
@@ -18,18 +18,19 @@
 //                    fixed block of 2^slot_lg slots — no count / scan / fill
 //                    passes. Larger faces go onto the huge list.
 //                    the other blocks: per 64 x 4 tile of the launch, the
-//                    shadow skips its pixels share (one test for the tile) and
-//                    the tile's look-back status word zeroed; block 0 also
-//                    zeroes the render kernels' queue heads + Stats words.
-//   k_frame_build2   persistent blocks over the launch's tiles in order: per
-//                    pixel its huge faces (the tile's share of the huge list,
-//                    a SAT test each, appended after the small faces), its
-//                    record (list length + skip bits: the tile's, or the
-//                    pixel's own test), its counter zeroed for the next call;
-//                    then the lean / general lists in tile order by a
-//                    single-pass decoupled look-back over the tiles (one 8-byte
-//                    status granule per tile, agent-scope sc1 stores / polls:
-//                    no global atomic counter, no scan launch).
+//                    shadow skips its pixels share (one test for the tile);
+//                    block 0 also zeroes the render kernels' queue heads +
+//                    Stats words.
+//   k_frame_build2   one block per tile: per pixel its huge faces (the tile's
+//                    share of the huge list, a SAT test each, appended after
+//                    the small faces), its record (list length + skip bits:
+//                    the tile's, or the pixel's own test), its counter zeroed
+//                    for the next call; with a split, the tile's lean /
+//                    general counts.
+//   k_frame_lists    (two-class launches) one block per 16 tiles: its offsets
+//                    summed by the block itself from every earlier tile's
+//                    counts (no inter-block hand-off, no scan launch), its
+//                    pixels written to the lean / general lists in tile order.
 // A pixel with more listed faces than its 2^slot_lg slots keeps its true
 // count in the record; the render kernels then traverse the BVH for that
 // pixel's camera rays (the same answers, rt_fast.h mesh_search) — exact, no
@@ -82,8 +83,9 @@ struct DevBinTri {
 // frame counters (one small device array). FC_HUGE0 / FC_HUGE1: the huge-face
 // list's length of calls of even / odd parity (k_frame_build1 appends to its
 // call's word and zeroes the other one, which the next call uses).
-// FC_OVERFLOW: kept for a build that could not complete (a look-back that
-// timed out); reported by the host (rtmi.cpp report_overflow).
+// FC_OVERFLOW: reserved for a build that could not complete (none can now:
+// a list past its slots takes the BVH); reported by the host
+// (rtmi.cpp report_overflow).
 enum : int32_t { FC_OVERFLOW = 0, FC_HEAVY = 1, FC_LEAN = 2, FC_HUGE0 = 3, FC_HUGE1 = 4, FC_WORDS = 8 };
 
 // Faces whose pixel rectangle holds more than kBigFace pixels are not walked
@@ -148,7 +150,7 @@ struct FrameLaunch {
   // tiles / records / lists (k_frame_build1 tile blocks, k_frame_build2)
   RecordsLaunch r;
   uint8_t* tile_bits;       // per tile: 1 = every light skipped for the whole tile
-  unsigned long long* status;  // per tile: the look-back granule
+  unsigned long long* tile_cls;  // per tile: lean << 32 | general pixel counts (split)
   int32_t tiles_x, ntiles;
   unsigned int* zero;       // words k_frame_build1 zeroes (queue heads + Stats), or nullptr
   int32_t nzero;
@@ -174,10 +176,9 @@ constexpr int kObjRectInts = 4 * 64 + 2;
 }  // namespace rtmi
 
 extern "C" {
-// The call's two build launches (k_frame_build1, k_frame_build2) on `stream`;
-// build2_blocks: the persistent grid of k_frame_build2 (<= the launch's
-// tiles, far below what stays resident).
-int rtmi_frame_build(const rtmi::FrameLaunch* a, int build2_blocks, void* stream);
+// The call's build launches (k_frame_build1, k_frame_build2 and, with a
+// split, k_frame_lists) on `stream`.
+int rtmi_frame_build(const rtmi::FrameLaunch* a, void* stream);
 long long rtmi_frame_tile_bytes(int ncols, int nrows);
 int rtmi_frame_obj_masks(const rtmi::ObjMaskLaunch* a, void* stream);
 }

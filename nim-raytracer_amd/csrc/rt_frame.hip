@@ -142,7 +142,7 @@ __device__ __forceinline__ void faces_body(const FrameLaunch& a, const int t) {
 }
 
 // blocks [0, face_blocks): faces; the rest: one tile per thread (its skip
-// bits; its look-back status zeroed for k_frame_build2). Block 0 also clears
+// bits). Block 0 also clears
 // the next call's huge-list counter and the render kernels' queue heads +
 // Stats words (one launch fewer than a memset).
 __global__ __launch_bounds__(256) void k_frame_build1(const FrameLaunch a, int face_blocks) {
@@ -156,7 +156,6 @@ __global__ __launch_bounds__(256) void k_frame_build1(const FrameLaunch a, int f
     return;
   }
   const int t = (int)((blockIdx.x - (unsigned)face_blocks) * 256u + threadIdx.x);
-  if (t < a.ntiles) a.status[t] = 0ull;
   if (a.r.records && a.r.have != 0u) {
     load_skip_grids(a.r, sg);
     tiles_body(a.r, t, a.tiles_x, a.ntiles, a.tile_bits, sg);
@@ -165,32 +164,8 @@ __global__ __launch_bounds__(256) void k_frame_build1(const FrameLaunch a, int f
 
 // ---- k_frame_build2: huge faces, records, counters, lean / general lists --
 
-// The lean / general lists in tile order, single pass: tiles are taken in
-// chunks of kChunkTiles consecutive tiles (one block per chunk, persistent
-// over chunks b, b + G, ...); a chunk's class counts are published as an
-// 8-byte granule {state, lean count, general count} (state AGG: this chunk
-// only, INCL: every chunk up to it), and the chunk finds its offset by
-// summing its predecessors' granules back to the nearest INCL one
-// (decoupled look-back; 256 predecessors per step, one per thread). Granules
-// are written by ONE sc1 (agent-scope) store and polled by sc1 loads — the
-// data is the flag (MI355X_MICROARCH.md, inter-workgroup visibility; R2 of
-// cdna_hip_programming.md Guideline 16) — and zeroed by k_frame_build1.
-// A chunk waits only on chunks before it; every block of the grid stays
-// resident (rtmi_frame_build sizes it far below residency) and takes its
-// chunks in increasing order, so the earliest unfinished chunk always
-// progresses. Spins are bounded: a look-back that times out (never seen)
-// sets FC_OVERFLOW, which fails the call on the host, and uses what it has
-// (list slots stay inside the lists; no out-of-range entry is written).
+// Tiles per block of k_frame_lists.
 constexpr int kChunkTiles = 16;
-constexpr unsigned long long kStAgg = 1ull << 62, kStIncl = 2ull << 62, kStVal = (1ull << 62) - 1ull;
-constexpr unsigned long long kLeanOne = 1ull << 31;  // a granule's counts: lean << 31 | general
-using gu64 = __attribute__((address_space(1))) unsigned long long;
-__device__ __forceinline__ unsigned long long granule_load(unsigned long long* p) {
-  return __hip_atomic_load((gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void granule_store(unsigned long long* p, unsigned long long v) {
-  __hip_atomic_store((gu64*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 
 // The class of a launch pixel: 1 lean (empty list, every light skipped), 2
 // general, 0 not drawn (a progressive pass skips it).
@@ -260,119 +235,87 @@ __device__ __forceinline__ int build2_tile(const FrameLaunch& a, int t, int nhug
 // k_frame_build2: one tile per block, all of them at once (a pixel's own
 // skip test is a long float64 chain: tiles taken in turn by a persistent
 // grid serialised those chains, 90 us per C3 call).
+// With split, the tile's lean / general pixel counts (lean << 32 | general)
+// go to tile_cls for k_frame_lists.
 __global__ __launch_bounds__(256) void k_frame_build2(const FrameLaunch a) {
   __shared__ bg::SkipGrid sg[8];
   __shared__ int32_t hl[256];
   __shared__ int hn;
+  __shared__ unsigned long long wsum[4];
   const RecordsLaunch& r = a.r;
   if (r.records && r.have != 0u) load_skip_grids(r, sg);
   const int nhuge = min(r.ctr[FC_HUGE0 + a.parity], kHugeCap);
-  (void)build2_tile(a, (int)blockIdx.x, nhuge, sg, hl, &hn);
+  const int cl = build2_tile(a, (int)blockIdx.x, nhuge, sg, hl, &hn);
+  if (!r.split) return;
+  const unsigned long long ml = __ballot(cl == 1), mh = __ballot(cl == 2);
+  if ((threadIdx.x & 63u) == 0) wsum[threadIdx.x >> 6] = ((unsigned long long)__popcll(ml) << 32) | __popcll(mh);
+  __syncthreads();
+  if (threadIdx.x == 0) a.tile_cls[blockIdx.x] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
 }
 
-// k_frame_lists: the lean / general lists (two-class launches), persistent
-// blocks over chunks of kChunkTiles tiles in order: each thread loads its
-// pixel's record in each of the chunk's tiles (all loads in flight), the
-// per-tile class counts go through LDS, the chunk's granule is published and
-// its predecessors' summed (look-back), and the chunk's pixels are written at
-// their offsets.
+// k_frame_lists: the lean / general lists (two-class launches) in tile
+// order. One block per chunk of kChunkTiles tiles: its offsets are the sum of
+// every earlier tile's counts (k_frame_build2's tile_cls), summed by the
+// block itself — each block re-reads the earlier counts (8,100 x 8 B at
+// 1080p, L2-resident) instead of waiting on other blocks: no inter-block
+// hand-off, no spin, no scan launch. Then each thread loads its pixel's
+// record in each of the chunk's tiles (all loads in flight), and the chunk's
+// pixels are written at their offsets (wave ballots, mbcnt ranks).
 __global__ __launch_bounds__(256) void k_frame_lists(const FrameLaunch a) {
-  __shared__ unsigned long long wpart[4];          // per-wave partial counts
+  __shared__ unsigned long long wpart[4];
   __shared__ unsigned long long wsum[kChunkTiles][4];
-  __shared__ int first_s, bad_s;
   const RecordsLaunch& r = a.r;
   const int tid = (int)threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int nchunks = (a.ntiles + kChunkTiles - 1) / kChunkTiles;
-  for (int c = (int)blockIdx.x; c < nchunks; c += (int)gridDim.x) {
-    const int t0 = c * kChunkTiles;
-    uint32_t inf[kChunkTiles];
-    LaunchPix px[kChunkTiles];
+  const int t0 = (int)blockIdx.x * kChunkTiles;
+  uint32_t inf[kChunkTiles];
+  LaunchPix px[kChunkTiles];
 #pragma unroll
-    for (int i = 0; i < kChunkTiles; ++i) {
-      const int t = t0 + i;
-      const int bx = t % a.tiles_x, by = t / a.tiles_x;
-      px[i] = launch_pixel(r, bx * kTileW + lane, by * kTileH + w);
-      px[i].valid = px[i].valid && t < a.ntiles;
-      inf[i] = px[i].valid ? r.info[(size_t)px[i].y * r.width + px[i].x] : 0u;
-    }
-    int cls[kChunkTiles];
-    unsigned long long agg = 0ull;
+  for (int i = 0; i < kChunkTiles; ++i) {
+    const int t = t0 + i;
+    const int bx = t % a.tiles_x, by = t / a.tiles_x;
+    px[i] = launch_pixel(r, bx * kTileW + lane, by * kTileH + w);
+    px[i].valid = px[i].valid && t < a.ntiles;
+    inf[i] = px[i].valid ? r.info[(size_t)px[i].y * r.width + px[i].x] : 0u;
+  }
+  // every earlier tile's counts (lean << 32 | general)
+  unsigned long long v = 0ull;
+  for (int t = tid; t < t0; t += 256) v += a.tile_cls[t];
 #pragma unroll
-    for (int i = 0; i < kChunkTiles; ++i) {
-      cls[i] = px[i].valid ? pixel_class(r, px[i], inf[i]) : 0;
-      const unsigned long long ml = __ballot(cls[i] == 1), mh = __ballot(cls[i] == 2);
-      if (lane == 0) wsum[i][w] = (unsigned long long)__popcll(ml) * kLeanOne + (unsigned long long)__popcll(mh);
-    }
-    __syncthreads();
+  for (int off = 32; off >= 1; off >>= 1) {
+    const unsigned lo = (unsigned)__shfl_xor((int)(unsigned)v, off);
+    const unsigned hi = (unsigned)__shfl_xor((int)(unsigned)(v >> 32), off);
+    v += ((unsigned long long)hi << 32) | lo;
+  }
+  if (lane == 0) wpart[w] = v;
+  int cls[kChunkTiles];
 #pragma unroll
-    for (int i = 0; i < kChunkTiles; ++i) agg += wsum[i][0] + wsum[i][1] + wsum[i][2] + wsum[i][3];
-    // publish, then look back (every thread one predecessor per step)
-    if (tid == 0) granule_store(&a.status[c], (c == 0 ? kStIncl : kStAgg) | agg);
-    unsigned long long excl = 0ull;
-    if (c > 0) {
-      int jj = c - 1;
-      for (int spins = 0;; ++spins) {
-        const int idx = jj - tid;
-        const unsigned long long g = idx >= 0 ? granule_load(&a.status[idx]) : kStIncl;  // before chunk 0: INCL 0
-        const unsigned long long st = g & ~kStVal;
-        const unsigned long long mi = __ballot(st == kStIncl), mz = __ballot(st == 0ull);
-        if (tid == 0) {
-          first_s = 1 << 30;
-          bad_s = 0;
-        }
-        __syncthreads();
-        if (lane == 0 && mi != 0ull) atomicMin(&first_s, w * 64 + (int)__builtin_ctzll(mi));
-        __syncthreads();
-        const int first = first_s;  // the nearest INCL predecessor's thread (>= 256: none in this window)
-        if (lane == 0 && mz != 0ull && w * 64 + (int)__builtin_ctzll(mz) <= first) bad_s = 1;
-        __syncthreads();
-        const bool bad = bad_s != 0, timeout = spins >= (1 << 20);
-        if (bad && !timeout) {  // a needed predecessor has not published yet
-          __syncthreads();
-          __builtin_amdgcn_s_sleep(2);
-          continue;
-        }
-        if (bad && tid == 0) atomicOr(&r.ctr[FC_OVERFLOW], 2);
-        unsigned long long v = tid <= first ? (g & kStVal) : 0ull;
+  for (int i = 0; i < kChunkTiles; ++i) {
+    cls[i] = px[i].valid ? pixel_class(r, px[i], inf[i]) : 0;
+    const unsigned long long ml = __ballot(cls[i] == 1), mh = __ballot(cls[i] == 2);
+    if (lane == 0) wsum[i][w] = ((unsigned long long)__popcll(ml) << 32) | __popcll(mh);
+  }
+  __syncthreads();
+  unsigned long long base = wpart[0] + wpart[1] + wpart[2] + wpart[3];
 #pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) {
-          const unsigned lo = (unsigned)__shfl_xor((int)(unsigned)v, off);
-          const unsigned hi = (unsigned)__shfl_xor((int)(unsigned)(v >> 32), off);
-          v += ((unsigned long long)hi << 32) | lo;
-        }
-        if (lane == 0) wpart[w] = v;
-        __syncthreads();
-        excl += wpart[0] + wpart[1] + wpart[2] + wpart[3];
-        __syncthreads();
-        if (first < 256 || bad) break;
-        jj -= 256;
-      }
-      if (tid == 0) granule_store(&a.status[c], kStIncl | (excl + agg));
+  for (int i = 0; i < kChunkTiles; ++i) {
+    const int t = t0 + i;
+    const unsigned long long ml = __ballot(cls[i] == 1), mh = __ballot(cls[i] == 2);
+    unsigned long long b = base;
+    for (int q = 0; q < w; ++q) b += wsum[i][q];
+    const int bx = t % a.tiles_x, by = t / a.tiles_x;
+    const int g = (by * kTileH + w) * r.ncols + bx * kTileW + lane;
+    if (cls[i] == 1) r.lean[(int)(b >> 32) + (int)lane_rank(ml)] = g;
+    if (cls[i] == 2) r.heavy[(int)(b & 0xffffffffull) + (int)lane_rank(mh)] = g;
+    base += wsum[i][0] + wsum[i][1] + wsum[i][2] + wsum[i][3];
+  }
+  if ((int)blockIdx.x == (int)gridDim.x - 1) {  // the last chunk: the list lengths, the lean list's -1 padding
+    const int nl = (int)(base >> 32), nh = (int)(base & 0xffffffffull);
+    if (tid == 0) {
+      r.ctr[FC_LEAN] = nl;
+      r.ctr[FC_HEAVY] = nh;
     }
-    // the chunk's pixels into the lists at their offsets (wave ballots, mbcnt ranks)
-    unsigned long long base = excl;
-#pragma unroll
-    for (int i = 0; i < kChunkTiles; ++i) {
-      const int t = t0 + i;
-      const unsigned long long ml = __ballot(cls[i] == 1), mh = __ballot(cls[i] == 2);
-      unsigned long long b = base;
-      for (int q = 0; q < w; ++q) b += wsum[i][q];
-      const int bx = t % a.tiles_x, by = t / a.tiles_x;
-      const int g = (by * kTileH + w) * r.ncols + bx * kTileW + lane;
-      if (cls[i] == 1) r.lean[(int)(b >> 31) + (int)lane_rank(ml)] = g;
-      if (cls[i] == 2) r.heavy[(int)(b & (kLeanOne - 1ull)) + (int)lane_rank(mh)] = g;
-      base += wsum[i][0] + wsum[i][1] + wsum[i][2] + wsum[i][3];
-    }
-    if (c == nchunks - 1) {  // the last chunk: the list lengths, the lean list's -1 padding
-      const int nl = (int)(base >> 31), nh = (int)(base & (kLeanOne - 1ull));
-      if (tid == 0) {
-        r.ctr[FC_LEAN] = nl;
-        r.ctr[FC_HEAVY] = nh;
-      }
-      const int end = nl == 0 ? 64 : (nl + 63) / 64 * 64;
-      for (int e = nl + tid; e < end; e += 256) r.lean[e] = -1;
-    }
-    __syncthreads();  // wsum reused by the next chunk
+    const int end = nl == 0 ? 64 : (nl + 63) / 64 * 64;
+    for (int e = nl + tid; e < end; e += 256) r.lean[e] = -1;
   }
 }
 
@@ -454,7 +397,7 @@ __global__ __launch_bounds__(256) void k_frame_obj_masks(const ObjMaskLaunch a) 
 }  // namespace
 }  // namespace rtmi
 
-extern "C" int rtmi_frame_build(const rtmi::FrameLaunch* a, int build2_blocks, void* stream) {
+extern "C" int rtmi_frame_build(const rtmi::FrameLaunch* a, void* stream) {
   using namespace rtmi;
   static_assert(sizeof(FrameLaunch) <= 4096, "kernel argument size");
   hipStream_t st = (hipStream_t)stream;
@@ -466,8 +409,7 @@ extern "C" int rtmi_frame_build(const rtmi::FrameLaunch* a, int build2_blocks, v
   hipLaunchKernelGGL(k_frame_build2, dim3((unsigned)a->ntiles), dim3(256), 0, st, *a);
   if ((e = hipGetLastError()) != hipSuccess || !a->r.split) return (int)e;
   const int nchunks = (a->ntiles + kChunkTiles - 1) / kChunkTiles;
-  hipLaunchKernelGGL(k_frame_lists, dim3((unsigned)std::max(1, std::min(build2_blocks, nchunks))), dim3(256), 0, st,
-                     *a);
+  hipLaunchKernelGGL(k_frame_lists, dim3((unsigned)nchunks), dim3(256), 0, st, *a);
   return (int)hipGetLastError();
 }
 

@@ -225,7 +225,7 @@ struct rt_scene {
     int w = 0, h = 0;
     DevBuf<int32_t> cnt, slots, lean, heavy, ctr, orect;
     DevBuf<uint32_t> info;
-    DevBuf<unsigned long long> omask, status;
+    DevBuf<unsigned long long> omask, status;  // status: per-tile class counts (FrameLaunch.tile_cls)
     DevBuf<HugeFace> huge;
     DevBuf<unsigned char> tiles;   // per-tile shadow skips (k_frame_build1)
     int slot_lg = -1;              // slots allocated for 2^slot_lg entries per pixel (-1: none)
@@ -1378,14 +1378,12 @@ int frame_build(rt_scene* s, const rt_options* o, const Mapping& mp, const FastP
   a.parity = (int32_t)(f.calls++ & 1u);
   records_launch(s, o, mp, p, records, split, a.r);
   a.tile_bits = f.tiles.p;
-  a.status = f.status.p;
+  a.tile_cls = f.status.p;
   a.tiles_x = (mp.ncols + 63) / 64;
   a.ntiles = a.tiles_x * ((mp.nrows + 3) / 4);
   a.zero = zero;
   a.nzero = nzero;
-  // k_frame_build2's persistent grid: two blocks per CU, far below what
-  // stays resident (its look-back waits on earlier chunks only)
-  if ((rc = rtmi_frame_build(&a, 2 * s->num_cus, st))) {
+  if ((rc = rtmi_frame_build(&a, st))) {
     // the first launch may have run (its counters non-zero, zeroed only by
     // the second): the next call re-allocates and re-zeroes the buffers
     f.invalidate();
