@@ -68,8 +68,9 @@ struct PixCam {
   double margin;            // rt_bins.h kPixelMargin
   int width, height;
 };
-__host__ __device__ inline bool face_pixel_rect(const PixCam& c, const double v[3][3], double q[6], int rect[4]) {
-  rect[0] = rect[1] = rect[2] = rect[3] = -1;
+// The single-sided cull of a face for every camera ray (geom.nim:306): true
+// when no camera ray reaching the face's plane can pass det >= 1e-6.
+__host__ __device__ inline bool face_is_back(const PixCam& c, const double v[3][3]) {
   double e1[3], e2[3], cr[3], nn[3], dc[3];
   for (int k = 0; k < 3; ++k) {
     e1[k] = v[1][k] - v[0][k];
@@ -86,7 +87,12 @@ __host__ __device__ inline bool face_pixel_rect(const PixCam& c, const double v[
     const double dv[3] = {v[a][0] - c.co[0], v[a][1] - c.co[1], v[a][2] - c.co[2]};
     maxd = dmax(maxd, norm3(dv));
   }
-  if (s <= 0.0 && maxd > 0.0 && never_passes(c.rd_min * s / maxd, c.rd_max, nlen)) return true;  // back face
+  return s <= 0.0 && maxd > 0.0 && never_passes(c.rd_min * s / maxd, c.rd_max, nlen);
+}
+// The face's projected vertices and grown pixel rectangle (rect[0] = -1:
+// off screen); false when a vertex lies at or behind the camera plane.
+__host__ __device__ inline bool face_project_rect(const PixCam& c, const double v[3][3], double q[6], int rect[4]) {
+  rect[0] = rect[1] = rect[2] = rect[3] = -1;
   double xmin = INFINITY, xmax = -INFINITY, ymin = INFINITY, ymax = -INFINITY;
   for (int a = 0; a < 3; ++a) {
     double pw[3], pc[3];
@@ -109,6 +115,13 @@ __host__ __device__ inline bool face_pixel_rect(const PixCam& c, const double v[
   rect[2] = (int)dmax(0.0, floor(ymin - m));
   rect[3] = (int)dmin((double)c.height - 1, floor(ymax + m));
   return true;
+}
+__host__ __device__ inline bool face_pixel_rect(const PixCam& c, const double v[3][3], double q[6], int rect[4]) {
+  if (face_is_back(c, v)) {  // a back face: in no pixel's list
+    rect[0] = rect[1] = rect[2] = rect[3] = -1;
+    return true;
+  }
+  return face_project_rect(c, v, q, rect);
 }
 
 // Shadow skips (build_shadow_skips) of one pixel whose camera-ray list is

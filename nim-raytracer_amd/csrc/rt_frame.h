@@ -10,9 +10,11 @@
 // the BVH, the light grids and their occupancy prefix sums, the faces'
 // float64 vertices. Each render call runs, on its own stream, three build
 // launches before its render kernels (round 4; round 3 took ten):
-//   k_frame_build1   blocks [0, face_blocks): per face (kFaceLanes threads)
-//                    its pixel rectangle and, for a face of <= kBigFace
-//                    pixels, a SAT test per pixel of the launch; a listed
+//   k_frame_build1   blocks [0, face_blocks): per face (one thread) its
+//                    pixel rectangle, a launch-row test and the cull, then
+//                    the block's (face, pixel) pairs dealt out over its
+//                    threads: for a face of <= kBigFace pixels a SAT test
+//                    per pixel of the launch; a listed
 //                    pixel's counter hands out its slot (atomicAdd) and the
 //                    face's record offset goes straight into the pixel's
 //                    fixed block of 2^slot_lg slots — no count / scan / fill
@@ -62,6 +64,22 @@ __host__ __device__ inline bool frame_has_row(const FrameRows& r, int y) {
   }
   return (y / r.band_h) % r.world == r.rank;
 }
+// some launch row in [ylo, yhi] (ylo <= yhi)
+__host__ __device__ inline bool frame_meets_rows(const FrameRows& r, int ylo, int yhi) {
+  ylo = ylo < 0 ? 0 : ylo;
+  yhi = yhi < r.height - 1 ? yhi : r.height - 1;
+  if (ylo > yhi) return false;
+  if (r.mode == 0) {
+    const int last = r.y0 + (r.nrows - 1) * r.step;
+    if (r.nrows <= 0 || yhi < r.y0 || ylo > last) return false;
+    const int d = ylo > r.y0 ? ylo - r.y0 : 0;
+    const int first = r.y0 + (d + r.step - 1) / r.step * r.step;  // first launch row >= ylo
+    return first <= yhi && first <= last;
+  }
+  const int b0 = ylo / r.band_h, b1 = yhi / r.band_h;
+  const int b = b0 + ((r.rank - b0 % r.world) % r.world + r.world) % r.world;  // first own band >= b0
+  return b <= b1;
+}
 // a column of the launch (its pixels: launch rows x launch columns)
 __host__ __device__ inline bool frame_has_col(const FrameRows& r, int x) {
   return r.mode != 0 || x % r.step == 0;
@@ -89,12 +107,12 @@ struct DevBinTri {
 enum : int32_t { FC_OVERFLOW = 0, FC_HEAVY = 1, FC_LEAN = 2, FC_HUGE0 = 3, FC_HUGE1 = 4, FC_WORDS = 8 };
 
 // Faces whose pixel rectangle holds more than kBigFace pixels are not walked
-// by their own kFaceLanes threads (a few large faces, e.g. a 576-face torus
-// filling a quarter of a 1080p frame, left a handful of threads looping over
+// by k_frame_build1's blocks (a few large faces, e.g. a 576-face torus
+// filling a quarter of a 1080p frame, left a handful of blocks looping over
 // thousands of pixels each: 3 ms per call); they go to the huge list, whose
 // faces k_frame_build2 tests per tile (each tile culls the list against its
 // pixel rectangle, then each pixel tests the tile's share). Past kHugeCap
-// faces the rest are walked by their own threads (slow, exact).
+// faces the rest are walked by their blocks (slow, exact).
 #ifndef RTMI_BIG_FACE
 #define RTMI_BIG_FACE 64
 #endif

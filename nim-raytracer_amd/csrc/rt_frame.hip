@@ -85,58 +85,93 @@ __device__ __forceinline__ void tiles_body(const RecordsLaunch& a, const int t, 
 
 // ---- k_frame_build1: faces (slot appends, huge list) + tiles -------------
 
-// kFaceLanes threads per face: each takes every kFaceLanes-th pixel of the
-// face's rectangle (a face covers a few pixels; one thread per face left the
-// GPU a quarter of a wave per SIMD — latency-bound at 69 k faces).
-constexpr int kFaceLanes = 4;
+// kFacesPerBlock faces per block, one per thread for the projection (each
+// face's rectangle, cull and row tests run once), then the block's
+// (face, rectangle pixel) pairs are dealt out evenly over its threads (a
+// face covers a few pixels, a few cover dozens: a face per thread for the
+// pixel loop left most lanes idle behind the largest face of their wave).
+constexpr int kFacesPerBlock = 256;
 
 // Per face: its pixel rectangle (rt_bins.cpp build_pixel_bins, the same
 // bounds); every launch pixel its grown projection meets gets the face's
 // record offset in its next slot (the pixel's counter hands slots out). A
-// face of more than kBigFace pixels goes onto the huge list instead (its
-// first thread takes the entry; the face's kFaceLanes threads are adjacent
-// lanes of one wave).
-__device__ __forceinline__ void faces_body(const FrameLaunch& a, const int t) {
-  const int i = t / kFaceLanes, q = t % kFaceLanes;
-  if (i >= a.nf) return;
-  double v[3][3];
+// face of more than kBigFace pixels goes onto the huge list instead. The
+// projection comes before the cull: a face with no launch row in its
+// rectangle (a band launch of a multi-GPU frame) is dropped without the
+// cull's square roots — it lists no launch pixel either way.
+__device__ __forceinline__ void faces_block(const FrameLaunch& a) {
+  __shared__ double s_pr[kFacesPerBlock][6];
+  __shared__ int s_pre[kFacesPerBlock + 1], s_x0[kFacesPerBlock], s_y0[kFacesPerBlock], s_rw[kFacesPerBlock];
+  __shared__ int32_t s_rec[kFacesPerBlock];
+  const int tid = (int)threadIdx.x, i = (int)blockIdx.x * kFacesPerBlock + tid;
+  int area = 0;
+  if (i < a.nf) {
+    double v[3][3];
 #pragma unroll
-  for (int p = 0; p < 3; ++p)
+    for (int p = 0; p < 3; ++p)
 #pragma unroll
-    for (int k = 0; k < 3; ++k) v[p][k] = a.tris[i].v[p][k];
-  double pr[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
-  int r[4];
-  // (a vertex at or behind the camera plane: the host checked the mesh box
-  // against the camera plane before launching, so this never fails)
-  if (!bg::face_pixel_rect(a.cam, v, pr, r)) r[0] = -1;
-  if (r[0] < 0) return;  // back face / off screen: in no pixel's list
-  const int rw = r[1] - r[0] + 1, area = rw * (r[3] - r[2] + 1);
-  const int32_t rec = a.tris[i].rec;
-  if (area > kBigFace) {
-    int slot = kHugeCap;
-    if (q == 0) slot = atomicAdd(&a.r.ctr[FC_HUGE0 + a.parity], 1);
-    slot = __shfl(slot, (int)(threadIdx.x & 63u) - q);
-    if (slot < kHugeCap) {
-      if (q == 0) {
-        HugeFace& h = a.huge[slot];
-        h.rec = rec;
+      for (int k = 0; k < 3; ++k) v[p][k] = a.tris[i].v[p][k];
+    double pr[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+    int r[4];
+    // (a vertex at or behind the camera plane: the host checked the mesh box
+    // against the camera plane before launching, so this never fails)
+    if (bg::face_project_rect(a.cam, v, pr, r) && r[0] >= 0 && frame_meets_rows(a.rows, r[2], r[3]) &&
+        !bg::face_is_back(a.cam, v)) {
+      const int rw = r[1] - r[0] + 1;
+      area = rw * (r[3] - r[2] + 1);
+      const int32_t rec = a.tris[i].rec;
+      if (area > kBigFace) {
+        const int slot = atomicAdd(&a.r.ctr[FC_HUGE0 + a.parity], 1);
+        if (slot < kHugeCap) {
+          HugeFace& h = a.huge[slot];
+          h.rec = rec;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) h.r[k] = r[k];
+          for (int k = 0; k < 4; ++k) h.r[k] = r[k];
 #pragma unroll
-        for (int k = 0; k < 6; ++k) h.pr[k] = pr[k];
+          for (int k = 0; k < 6; ++k) h.pr[k] = pr[k];
+          area = 0;
+        }
+        // the list is full: the block's threads walk this face (slow, exact)
       }
-      return;
+      if (area > 0) {
+#pragma unroll
+        for (int k = 0; k < 6; ++k) s_pr[tid][k] = pr[k];
+        s_x0[tid] = r[0];
+        s_y0[tid] = r[2];
+        s_rw[tid] = rw;
+        s_rec[tid] = rec;
+      }
     }
-    // the list is full: this face's own threads walk it (slow, exact)
   }
+  // exclusive prefix of the areas (Hillis-Steele over the block)
+  s_pre[tid + 1] = area;
+  if (tid == 0) s_pre[0] = 0;
+  __syncthreads();
+  for (int d = 1; d < kFacesPerBlock; d <<= 1) {
+    const int add = tid + 1 > d ? s_pre[tid + 1 - d] : 0;
+    __syncthreads();
+    s_pre[tid + 1] += add;
+    __syncthreads();
+  }
+  const int total = s_pre[kFacesPerBlock];
   const double m = a.cam.margin;
-  for (int idx = q; idx < area; idx += kFaceLanes) {
-    const int y = r[2] + idx / rw, x = r[0] + idx % rw;
-    if (frame_has_row(a.rows, y) && frame_has_col(a.rows, x) &&
-        bg::tri_meets_box(pr, x - m, y - m, x + 1 + m, y + 1 + m)) {
+  for (int idx = tid; idx < total; idx += kFacesPerBlock) {
+    int lo = 0, hi = kFacesPerBlock - 1;  // the last face whose range starts at or before idx
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (s_pre[mid] <= idx) lo = mid;
+      else hi = mid - 1;
+    }
+    const int local = idx - s_pre[lo], rw = s_rw[lo];
+    const int y = s_y0[lo] + local / rw, x = s_x0[lo] + local % rw;
+    if (!frame_has_row(a.rows, y) || !frame_has_col(a.rows, x)) continue;
+    double pr[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) pr[k] = s_pr[lo][k];
+    if (bg::tri_meets_box(pr, x - m, y - m, x + 1 + m, y + 1 + m)) {
       const size_t pix = (size_t)y * a.cam.width + x;
       const int s = atomicAdd(&a.cnt[pix], 1);
-      if (s < (1 << a.slot_lg)) a.slots[(pix << a.slot_lg) + s] = rec;
+      if (s < (1 << a.slot_lg)) a.slots[(pix << a.slot_lg) + s] = s_rec[lo];
     }
   }
 }
@@ -152,7 +187,7 @@ __global__ __launch_bounds__(256) void k_frame_build1(const FrameLaunch a, int f
     if (threadIdx.x == 0) a.r.ctr[FC_HUGE0 + (a.parity ^ 1)] = 0;
   }
   if ((int)blockIdx.x < face_blocks) {
-    faces_body(a, (int)(blockIdx.x * 256u + threadIdx.x));
+    faces_block(a);
     return;
   }
   const int t = (int)((blockIdx.x - (unsigned)face_blocks) * 256u + threadIdx.x);
@@ -401,7 +436,7 @@ extern "C" int rtmi_frame_build(const rtmi::FrameLaunch* a, void* stream) {
   using namespace rtmi;
   static_assert(sizeof(FrameLaunch) <= 4096, "kernel argument size");
   hipStream_t st = (hipStream_t)stream;
-  const int face_blocks = std::max(1, (int)(((long long)a->nf * kFaceLanes + 255) / 256));
+  const int face_blocks = std::max(1, (a->nf + kFacesPerBlock - 1) / kFacesPerBlock);
   const int tile_blocks = (a->ntiles + 255) / 256;
   hipLaunchKernelGGL(k_frame_build1, dim3(face_blocks + tile_blocks), dim3(256), 0, st, *a, face_blocks);
   hipError_t e = hipGetLastError();
