@@ -85,12 +85,13 @@ __device__ __forceinline__ void tiles_body(const RecordsLaunch& a, const int t, 
 
 // ---- k_frame_build1: faces (slot appends, huge list) + tiles -------------
 
-// kFacesPerBlock faces per block, one per thread for the projection (each
-// face's rectangle, cull and row tests run once), then the block's
-// (face, rectangle pixel) pairs are dealt out evenly over its threads (a
-// face covers a few pixels, a few cover dozens: a face per thread for the
-// pixel loop left most lanes idle behind the largest face of their wave).
-constexpr int kFacesPerBlock = 256;
+// kFacesPerBlock faces per block, one per thread of its first wave for the
+// projection (each face's rectangle, cull and row tests run once), then the
+// block's (face, rectangle pixel) pairs are dealt out evenly over all its
+// threads (a face covers a few pixels, a few cover dozens: a face per thread
+// for the pixel loop left most lanes idle behind the largest face of their
+// wave; 256 faces per block left one wave per SIMD for the pixel loop).
+constexpr int kFacesPerBlock = 64;
 
 // Per face: its pixel rectangle (rt_bins.cpp build_pixel_bins, the same
 // bounds); every launch pixel its grown projection meets gets the face's
@@ -105,7 +106,7 @@ __device__ __forceinline__ void faces_block(const FrameLaunch& a) {
   __shared__ int32_t s_rec[kFacesPerBlock];
   const int tid = (int)threadIdx.x, i = (int)blockIdx.x * kFacesPerBlock + tid;
   int area = 0;
-  if (i < a.nf) {
+  if (tid < kFacesPerBlock && i < a.nf) {
     double v[3][3];
 #pragma unroll
     for (int p = 0; p < 3; ++p)
@@ -144,18 +145,18 @@ __device__ __forceinline__ void faces_block(const FrameLaunch& a) {
     }
   }
   // exclusive prefix of the areas (Hillis-Steele over the block)
-  s_pre[tid + 1] = area;
+  if (tid < kFacesPerBlock) s_pre[tid + 1] = area;
   if (tid == 0) s_pre[0] = 0;
   __syncthreads();
   for (int d = 1; d < kFacesPerBlock; d <<= 1) {
-    const int add = tid + 1 > d ? s_pre[tid + 1 - d] : 0;
+    const int add = tid < kFacesPerBlock && tid + 1 > d ? s_pre[tid + 1 - d] : 0;
     __syncthreads();
-    s_pre[tid + 1] += add;
+    if (tid < kFacesPerBlock) s_pre[tid + 1] += add;
     __syncthreads();
   }
   const int total = s_pre[kFacesPerBlock];
   const double m = a.cam.margin;
-  for (int idx = tid; idx < total; idx += kFacesPerBlock) {
+  for (int idx = tid; idx < total; idx += (int)blockDim.x) {
     int lo = 0, hi = kFacesPerBlock - 1;  // the last face whose range starts at or before idx
     while (lo < hi) {
       const int mid = (lo + hi + 1) >> 1;
