@@ -314,8 +314,17 @@ __global__ __launch_bounds__(256) void k_frame_lists(const FrameLaunch a) {
     inf[i] = px[i].valid ? r.info[(size_t)px[i].y * r.width + px[i].x] : 0u;
   }
   // every earlier tile's counts (lean << 32 | general)
+  // (kSumUnroll independent loads in flight per thread: a load-add chain of
+  // t0 / 256 steps was most of the kernel's time)
+  constexpr int kSumUnroll = 8;
   unsigned long long v = 0ull;
-  for (int t = tid; t < t0; t += 256) v += a.tile_cls[t];
+  for (int t = tid; t < t0; t += 256 * kSumUnroll) {
+    unsigned long long part[kSumUnroll];
+#pragma unroll
+    for (int u = 0; u < kSumUnroll; ++u) part[u] = t + u * 256 < t0 ? a.tile_cls[t + u * 256] : 0ull;
+#pragma unroll
+    for (int u = 0; u < kSumUnroll; ++u) v += part[u];
+  }
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) {
     const unsigned lo = (unsigned)__shfl_xor((int)(unsigned)v, off);

@@ -1787,7 +1787,10 @@ int launch(rt_scene* s, const rt_options* o, const Mapping& mp, float* d_out, hi
       // (a short launch, e.g. a multi-GPU rank's bands), then 4
       const long long lwaves4 =
           4LL * std::min<long long>((long long)rtmi_lean1_f32_blocks_per_cu(p.nlight, 4) * s->num_cus, s->max_waves / 4);
-      const int lp = !(lean1 && rtmi_lean1_quads()) ? 64 : ((long long)(p.ngroups + 15) / 16 >= 8 * lwaves4 ? 4 : 16);
+      static const int lp_env = std::getenv("RTMI_LEAN_LP") ? std::atoi(std::getenv("RTMI_LEAN_LP")) : 0;  // diagnostic: 4 / 16
+      const int lp = !(lean1 && rtmi_lean1_quads())
+                         ? 64
+                         : (lp_env == 4 || lp_env == 16 ? lp_env : ((long long)(p.ngroups + 15) / 16 >= 8 * lwaves4 ? 4 : 16));
       const long long lcap =
           (long long)(lean1 ? rtmi_lean1_f32_blocks_per_cu(p.nlight, lp) : rtmi_lean_f32_blocks_per_cu(sub, shmem)) *
           s->num_cus;
