@@ -167,7 +167,7 @@ struct FrameLaunch {
   int32_t parity;           // the call's FC_HUGE word: FC_HUGE0 + parity
   // tiles / records / lists (k_frame_build1 tile blocks, k_frame_build2)
   RecordsLaunch r;
-  uint8_t* tile_bits;       // per tile: 1 = every light skipped for the whole tile
+  uint8_t* tile_bits;       // per skip cell (kSkipCells per tile): 1 = every light skipped for the whole cell
   unsigned long long* tile_cls;  // per tile: lean << 32 | general pixel counts (split)
   int32_t tiles_x, ntiles;
   unsigned int* zero;       // words k_frame_build1 zeroes (queue heads + Stats), or nullptr
@@ -198,5 +198,6 @@ extern "C" {
 // split, k_frame_lists) on `stream`.
 int rtmi_frame_build(const rtmi::FrameLaunch* a, void* stream);
 long long rtmi_frame_tile_bytes(int ncols, int nrows);
+long long rtmi_frame_skip_cells(int ncols, int nrows);
 int rtmi_frame_obj_masks(const rtmi::ObjMaskLaunch* a, void* stream);
 }

@@ -58,19 +58,28 @@ __device__ __forceinline__ void load_skip_grids(const RecordsLaunch& a, bg::Skip
 }
 
 // Records are built per tile of kTileW launch columns x kTileH launch rows
-// (one block, one wave per launch row). The tile's shadow skips are tested
-// once for the rectangle its pixels span (rt_bins_geom.h rect_skip_bits:
-// the tile's grown corner rays bound every pixel's, so a tile whose bits
-// cover every light gives each of its pixels exactly the bits the per-pixel
-// test would); the pixels of other tiles take the per-pixel test.
-constexpr int kTileW = 64, kTileH = 4;
+// (one block, one wave per launch row). The shadow skips are tested once per
+// cell of kSkipW columns of a tile for the rectangle its pixels span
+// (rt_bins_geom.h rect_skip_bits: the cell's grown corner rays bound every
+// pixel's, so a cell whose bits cover every light gives each of its pixels
+// exactly the bits the per-pixel test would); the pixels of other cells take
+// the per-pixel test (a long float64 chain: a whole 64-column tile's test
+// failed wherever any of its pixels neared the object's shadow or a
+// horizon, and its 256 pixels then each ran the chain).
+constexpr int kTileW = 64, kTileH = 4, kSkipW = 16, kSkipCells = kTileW / kSkipW;
 
-// One thread per tile: the tile's skip bits (0 when not every light is skipped).
+// One thread per skip cell: its bits (1 = every light skipped).
 __device__ __forceinline__ void tiles_body(const RecordsLaunch& a, const int t, int tiles_x, int ntiles,
                                            uint8_t* tile_bits, const bg::SkipGrid* sg) {
-  if (t >= ntiles) return;
-  const int tj = t % tiles_x, tk = t / tiles_x;
-  const int j0 = tj * kTileW, j1 = min(j0 + kTileW, a.ncols) - 1;
+  if (t >= ntiles * kSkipCells) return;
+  const int tile = t / kSkipCells, c = t % kSkipCells;
+  const int tj = tile % tiles_x, tk = tile / tiles_x;
+  const int j0 = tj * kTileW + c * kSkipW;
+  if (j0 >= a.ncols) {
+    tile_bits[t] = 0;
+    return;
+  }
+  const int j1 = min(j0 + kSkipW, a.ncols) - 1;
   int ylo = 0x7fffffff, yhi = -1;
   for (int k = tk * kTileH; k < min(tk * kTileH + kTileH, a.nrows); ++k) {
     const LaunchPix p = launch_pixel(a, j0, k);
@@ -260,7 +269,7 @@ __device__ __forceinline__ int build2_tile(const FrameLaunch& a, int t, int nhug
   if (n0 != 0) a.cnt[pix] = 0;  // zero for the next call
   uint32_t info = n < (int32_t)kPixCount ? (uint32_t)n : kPixCount;
   if (n == 0 && r.records && r.have != 0u) {
-    const bool tile = a.tile_bits[t] != 0;
+    const bool tile = a.tile_bits[t * kSkipCells + (int)(threadIdx.x & 63u) / kSkipW] != 0;
     const unsigned bits = tile ? r.have : bg::pixel_skip_bits(r.cam, r.planes, r.nplanes, sg, r.nl, r.have, p.x, p.y);
     info |= bits << 24;
   }
@@ -447,7 +456,7 @@ extern "C" int rtmi_frame_build(const rtmi::FrameLaunch* a, void* stream) {
   static_assert(sizeof(FrameLaunch) <= 4096, "kernel argument size");
   hipStream_t st = (hipStream_t)stream;
   const int face_blocks = std::max(1, (a->nf + kFacesPerBlock - 1) / kFacesPerBlock);
-  const int tile_blocks = (a->ntiles + 255) / 256;
+  const int tile_blocks = (a->ntiles * kSkipCells + 255) / 256;
   hipLaunchKernelGGL(k_frame_build1, dim3(face_blocks + tile_blocks), dim3(256), 0, st, *a, face_blocks);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || a->ntiles <= 0) return (int)e;
@@ -456,6 +465,11 @@ extern "C" int rtmi_frame_build(const rtmi::FrameLaunch* a, void* stream) {
   const int nchunks = (a->ntiles + kChunkTiles - 1) / kChunkTiles;
   hipLaunchKernelGGL(k_frame_lists, dim3((unsigned)nchunks), dim3(256), 0, st, *a);
   return (int)hipGetLastError();
+}
+
+extern "C" long long rtmi_frame_skip_cells(int ncols, int nrows) {
+  using namespace rtmi;
+  return (long long)((ncols + kTileW - 1) / kTileW) * ((nrows + kTileH - 1) / kTileH) * kSkipCells;
 }
 
 extern "C" long long rtmi_frame_tile_bytes(int ncols, int nrows) {

@@ -227,7 +227,7 @@ struct rt_scene {
     DevBuf<uint32_t> info;
     DevBuf<unsigned long long> omask, status;  // status: per-tile class counts (FrameLaunch.tile_cls)
     DevBuf<HugeFace> huge;
-    DevBuf<unsigned char> tiles;   // per-tile shadow skips (k_frame_build1)
+    DevBuf<unsigned char> tiles;   // per skip cell of a tile: shadow skips (k_frame_build1)
     int slot_lg = -1;              // slots allocated for 2^slot_lg entries per pixel (-1: none)
     int want_lg = slot_lg_env();   // test hook (rtmi_test_slot_lg) / RTMI_SLOT_LG; -1: by image size
     uint32_t calls = 0;            // build launches (their parity picks the huge-list counter)
@@ -1280,7 +1280,7 @@ int frame_buffers(rt_scene* s, int w, int h, hipStream_t st) {
   f.invalidate();
   if ((rc = f.cnt.alloc(npx + 1)) || (rc = f.info.alloc(npx)) || (rc = f.lean.alloc(npx + 64)) ||
       (rc = f.heavy.alloc(npx)) || (rc = f.ctr.alloc(FC_WORDS)) ||
-      (rc = f.tiles.alloc((size_t)rtmi_frame_tile_bytes(w, h))) ||
+      (rc = f.tiles.alloc((size_t)rtmi_frame_skip_cells(w, h))) ||
       (rc = f.status.alloc((size_t)rtmi_frame_tile_bytes(w, h))))
     return rc;
   if (s->objbins && ((rc = f.omask.alloc(npx)) || (rc = f.orect.alloc(kObjRectInts)))) return rc;
