@@ -270,7 +270,7 @@ __device__ __forceinline__ int build2_tile(const FrameLaunch& a, int t, int nhug
   uint32_t info = n < (int32_t)kPixCount ? (uint32_t)n : kPixCount;
   if (n == 0 && r.records && r.have != 0u) {
     const bool tile = a.tile_bits[t * kSkipCells + (int)(threadIdx.x & 63u) / kSkipW] != 0;
-    const unsigned bits = tile ? r.have : bg::pixel_skip_bits(r.cam, r.planes, r.nplanes, sg, r.nl, r.have, p.x, p.y);
+    const unsigned bits = tile || a.diag == 1 ? r.have : bg::pixel_skip_bits(r.cam, r.planes, r.nplanes, sg, r.nl, r.have, p.x, p.y);
     info |= bits << 24;
   }
   r.info[pix] = info;

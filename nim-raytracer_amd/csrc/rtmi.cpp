@@ -1379,6 +1379,7 @@ int frame_build(rt_scene* s, const rt_options* o, const Mapping& mp, const FastP
   records_launch(s, o, mp, p, records, split, a.r);
   a.tile_bits = f.tiles.p;
   a.tile_cls = f.status.p;
+  a.diag = std::getenv("RTMI_DIAG_B2") ? std::atoi(std::getenv("RTMI_DIAG_B2")) : 0;
   a.tiles_x = (mp.ncols + 63) / 64;
   a.ntiles = a.tiles_x * ((mp.nrows + 3) / 4);
   a.zero = zero;
