@@ -1819,7 +1819,8 @@ int launch(rt_scene* s, const rt_options* o, const Mapping& mp, float* d_out, hi
         const long long mcap = (long long)rtmi_mix1_f32_blocks_per_cu(p.nlight, lp) * s->num_cus;
         const int mb = (int)std::max(1LL, std::min<long long>(std::min<long long>(mcap, blocks),
                                                               ((long long)p.ngroups + lruns + 3) / 4));
-        pm.shards = std::min(kQueueShards, mb);
+        static const int shard_cap = std::getenv("RTMI_SHARDS") ? std::atoi(std::getenv("RTMI_SHARDS")) : 0;  // diagnostic
+        pm.shards = std::min(shard_cap > 0 ? std::min(shard_cap, kQueueShards) : kQueueShards, mb);
         pm.shards2 = pm.shards;
         const int e = rtmi_launch_mix1_f32(&pm, p.nlight, lp, mb, st);
         if (e) return fail(RT_E_DEVICE, "render kernel launch failed: %s", hipGetErrorString((hipError_t)e));

@@ -36,7 +36,7 @@ def med(fn):
     return round(sorted(su)[REPS // 2] * 1000, 1), round(sorted(re)[REPS // 2] * 1000, 1)
 
 
-for world in (1, 2, 4, 8, 16):
+for world in [int(w) for w in os.environ.get("WORLDS", "1,2,4,8,16").split(",")]:
     res = {"world": world}
     for bh in (4, 16):
         s, r = med(lambda: ds.render_bands_device(opts, buf, bh, 0, world, stream=stream, stats=False))
