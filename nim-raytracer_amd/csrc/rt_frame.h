@@ -172,7 +172,7 @@ struct FrameLaunch {
   int32_t tiles_x, ntiles;
   unsigned int* zero;       // words k_frame_build1 zeroes (queue heads + Stats), or nullptr
   int32_t nzero;
-  int32_t diag;             // TEMP diagnostic (RTMI_DIAG_B2): 1 = no per-pixel skip tests (wrong bits)
+  int32_t diag;             // TEMP diagnostic (RTMI_DIAG_B2): 1 = no per-pixel skip tests, 2 = no faces, 3 = no skip cells (wrong data)
 };
 
 // object bins (rt_bins.h build_object_pixel_masks): world boxes of the objects

@@ -197,9 +197,10 @@ __global__ __launch_bounds__(256) void k_frame_build1(const FrameLaunch a, int f
     if (threadIdx.x == 0) a.r.ctr[FC_HUGE0 + (a.parity ^ 1)] = 0;
   }
   if ((int)blockIdx.x < face_blocks) {
-    faces_block(a);
+    if (a.diag != 2) faces_block(a);
     return;
   }
+  if (a.diag == 3) return;
   const int t = (int)((blockIdx.x - (unsigned)face_blocks) * 256u + threadIdx.x);
   if (a.r.records && a.r.have != 0u) {
     load_skip_grids(a.r, sg);
