@@ -1,6 +1,7 @@
 // rt_frame.hip — per-call device builders of the camera-dependent data of
 // the float32 kernels (rt_frame.h). float64 geometry (rt_bins_geom.h), built
 // with -ffp-contract=off like the host builders the tests compare against.
+#include <cstdlib>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -283,7 +284,8 @@ __device__ __forceinline__ int build2_tile(const FrameLaunch& a, int t, int nhug
 // grid serialised those chains, 90 us per C3 call).
 // With split, the tile's lean / general pixel counts (lean << 32 | general)
 // go to tile_cls for k_frame_lists.
-__global__ __launch_bounds__(256) void k_frame_build2(const FrameLaunch a) {
+template <int W>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W))) void k_frame_build2(const FrameLaunch a) {
   __shared__ bg::SkipGrid sg[8];
   __shared__ int32_t hl[256];
   __shared__ int hn;
@@ -461,7 +463,11 @@ extern "C" int rtmi_frame_build(const rtmi::FrameLaunch* a, void* stream) {
   hipLaunchKernelGGL(k_frame_build1, dim3(face_blocks + tile_blocks), dim3(256), 0, st, *a, face_blocks);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || a->ntiles <= 0) return (int)e;
-  hipLaunchKernelGGL(k_frame_build2, dim3((unsigned)a->ntiles), dim3(256), 0, st, *a);
+  static const int b2w = std::getenv("RTMI_B2_WAVES") ? std::atoi(std::getenv("RTMI_B2_WAVES")) : 4;  // diagnostic
+  if (b2w == 8)
+    hipLaunchKernelGGL(k_frame_build2<8>, dim3((unsigned)a->ntiles), dim3(256), 0, st, *a);
+  else
+    hipLaunchKernelGGL(k_frame_build2<4>, dim3((unsigned)a->ntiles), dim3(256), 0, st, *a);
   if ((e = hipGetLastError()) != hipSuccess || !a->r.split) return (int)e;
   const int nchunks = (a->ntiles + kChunkTiles - 1) / kChunkTiles;
   hipLaunchKernelGGL(k_frame_lists, dim3((unsigned)nchunks), dim3(256), 0, st, *a);
