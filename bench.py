@@ -246,13 +246,13 @@ def main():
         # render this rank's bands (world == 1: the whole frame, one band set)
         buf = local_bufs[nframe[0] % 2]
         nframe[0] += 1
-        if time_kernel is not None:
+        if time_kernel is not None and time_kernel[0] is not None:
             time_kernel[0].record(stream)
         if distributed:
             ds.render_bands_device(opts, buf, BAND_H, rank, world, stream=stream, stats=False)
         else:
             ds.render_device(opts, fb, stream=stream, stats=False)
-        if time_kernel is not None:
+        if time_kernel is not None and time_kernel[1] is not None:
             time_kernel[1].record(stream)
         if distributed:
             finish_frame()  # frame k-1, whose gather overlapped this render
@@ -283,14 +283,15 @@ def main():
         rays_frame, prim_frame, shadow_frame = rays_local, st.numPrimaryRays, st.numShadowRays
 
     # timed region
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(args.steps)]
+    # one event pair around the K render calls (a timing event per step is
+    # a marker packet between calls): call_ms = their GPU span / K
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if distributed:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(args.steps):
-        step(evs[k])
+        step((ev0 if k == 0 else None, ev1 if k == args.steps - 1 else None))
     finish_frame()  # the last frame's gather + un-interleave, inside the timed region
     torch.cuda.synchronize()
     if distributed:
@@ -300,7 +301,7 @@ def main():
         e = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
-    call_ms = sum(a.elapsed_time(b) for a, b in evs) / max(1, args.steps)
+    call_ms = ev0.elapsed_time(ev1) / max(1, args.steps)
     lean_groups, general_groups = ds.last_split()
     kinds = ds.last_lean_kernel()
     lean_k = {0: None, 1: "k_render_lean", 2: "k_render_lean1q (one-plane lean pixels)", 3: None}[kinds & 3]
@@ -386,8 +387,8 @@ def main():
                        f"{CLOCK_GHZ} GHz / {VALU_CYCLES} cycles per wave64 VALU instruction; salu_frac likewise "
                        "against one scalar instruction per CU per cycle; traffic = PMC HBM bytes per call "
                        "(2 x FETCH_SIZE + WRITE_SIZE, MI355X_MICROARCH.md)"),
-        "setup": ("per-call camera-dependent build on the device (rt_frame.hip: face-list count / scan / fill, "
-                  "pixel records + lean/general lists), inside every timed step"),
+        "setup": ("per-call camera-dependent build on the device (rt_frame.hip, three launches: faces into "
+                  "per-pixel list slots + skip cells; pixel records; lean / general lists), inside every timed step"),
         "survey_bvh_model_gbs": round(bvh_model_bytes / (render_ms * 1e-3) / 1e9, 1),
         "survey_bvh_model_note": ("SURVEY 8(d) bytes of a per-ray BVH tracer (32 B/box, 36 B/triangle, 12 B/pixel) "
                                   "from one instrumented BVH-only launch, over the render kernels' time: a model, "

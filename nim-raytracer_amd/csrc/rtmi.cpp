@@ -167,7 +167,12 @@ struct rt_scene {
   bool timed = false;
   int64_t last_lean = 0, last_general = 0;  // rt_scene_last_split
   int32_t last_lean_kind = 0;                // rt_scene_last_lean_kernel
-  bool stats_kept = true;                    // the last call reduced its Stats (no RT_FLAG_NO_STATS)
+  bool stats_kept = true;                    // the last call kept its Stats (no RT_FLAG_NO_STATS)
+  // per-wave Stats rows of the last call not yet reduced into acc(): a call
+  // whose caller does not read its Stats leaves them to the first reader
+  // (rt_scene_last_stats / _last_counters), one launch fewer per call
+  int32_t pending_reduce = 0;
+  hipStream_t done_stream = nullptr;  // the stream `done` was last recorded on
   int64_t last_batched = 0, last_fallback = -1;  // rt_scene_last_batch
   int32_t nobj = 0, nlight = 0, nmesh = 0;
   int32_t shadow_mesh = -1;  // the only mesh object, or -1 (FastParams.shadow_mesh)
@@ -1705,6 +1710,7 @@ int launch(rt_scene* s, const rt_options* o, const Mapping& mp, float* d_out, hi
   // when it returns early or runs the float64 kernel
   s->fr.counted = false;
   s->fr.listed = false;
+  s->pending_reduce = 0;
   s->last_lean = 0;
   s->last_lean_kind = 0;
   s->last_general = 0;
@@ -1914,8 +1920,19 @@ int launch(rt_scene* s, const rt_options* o, const Mapping& mp, float* d_out, hi
       }
     }
   }
-  if (!reduce) return RT_OK;  // nobody reads this call's Stats: no reduction launch
-  const int e = rtmi_launch_reduce_stats(s->partials.p, blocks * 4, s->acc(), st);
+  // the per-wave rows are reduced when the Stats are read (flush_reduce)
+  if (reduce) s->pending_reduce = blocks * 4;
+  return RT_OK;
+}
+
+// The last call's Stats rows into acc(), on stream st (ordered after the
+// call): at the end of a call whose caller reads its Stats, else by the
+// first rt_scene_last_stats / _last_counters (the scene mutex is held; a
+// later call replaces the rows and the pending count).
+int flush_reduce(rt_scene* s, hipStream_t st) {
+  if (s->pending_reduce <= 0) return RT_OK;
+  const int e = rtmi_launch_reduce_stats(s->partials.p, s->pending_reduce, s->acc(), st);
+  s->pending_reduce = 0;
   if (e) return fail(RT_E_DEVICE, "stats reduction launch failed: %s", hipGetErrorString((hipError_t)e));
   return RT_OK;
 }
@@ -1978,7 +1995,9 @@ int render_device(rt_scene* s, const rt_options* o, const Mapping& mp, float* d_
                   rt_stats* out, bool need_stats = false) {
   const bool reduce = need_stats || out || !(o->flags & RT_FLAG_NO_STATS) || (o->flags & RT_FLAG_COUNT_TRAVERSAL);
   s->stats_kept = reduce;
-  HIP_TRY(hipStreamWaitEvent(st, s->done, 0));
+  // after the scene's previous call (a call on that call's own stream is
+  // already ordered after it: no wait packet)
+  if (st != s->done_stream) HIP_TRY(hipStreamWaitEvent(st, s->done, 0));
   s->timed = (o->flags & RT_FLAG_TIMING) != 0;
   if (s->timed) {  // (tev[1] again before the render kernels; here for launches with nothing to render)
     HIP_TRY(hipEventRecord(s->tev[0], st));
@@ -1989,8 +2008,10 @@ int render_device(rt_scene* s, const rt_options* o, const Mapping& mp, float* d_
   const size_t q1 = rt_scene::kQueueWords + (reduce ? 2 * (size_t)kStatSlots : 0);
   int rc = launch(s, o, mp, d_out, st, reduce, s->queue.p + q0, (int)(q1 - q0));
   if (rc) return rc;
+  if ((out || need_stats || (o->flags & RT_FLAG_COUNT_TRAVERSAL)) && (rc = flush_reduce(s, st))) return rc;
   if (s->timed) HIP_TRY(hipEventRecord(s->tev[2], st));
   HIP_TRY(hipEventRecord(s->done, st));
+  s->done_stream = st;
   if (out) return read_stats(s, st, out);
   return RT_OK;
 }
@@ -2086,6 +2107,7 @@ extern "C" int rt_scene_last_stats(rt_scene* s, rt_stats* out) {
   if (!s->stats_kept) return fail(RT_E_INVALID, "the last render call set RT_FLAG_NO_STATS");
   DeviceGuard g(s->device);
   HIP_TRY(hipStreamWaitEvent(s->stream, s->done, 0));
+  if (int rc = flush_reduce(s, s->stream)) return rc;
   return read_stats(s, s->stream, out);
 }
 
@@ -2200,7 +2222,9 @@ extern "C" int rt_scene_last_counters(rt_scene* s, rt_traversal_counters* out) {
   if (!s->stats_kept) return fail(RT_E_INVALID, "the last render call set RT_FLAG_NO_STATS");
   DeviceGuard g(s->device);
   unsigned long long h[kStatSlots];
-  HIP_TRY(hipEventSynchronize(s->done));
+  HIP_TRY(hipStreamWaitEvent(s->stream, s->done, 0));
+  if (int rc = flush_reduce(s, s->stream)) return rc;
+  HIP_TRY(hipStreamSynchronize(s->stream));
   HIP_TRY(hipMemcpy(h, s->acc(), sizeof h, hipMemcpyDeviceToHost));
   out->wave_node_fetches = h[STAT_NODE_FETCH];
   out->wave_tri_fetches = h[STAT_TRI_FETCH];
