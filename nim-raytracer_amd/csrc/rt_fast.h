@@ -1553,6 +1553,12 @@ __device__ __forceinline__ void tri_test_t(const TR& T, F3 o, F3 d, float& best,
 // searched in its turn).
 // diag (RTMI_DIAG_LANES builds, else nullptr): += the lanes still searching
 // at each face test of each flagged sample (lane occupancy of the search).
+// RTMI_LDS_STAGE (default 1; 0 for the A/B): each step's four face records
+// staged through the wave's LDS slice instead of one scalar load per record
+// (DESIGN.md "LDS staging": C3 0.912 -> 0.895 ms, C5 79.5 -> 78.4 ms).
+#ifndef RTMI_LDS_STAGE
+#define RTMI_LDS_STAGE 1
+#endif
 template <int S, bool KEY>
 __device__ __forceinline__ int list_search_batch(KP p, const int32_t* ent, int b, int e, unsigned fl,
                                                   const F3 (&ro)[S], const F3 (&rd)[S], const float (&stop)[S],
@@ -1584,7 +1590,7 @@ __device__ __forceinline__ int list_search_batch(KP p, const int32_t* ent, int b
       ++b;
     }
   }
-#ifdef RTMI_LDS_STAGE
+#if RTMI_LDS_STAGE
   // A/B variant (DESIGN.md "LDS staging"): the 4 face records of a step
   // staged through the wave's LDS slice — lane 16 j + w loads dword w of
   // record j (one coalesced vector load for all four), then every lane
@@ -1596,7 +1602,7 @@ __device__ __forceinline__ int list_search_batch(KP p, const int32_t* ent, int b
   for (int k0 = b; k0 < e; k0 += 4) {
     const RT_CONST int32_t* q = cp(ent) + k0;
     const int r[4] = {q[0], q[1], q[2], q[3]};
-#ifdef RTMI_LDS_STAGE
+#if RTMI_LDS_STAGE
     {
       const int lane = (int)__lane_id(), j = lane >> 4, w = lane & 15;
       const int rj = j == 0 ? r[0] : j == 1 ? r[1] : j == 2 ? r[2] : r[3];
@@ -1608,7 +1614,7 @@ __device__ __forceinline__ int list_search_batch(KP p, const int32_t* ent, int b
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       if (j > 0 && k0 + j >= e) break;
-#ifdef RTMI_LDS_STAGE
+#if RTMI_LDS_STAGE
       TriRegs T;
       {
         const uint4 a = stage[4 * j + 0], bq = stage[4 * j + 1], c = stage[4 * j + 2], d4 = stage[4 * j + 3];
@@ -2920,6 +2926,97 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
   if (lane < kStatSlots) p->partials[(size_t)wave * kStatSlots + lane] = lds_tot[wib][lane];
 }
 
+// Work queue of one list of n items over `shards` heads at `queue`; the
+// blocks b with b % shards == s pull from head s, so shard s runs on XCD
+// s % 8 (workgroups are dealt out to the 8 XCDs round robin).
+// Default: shard s hands out items s, s + S, s + 2S, ... (every shard's
+// items span the image). RTMI_XCD_CHUNK=1 (A/B only, measured slower: C3
+// 0.93 -> 1.10 ms, rank 0 of 8 0.165 -> 0.396 ms — the bunny's expensive
+// items fall into few chunks and the other XCDs end up stealing from one
+// head): the list is cut into S contiguous chunks,
+// chunk c = [c n / S, (c + 1) n / S), and the S / 8 shards of an XCD own
+// consecutive chunks (shard s: chunk (s % 8) S / 8 + s / 8; S a multiple of
+// 8, else chunk s) — the lists are in image tile order, so an XCD's waves
+// work on one horizontal slab of the image and its L2 holds that slab's faces
+// and cell lists. A wave whose chunk is exhausted moves on to the next chunk
+// (the next shard of its XCD, at the slab's end the next XCD's first) and
+// takes that chunk's next items, so no XCD idles while items remain; each
+// wave visits every chunk at most once (the loop ends). The next
+// reservation is fetched one item ahead (its atomic's latency hides behind
+// the item).
+#ifndef RTMI_XCD_CHUNK
+#define RTMI_XCD_CHUNK 0
+#endif
+struct WorkQ {
+  unsigned int* queue;
+  int shards, n, cur, left, lo, len, qj_next, head;
+  __device__ __forceinline__ void bounds() {
+#if RTMI_XCD_CHUNK
+    lo = (int)(((long long)cur * n) / shards);
+    len = (int)(((long long)(cur + 1) * n) / shards) - lo;
+    const int per = shards >> 3;  // chunks per XCD
+    head = (shards & 7) == 0 ? (cur % per) * 8 + cur / per : cur;
+#else
+    head = cur;
+    lo = cur;
+    len = n;
+#endif
+  }
+  __device__ __forceinline__ int reserve() {
+    int q = 0;
+    if (__lane_id() == 0) q = (int)atomicAdd(queue + head * kQueueStride, 1u);
+    return q;
+  }
+  __device__ __forceinline__ int item(int qj) const {
+#if RTMI_XCD_CHUNK
+    return lo + qj;
+#else
+    return lo + qj * shards;
+#endif
+  }
+  __device__ __forceinline__ bool in(int qj) const {
+#if RTMI_XCD_CHUNK
+    return qj < len;
+#else
+    return item(qj) < n;
+#endif
+  }
+  // the first item (-1: none)
+  __device__ __forceinline__ int start(unsigned int* q, int s, int items) {
+    queue = q;
+    shards = s;
+    n = items;
+    const int shard = (int)(blockIdx.x % (unsigned int)s);
+#if RTMI_XCD_CHUNK
+    cur = (s & 7) == 0 ? (shard & 7) * (s >> 3) + (shard >> 3) : shard;
+#else
+    cur = shard;
+#endif
+    left = s;
+    bounds();
+    qj_next = reserve();
+    return next();
+  }
+  // the next item (-1: every shard is exhausted)
+  __device__ __forceinline__ int next() {
+    for (;;) {
+      const int qj = __builtin_amdgcn_readfirstlane(qj_next);
+      if (in(qj)) {
+        qj_next = reserve();
+        return item(qj);
+      }
+#if RTMI_XCD_CHUNK
+      if (--left <= 0) return -1;
+      cur = cur + 1 == shards ? 0 : cur + 1;
+      bounds();
+      qj_next = reserve();
+#else
+      return -1;
+#endif
+    }
+  }
+};
+
 // A one-pixel group's placement computed per lane (g differs per lane):
 // group_pixel for tile 1 x 1 (lanes_per_px = 64), without the validity test
 // (list entries are pixels of the launch).
@@ -2965,15 +3062,9 @@ template <int NL, int LP>
 __device__ __forceinline__ void lean1q_loop(KP p, const int32_t* order, int ngroups, unsigned int* queue, int shards,
                                             Stats32& ws, unsigned long long* tot, int& nflush) {
   const int lane = (int)__lane_id();
-  const int shard = (int)(blockIdx.x % (unsigned int)shards);
-  unsigned int* head = queue + shard * kQueueStride;
-  int qj = 0;
-  if (lane == 0) qj = (int)atomicAdd(head, 1u);
-  qj = __builtin_amdgcn_readfirstlane(qj);
-  int qj_next = 0;
-  if (lane == 0) qj_next = (int)atomicAdd(head, 1u);
-  int g = qj * shards + shard;
-  if (g >= ngroups) return;
+  WorkQ wq;
+  int g = wq.start(queue, shards, ngroups);
+  if (g < 0) return;
   const int iters = p->iters;
   const int po = p->shadow_mesh == 0 ? 1 : 0;
   const FObj pl = at(p->objs, po);
@@ -3022,10 +3113,8 @@ __device__ __forceinline__ void lean1q_loop(KP p, const int32_t* order, int ngro
     av = mul3(alb, E);
   }
   asm volatile("" : "+v"(av.x), "+v"(av.y), "+v"(av.z));
-  while (g < ngroups) {
+  while (g >= 0) {
     const int gg = order[g * PPI + lane / LP];  // this lane's pixel (list entry; -1: padding)
-    qj = __builtin_amdgcn_readfirstlane(qj_next);
-    if (lane == 0) qj_next = (int)atomicAdd(head, 1u);
     const unsigned long long vmask = bal(gg >= 0);
     const GroupPix gp = lane_pixel(p, gg >= 0 ? gg : 0);
     const float pxb = (float)gp.x, pyb = (float)gp.y;
@@ -3164,7 +3253,7 @@ __device__ __forceinline__ void lean1q_loop(KP p, const int32_t* order, int ngro
       flush_stats(ws, tot, lane);
       nflush = 0;
     }
-    g = qj * shards + shard;
+    g = wq.next();
   }
 }
 
@@ -3298,16 +3387,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RTMI_GEN_WA
 template <int NL>
 __device__ __forceinline__ void gen1_loop(KP p, LdsF* ls, Stats32& ws, unsigned long long* tot, int& nflush) {
   constexpr unsigned F = F_PLANE | F_MESH;
-  const int shard = (int)(blockIdx.x % (unsigned int)p->shards);
-  unsigned int* head = p->queue + shard * kQueueStride;
-  int qj = 0;
-  if (__lane_id() == 0) qj = (int)atomicAdd(head, 1u);
-  qj = __builtin_amdgcn_readfirstlane(qj);
-  int qj_next = 0;
-  if (__lane_id() == 0) qj_next = (int)atomicAdd(head, 1u);
-  int g = qj * p->shards + shard;
-  const int ngroups = list_items(p->list_n, p->ngroups, 1);
-  while (g < ngroups) {
+  WorkQ wq;
+  int g = wq.start(p->queue, p->shards, list_items(p->list_n, p->ngroups, 1));
+  while (g >= 0) {
     p = params();
     const int iters = p->iters;
     const int gg = cp(p->order)[g];
@@ -3358,9 +3440,7 @@ __device__ __forceinline__ void gen1_loop(KP p, LdsF* ls, Stats32& ws, unsigned 
       flush_stats(ws, tot, lane);
       nflush = 0;
     }
-    qj = __builtin_amdgcn_readfirstlane(qj_next);
-    if (lane == 0) qj_next = (int)atomicAdd(head, 1u);
-    g = qj * p->shards + shard;
+    g = wq.next();
   }
 }
 

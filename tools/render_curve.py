@@ -20,7 +20,7 @@ ds = DeviceScene(scenes.mesh_bunny())
 opts = Options(width=W, height=H, antialias=Antialias(akGrid, M), bias=1e-4, precision=Precision.fp32,
                flags=RT_FLAG_TIMING | int(os.environ.get("RTMI_FLAGS", "0"), 0))
 stream = torch.cuda.current_stream()
-buf = torch.zeros(W * H * 3, dtype=torch.float32, device="cuda")
+buf = torch.zeros((H + 16 * 16) * W * 3, dtype=torch.float32, device="cuda")  # (band buffers round up)
 
 
 def med(fn):
