@@ -1590,43 +1590,44 @@ __device__ __forceinline__ int list_search_batch(KP p, const int32_t* ent, int b
       ++b;
     }
   }
+  // LDS staging (RTMI_LDS_STAGE, DESIGN.md "LDS staging"): the 4 face
+  // records of a step staged through the wave's LDS slice — lane 16 j + w
+  // loads dword w of record j (one coalesced vector load for all four), then
+  // every lane reads each record back as a broadcast (ds_read_b128 x 4) —
+  // instead of one scalar load per record. 1: both searches, 2: the shadow
+  // (cell list) searches only, 3: the camera (pixel list) searches only.
+  constexpr bool kStage = RTMI_LDS_STAGE == 1 || (RTMI_LDS_STAGE == 2 && !KEY) || (RTMI_LDS_STAGE == 3 && KEY);
 #if RTMI_LDS_STAGE
-  // A/B variant (DESIGN.md "LDS staging"): the 4 face records of a step
-  // staged through the wave's LDS slice — lane 16 j + w loads dword w of
-  // record j (one coalesced vector load for all four), then every lane
-  // reads each record back as a broadcast (ds_read_b128 x 4) — instead of
-  // one scalar load per record
   __shared__ uint4 stage_lds[4][16];
   uint4* stage = stage_lds[threadIdx.x >> 6];
+#else
+  uint4* stage = nullptr;
 #endif
   for (int k0 = b; k0 < e; k0 += 4) {
     const RT_CONST int32_t* q = cp(ent) + k0;
     const int r[4] = {q[0], q[1], q[2], q[3]};
-#if RTMI_LDS_STAGE
-    {
+    if constexpr (kStage) {
       const int lane = (int)__lane_id(), j = lane >> 4, w = lane & 15;
       const int rj = j == 0 ? r[0] : j == 1 ? r[1] : j == 2 ? r[2] : r[3];
       const unsigned int* src = (const unsigned int*)((const char*)p->tree + (unsigned)rj);
       ((unsigned int*)stage)[lane] = k0 + j < e ? src[w] : 0u;
       __builtin_amdgcn_wave_barrier();
     }
-#endif
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       if (j > 0 && k0 + j >= e) break;
-#if RTMI_LDS_STAGE
       TriRegs T;
-      {
+      if constexpr (kStage) {
         const uint4 a = stage[4 * j + 0], bq = stage[4 * j + 1], c = stage[4 * j + 2], d4 = stage[4 * j + 3];
         T.v0[0] = __uint_as_float(a.x), T.v0[1] = __uint_as_float(a.y), T.v0[2] = __uint_as_float(a.z);
         T.id = a.w;
         T.e2[0] = __uint_as_float(bq.x), T.e2[1] = __uint_as_float(bq.y), T.e2[2] = __uint_as_float(bq.z);
         T.e1n[0] = __uint_as_float(c.x), T.e1n[1] = __uint_as_float(c.y), T.e1n[2] = __uint_as_float(c.z);
         T.nn[0] = __uint_as_float(d4.x), T.nn[1] = __uint_as_float(d4.y), T.nn[2] = __uint_as_float(d4.z);
+      } else {
+        (void)stage;
+        T = load_tri(rec<TriFast>(p, r[j]));
       }
-#else
-      const TriRegs T = load_tri(rec<TriFast>(p, r[j]));
-#endif
       lanes();
 #pragma unroll
       for (int k = 0; k < S; ++k)
@@ -1965,6 +1966,15 @@ __device__ __forceinline__ bool gen_batch(KP p, const GroupPix& gp, int it0, con
 // are gen_batch's, unchanged. Returns false, before adding anything, where
 // gen_batch does (a shadow ray that needs the BVH). Frames and Stats
 // bit-identical to gen_batch (tests/test_gpu_split.py, RT_FLAG_NO_GEN1).
+// RTMI_GEN1_COMPACT=1 (A/B, row n2): the two samples' rays of a light cell
+// packed into one slot when they fit one wave (gen1_batch's cell loop).
+// Exact (frames and Stats bit-identical, GPU parity tests green) but slower:
+// C3 0.901 -> 0.918 ms, C5 78.5 -> 79.4 ms — the pairing and permutes cost
+// more than the face tests they save, and the kernel's spills grow from 4
+// to 18 VGPRs (DESIGN.md "Live-ray compaction of the light-cell searches").
+#ifndef RTMI_GEN1_COMPACT
+#define RTMI_GEN1_COMPACT 0
+#endif
 template <int S, int NL>
 __device__ __forceinline__ bool gen1_batch(KP p, const GroupPix& gp, int pu, int it0, unsigned pinfo, Acc& acc,
                                            Stats32& wi) {
@@ -2156,6 +2166,10 @@ __device__ __forceinline__ bool gen1_batch(KP p, const GroupPix& gp, int pu, int
           if (mesh == 0) stop[k] = tpl[k] >= 0.0f ? fminf(stop[k], tpl[k]) : stop[k];
         }
         const RT_CONST LightGrid& G = cp(q->grids)[li];
+#if RTMI_GEN1_COMPACT
+        __shared__ int cmp_lds_all[4][64];  // per wave: the lane pairing of a compacted cell search
+        int* cmp_lds = cmp_lds_all[threadIdx.x >> 6];
+#endif
         int cell[S];
         unsigned long long todo[S], left = 0ull, unsafe = 0ull;
 #pragma unroll
@@ -2198,6 +2212,65 @@ __device__ __forceinline__ bool gen1_batch(KP p, const GroupPix& gp, int pu, int
           }
 #ifdef RTMI_DIAG_GEN_NOTESTS
           continue;  // diagnostic build only (wrong images): the cell loop without its face tests
+#endif
+#if RTMI_GEN1_COMPACT
+          // Both samples have rays in this cell and together they fit one
+          // wave: sample 1's rays move into the lanes sample 0 leaves free
+          // (ballot + v_mbcnt ranks, the lane pairing through LDS, the ray
+          // state by ds_bpermute) and the cell's faces are tested once
+          // instead of twice; each ray's tests and its retirement are
+          // unchanged, so `best` (the only state the shade reads back: found /
+          // not found, and its order against `stop`) is the two-slot
+          // search's. Lanes outside the cell test faces as a harmless
+          // superset either way (list_search_batch).
+          if constexpr (S == 2) {
+            const unsigned long long m0 = own[0], m1 = own[1], fr0 = ~own[0];
+            const unsigned n1 = pc(m1);
+            if (fl == 3u && pc(m0) + n1 <= 64u) {
+              const int lane = (int)__lane_id();
+              const unsigned r1 = __builtin_amdgcn_mbcnt_hi((unsigned)(m1 >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m1, 0u));
+              const unsigned rf = __builtin_amdgcn_mbcnt_hi((unsigned)(fr0 >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)fr0, 0u));
+              const bool src = lane_in(m1), dst = lane_in(fr0) && rf < n1;
+              int* pair = cmp_lds;
+              if (src) pair[r1] = lane;          // the r-th ray of sample 1 ...
+              __builtin_amdgcn_wave_barrier();
+              const int from = dst ? pair[rf] : lane;  // ... goes to the r-th free lane
+              __builtin_amdgcn_wave_barrier();
+              if (dst) pair[rf] = lane;
+              __builtin_amdgcn_wave_barrier();
+              const int to = src ? pair[r1] : lane;
+              __builtin_amdgcn_wave_barrier();
+              auto take = [&](float v0, float v1) {  // slot 0's value, or sample 1's from `from`
+                const float m = __int_as_float(__builtin_amdgcn_ds_bpermute(from << 2, __float_as_int(v1)));
+                return dst ? m : v0;
+              };
+              F3 ro_c[1] = {f3(take(ro[0].x, ro[1].x), take(ro[0].y, ro[1].y), take(ro[0].z, ro[1].z))};
+              const F3 rd_c[1] = {rd[0]};  // (both samples: the light's direction)
+              const float stop_c[1] = {take(stop[0], stop[1])};
+              float best_c[1] = {take(best[0], best[1])}, tc_c[1] = {take(tc[0], tc[1])};
+              const unsigned long long own_c[1] = {m0 | bal(dst)};
+              unsigned long long key_c[1] = {0ull};
+#ifdef RTMI_DIAG_LANES
+              unsigned dl = 0u;
+              const int nt = list_search_batch<1, false>(q, bent, cp(q->grid_off)[kb], cp(q->grid_off)[kb + 1], 1u, ro_c,
+                                                         rd_c, stop_c, own_c, key_c, best_c, tc_c, &dl);
+              wi.v[STAT_NODE_FETCH] += (unsigned)nt;
+              wi.v[STAT_LANE_NODES] += dl;
+#else
+              (void)list_search_batch<1, false>(q, bent, cp(q->grid_off)[kb], cp(q->grid_off)[kb + 1], 1u, ro_c, rd_c,
+                                                stop_c, own_c, key_c, best_c, tc_c);
+#endif
+              // back: slot 0 in place, sample 1's rays from the lane they moved to
+              const float b1 = __int_as_float(__builtin_amdgcn_ds_bpermute(to << 2, __float_as_int(best_c[0])));
+              const float t1 = __int_as_float(__builtin_amdgcn_ds_bpermute(to << 2, __float_as_int(tc_c[0])));
+              const bool in0 = lane_in(m0);
+              best[0] = in0 ? best_c[0] : best[0];
+              tc[0] = in0 ? tc_c[0] : tc[0];
+              best[1] = src ? b1 : best[1];
+              tc[1] = src ? t1 : tc[1];
+              continue;
+            }
+          }
 #endif
 #ifdef RTMI_DIAG_LANES  // diagnostic: shadow face tests (x flagged samples) and the lanes still searching
           unsigned dl = 0u;
@@ -2929,8 +3002,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
 // Work queue of one list of n items over `shards` heads at `queue`; the
 // blocks b with b % shards == s pull from head s, so shard s runs on XCD
 // s % 8 (workgroups are dealt out to the 8 XCDs round robin).
-// Default: shard s hands out items s, s + S, s + 2S, ... (every shard's
-// items span the image). RTMI_XCD_CHUNK=1 (A/B only, measured slower: C3
+// Default: shard s hands out runs of R consecutive items, s R .. s R + R - 1,
+// then (s + S) R .., ... (every shard's items span the image; R = RUN: a run
+// of neighbouring pixels is written by one XCD, so fewer framebuffer lines
+// are written back partially by two XCDs' L2s). RTMI_XCD_CHUNK=1 (A/B only, measured slower: C3
 // 0.93 -> 1.10 ms, rank 0 of 8 0.165 -> 0.396 ms — the bunny's expensive
 // items fall into few chunks and the other XCDs end up stealing from one
 // head): the list is cut into S contiguous chunks,
@@ -2947,6 +3022,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
 #ifndef RTMI_XCD_CHUNK
 #define RTMI_XCD_CHUNK 0
 #endif
+#ifndef RTMI_GEN_RUN
+#define RTMI_GEN_RUN 8   // general items (one pixel each): 8 pixels = 96 B of framebuffer per run
+#endif
+#ifndef RTMI_LEAN_RUN
+#define RTMI_LEAN_RUN 2  // one-plane lean items (4 or 16 pixels each)
+#endif
+template <int RUN = 1>
 struct WorkQ {
   unsigned int* queue;
   int shards, n, cur, left, lo, len, qj_next, head;
@@ -2971,7 +3053,7 @@ struct WorkQ {
 #if RTMI_XCD_CHUNK
     return lo + qj;
 #else
-    return lo + qj * shards;
+    return (qj / RUN * shards + lo) * RUN + qj % RUN;
 #endif
   }
   __device__ __forceinline__ bool in(int qj) const {
@@ -3062,7 +3144,7 @@ template <int NL, int LP>
 __device__ __forceinline__ void lean1q_loop(KP p, const int32_t* order, int ngroups, unsigned int* queue, int shards,
                                             Stats32& ws, unsigned long long* tot, int& nflush) {
   const int lane = (int)__lane_id();
-  WorkQ wq;
+  WorkQ<RTMI_LEAN_RUN> wq;
   int g = wq.start(queue, shards, ngroups);
   if (g < 0) return;
   const int iters = p->iters;
@@ -3387,7 +3469,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RTMI_GEN_WA
 template <int NL>
 __device__ __forceinline__ void gen1_loop(KP p, LdsF* ls, Stats32& ws, unsigned long long* tot, int& nflush) {
   constexpr unsigned F = F_PLANE | F_MESH;
-  WorkQ wq;
+  WorkQ<RTMI_GEN_RUN> wq;
   int g = wq.start(p->queue, p->shards, list_items(p->list_n, p->ngroups, 1));
   while (g >= 0) {
     p = params();

@@ -156,7 +156,7 @@ struct rt_scene {
   int device = 0;
   int num_cus = 256;
   hipStream_t stream = nullptr;
-  hipEvent_t done = nullptr;
+  hipEvent_t done = nullptr;  // the last call's completion: its buffer set's `used` event (not owned)
   // two-class launches: the lean kernel runs on `aux`, forked from and
   // joined back into the caller's stream, so its waves take the general
   // kernel's slots as that kernel's waves drain (no tail between the two)
@@ -164,9 +164,13 @@ struct rt_scene {
   hipEvent_t fork = nullptr, join = nullptr;
   // Pipelined calls alternate between two sets of per-call buffers (Frame +
   // queue heads / Stats words): the call's camera-dependent build runs on
-  // `bstream`, after only the call two back that used the same set, so it
-  // overlaps the previous call's render kernels; the render waits for its own
-  // build (Frame::built). A float32 call is pipelined when it renders at most
+  // `bstream` (the device's highest stream priority), after only the call two
+  // back that used the same set, so it overlaps the previous call's render
+  // kernels; the render waits for its own build (Frame::built). The render's
+  // persistent waves leave the build about one block per CU, so its first
+  // launch stretches over the render and the other two follow it (rank 0 of
+  // 8: 35 us of build in stream order, 23 us exposed when pipelined; a third
+  // buffer set measured no better). A float32 call is pipelined when it renders at most
   // a third of the image (a multi-GPU rank's bands, a pool's scanlines: the
   // build is about fixed per call, the render shrinks with the launch); a
   // whole frame fills the GPU by itself and runs its build in stream order
@@ -297,7 +301,6 @@ struct rt_scene {
     bin_dev.release();
     sat_dev.release();
     objbox_dev.release();
-    if (done) (void)hipEventDestroy(done);
     if (fork) (void)hipEventDestroy(fork);
     for (hipEvent_t& e : tev)
       if (e) (void)hipEventDestroy(e);
@@ -774,16 +777,25 @@ extern "C" int rt_scene_create(const rt_scene_desc* d, rt_scene** out_scene) {
   std::memcpy(s->c2w, d->camera_to_world, sizeof s->c2w);
   std::memcpy(s->bg, d->bg_color, sizeof s->bg);
   HIP_TRY(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
-  HIP_TRY(hipEventCreateWithFlags(&s->done, hipEventDisableTiming));
   HIP_TRY(hipStreamCreateWithFlags(&s->aux, hipStreamNonBlocking));
   HIP_TRY(hipEventCreateWithFlags(&s->fork, hipEventDisableTiming));
   HIP_TRY(hipEventCreateWithFlags(&s->join, hipEventDisableTiming));
   for (hipEvent_t& e : s->tev) HIP_TRY(hipEventCreate(&e));
-  HIP_TRY(hipStreamCreateWithFlags(&s->bstream, hipStreamNonBlocking));
+  {
+    // the build stream at the highest priority (rank 0 of 8 back to back:
+    // 0.163 -> 0.161 ms); RTMI_PIPE_PRIO=0: the default priority (A/B)
+    int lo = 0, hi = 0;
+    const char* pe = std::getenv("RTMI_PIPE_PRIO");
+    if (!(pe && std::atoi(pe) == 0) && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess)
+      HIP_TRY(hipStreamCreateWithPriority(&s->bstream, hipStreamNonBlocking, hi));
+    else
+      HIP_TRY(hipStreamCreateWithFlags(&s->bstream, hipStreamNonBlocking));
+  }
   for (rt_scene::Frame* f : {&s->fr, &s->fr2}) {
     HIP_TRY(hipEventCreateWithFlags(&f->built, hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&f->used, hipEventDisableTiming));
   }
+  s->done = s->fr.used;
   s->fr2.id = 1;
   {
     const char* e = std::getenv("RTMI_PIPE");
@@ -1888,7 +1900,11 @@ int launch(rt_scene* s, const rt_options* o, const Mapping& mp, float* d_out, hi
         static const int shard_cap = std::getenv("RTMI_SHARDS") ? std::atoi(std::getenv("RTMI_SHARDS")) : 0;  // diagnostic
         pm.shards = std::min(shard_cap > 0 ? std::min(shard_cap, kQueueShards) : kQueueShards, mb);
         pm.shards2 = pm.shards;
-        const int e = rtmi_launch_mix1_f32(&pm, p.nlight, lp, mb, st);
+        // diagnostic (RTMI_PIPE_GRID=<percent>): a pipelined call's grid capped,
+        // leaving CU slots to the next call's build
+        static const int pipe_grid = std::getenv("RTMI_PIPE_GRID") ? std::atoi(std::getenv("RTMI_PIPE_GRID")) : 0;
+        const int mbl = s->pipe && pipe_grid > 0 ? std::max(1, (int)((long long)mb * pipe_grid / 100)) : mb;
+        const int e = rtmi_launch_mix1_f32(&pm, p.nlight, lp, mbl, st);
         if (e) return fail(RT_E_DEVICE, "render kernel launch failed: %s", hipGetErrorString((hipError_t)e));
         blocks = mb;
         s->last_lean_kind = 3 | (3 << 2) | (lp << 8);
@@ -2077,9 +2093,10 @@ int render_device(rt_scene* s, const rt_options* o, const Mapping& mp, float* d_
   if (rc) return rc;
   if ((out || need_stats || (o->flags & RT_FLAG_COUNT_TRAVERSAL)) && (rc = flush_reduce(s, st))) return rc;
   if (s->timed) HIP_TRY(hipEventRecord(s->tev[2], st));
-  HIP_TRY(hipEventRecord(s->done, st));
+  // one event per call: the set's `used` is also the scene's `done`
   HIP_TRY(hipEventRecord(s->fr.used, st));
   s->fr.used_rec = true;
+  s->done = s->fr.used;
   s->done_stream = st;
   if (out) return read_stats(s, st, out);
   return RT_OK;
