@@ -1230,6 +1230,14 @@ constexpr int kLeanBatch = RTMI_LEAN_BATCH;
 // only those of the light-grid cells their origins fall in — in scene order,
 // exactly as trace's object bins (an object no bin lists cannot be hit, so it
 // adds nothing to a closest hit or a hit count).
+// RTMI_OB_CELLS_JOINT (default 1): an object-binned batch walks the distinct
+// light-grid cells of all its samples' shadow origins once (up to 2 S cells,
+// then every object), not each sample's cells in turn (up to 4 each). The
+// object mask either way holds every object a shadow ray can hit, so frames
+// and Stats do not change.
+#ifndef RTMI_OB_CELLS_JOINT
+#define RTMI_OB_CELLS_JOINT 1
+#endif
 template <unsigned F, int S = kLeanBatch, bool OB = false>
 __device__ __forceinline__ void lean_batch(KP p, const GroupPix& gp, int it0, const LdsF* tb, Acc& acc,
                                            Stats32& ws, unsigned long long cmask = ~0ull) {
@@ -1415,6 +1423,41 @@ __device__ __forceinline__ void lean_batch(KP p, const GroupPix& gp, int it0, co
           const RT_CONST LightGrid& G = cp(p->obj_grids)[li];
           unsigned long long m = p->obj_off_grid;
           bool every = false;
+#if RTMI_OB_CELLS_JOINT
+          // the distinct cells of all S samples' origins, each mask loaded
+          // once (the samples of a pixel's lanes mostly share their cells:
+          // per sample the same cells were walked S times)
+          int cell[S];
+          unsigned long long todo[S], left = 0ull;
+#pragma unroll
+          for (int k = 0; k < S; ++k) {
+            const bool lk = lane_in(litm[k]);
+            const F3 q = so[k];
+            const float gu = __builtin_fmaf(q.x, G.e1[0], __builtin_fmaf(q.y, G.e1[1], q.z * G.e1[2]));
+            const float gv = __builtin_fmaf(q.x, G.e2[0], __builtin_fmaf(q.y, G.e2[1], q.z * G.e2[2]));
+            const float fu = (gu - G.u0) * G.inv_h, fv = (gv - G.v0) * G.inv_h;
+            const bool safe = fmaxf(fmaxf(fabsf(q.x), fabsf(q.y)), fabsf(q.z)) <= G.rmax;
+            const bool on = fu >= 0.0f && fu < (float)G.gu && fv >= 0.0f && fv < (float)G.gv;
+            cell[k] = on ? (int)fv * G.gu + (int)fu : -1;
+            todo[k] = bal(lk && safe && on);
+            left |= todo[k];
+            every = every || bal(lk && !safe) != 0ull;
+          }
+          for (int it = 0; it < 2 * S && left != 0ull; ++it) {
+            int kc = 0;
+#pragma unroll
+            for (int k = S - 1; k >= 0; --k)
+              if (todo[k]) kc = __builtin_amdgcn_readlane(cell[k], (int)__builtin_ctzll(todo[k]));
+            left = 0ull;
+#pragma unroll
+            for (int k = 0; k < S; ++k) {
+              todo[k] &= ~bal(cell[k] == kc);
+              left |= todo[k];
+            }
+            m |= cp(p->obj_grid_mask)[G.off_base + kc];
+          }
+          every = every || left != 0ull;
+#else
 #pragma unroll
           for (int k = 0; k < S; ++k) {
             const bool lk = lane_in(litm[k]);
@@ -1433,6 +1476,7 @@ __device__ __forceinline__ void lean_batch(KP p, const GroupPix& gp, int it0, co
             }
             every = every || todo != 0ull || bal(lk && !safe) != 0ull;
           }
+#endif
           smask = every ? smask : m;
         }
       }
