@@ -1862,14 +1862,17 @@ int launch(rt_scene* s, const rt_options* o, const Mapping& mp, float* d_out, hi
       const bool lean1 = one_plane && !(o->flags & RT_FLAG_NO_LEAN1);
       // work items: runs of kLeanRun pixels (k_render_lean, k_render_lean1),
       // 64 / lp pixels (k_render_lean1q, lp lanes per pixel): 16 per item
-      // unless the launch's groups make fewer than 8 items per resident wave
-      // (a short launch, e.g. a multi-GPU rank's bands), then 4
+      // unless the launch's groups make fewer items than resident waves (a
+      // short launch, e.g. a scanline), then 4. (Round 3 switched below 8
+      // items per wave; a rank's bands at N = 8 — 2 per wave — render faster
+      // at 16 pixels per item in a back-to-back loop: 0.1605 -> 0.1539 ms,
+      // N = 4 0.278 -> 0.265 ms, profiles/r4/ab/r4t_*)
       const long long lwaves4 =
           4LL * std::min<long long>((long long)rtmi_lean1_f32_blocks_per_cu(p.nlight, 4) * s->num_cus, s->max_waves / 4);
       static const int lp_env = std::getenv("RTMI_LEAN_LP") ? std::atoi(std::getenv("RTMI_LEAN_LP")) : 0;  // diagnostic: 4 / 16
       const int lp = !(lean1 && rtmi_lean1_quads())
                          ? 64
-                         : (lp_env == 4 || lp_env == 16 ? lp_env : ((long long)(p.ngroups + 15) / 16 >= 8 * lwaves4 ? 4 : 16));
+                         : (lp_env == 4 || lp_env == 16 ? lp_env : ((long long)(p.ngroups + 15) / 16 >= lwaves4 ? 4 : 16));
       const long long lcap =
           (long long)(lean1 ? rtmi_lean1_f32_blocks_per_cu(p.nlight, lp) : rtmi_lean_f32_blocks_per_cu(sub, shmem)) *
           s->num_cus;
