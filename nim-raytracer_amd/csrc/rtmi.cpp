@@ -791,9 +791,20 @@ extern "C" int rt_scene_create(const rt_scene_desc* d, rt_scene** out_scene) {
     else
       HIP_TRY(hipStreamCreateWithFlags(&s->bstream, hipStreamNonBlocking));
   }
-  for (rt_scene::Frame* f : {&s->fr, &s->fr2}) {
-    HIP_TRY(hipEventCreateWithFlags(&f->built, hipEventDisableTiming));
-    HIP_TRY(hipEventCreateWithFlags(&f->used, hipEventDisableTiming));
+  {
+    // `built` only orders the build stream before the caller's stream on this
+    // device: a device-scope release (no system-scope cache writeback) is
+    // enough. `used` doubles as `done`, which the host waits on before
+    // reading device memory and peers copy behind: system scope.
+    // RTMI_EVENT_SCOPE (A/B): 0 both system scope, 2 both device scope.
+    const char* es = std::getenv("RTMI_EVENT_SCOPE");
+    const int scope = es && *es ? std::atoi(es) : 1;
+    const unsigned fb = hipEventDisableTiming | (scope >= 1 ? hipEventReleaseToDevice : 0u);
+    const unsigned fu = hipEventDisableTiming | (scope >= 2 ? hipEventReleaseToDevice : 0u);
+    for (rt_scene::Frame* f : {&s->fr, &s->fr2}) {
+      HIP_TRY(hipEventCreateWithFlags(&f->built, fb));
+      HIP_TRY(hipEventCreateWithFlags(&f->used, fu));
+    }
   }
   s->done = s->fr.used;
   s->fr2.id = 1;
