@@ -143,6 +143,11 @@ struct RenderParams {
   int32_t tile_x, tile_y;          // pixels per wave = tile_x * tile_y = 64 / L
   int32_t tiles_x;
   long long ngroups;               // tiles_x * tiles_y
+  // this call's pixel records (rt_frame.h: list length + shadow skip bits
+  // << 24), or nullptr: a pixel whose camera rays provably miss the mesh
+  // skips its traversal for them, and for the shadow rays of the lights
+  // whose skip bit is set (the camera level only)
+  const uint32_t* pix_info;
 };
 
 // ---- float32 performance-kernel records (rt_fast.h) -------------------------

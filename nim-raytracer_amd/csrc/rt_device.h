@@ -400,7 +400,7 @@ __device__ __forceinline__ R analytic_t(const RT_CONST DevObject<R>& ob, int typ
 // later comparison is decided, so the lane stops searching for a closer face.
 template <class R, bool COUNT>
 __device__ __forceinline__ Hit<R> trace(const RenderParams<R>& p, V3<R> o, V3<R> d, R t_near,
-                                        bool active, bool shadow, WaveStats& ws) {
+                                        bool active, bool shadow, WaveStats& ws, bool no_mesh = false) {
   Hit<R> h{-1, -1, t_near};
   ws.v[STAT_TESTS] += popc32(ballot(active)) * (unsigned int)p.nobj;
   const bool early = shadow && p.shadow_mesh >= 0;
@@ -436,7 +436,9 @@ __device__ __forceinline__ Hit<R> trace(const RenderParams<R>& p, V3<R> o, V3<R>
       // TriangleMesh.intersect (geom.nim:339-358): AABB gate (tmin < 0 ->
       // miss, so rays starting inside the box miss), then closest face.
       const R gate = aabb_ref<R>(V3<R>{m.lo[0], m.lo[1], m.lo[2]}, V3<R>{m.hi[0], m.hi[1], m.hi[2]}, r);
-      const bool in = active && gate >= R(0);
+      // no_mesh: the pixel's record proves that no face of the mesh can be
+      // hit by this ray: the traversal would find none (best stays -1)
+      const bool in = active && gate >= R(0) && !no_mesh;
       R tb = h.t;
       int best = -1;
       traverse<R, COUNT>(p, m.root, r.o, r.d, in, early && i == p.shadow_mesh, stop, tb, best, ws);
@@ -490,7 +492,7 @@ __device__ __forceinline__ V3<R> object_normal(const RT_CONST DevObject<R>& ob, 
 // into a loop of levels. Returns the sample colour (renderer.nim:71-127).
 template <class R, bool COUNT>
 __device__ __forceinline__ V3<R> shade_path(const RenderParams<R>& p, V3<R> o, V3<R> d, bool active,
-                                            WaveStats& ws) {
+                                            WaveStats& ws, unsigned pinfo = kPixCount) {
   constexpr R kPi = R(3.14159265358979323846);
   bool act = active;
   int depth = 1;
@@ -504,7 +506,10 @@ __device__ __forceinline__ V3<R> shade_path(const RenderParams<R>& p, V3<R> o, V
   int nlev = 0;
   for (int lev = 0; lev < kMaxShadeLevels; ++lev) {
     if (ballot(act) == 0ull) break;
-    const Hit<R> hit = trace<R, COUNT>(p, o, d, pinf<R>(), act, false, ws);
+    // the pixel's record (camera level only): an empty camera-ray list, and
+    // per distant light a skip bit for the shadow rays from its camera hits
+    const bool cam_skip = lev == 0 && (pinfo & kPixCount) == 0u;
+    const Hit<R> hit = trace<R, COUNT>(p, o, d, pinf<R>(), act, false, ws, cam_skip);
     if (act && hit.obj < 0) terminal = V3<R>{p.bg[0], p.bg[1], p.bg[2]};
     const bool lit = act && hit.obj >= 0;
     const V3<R> hw{o.x + d.x * hit.t, o.y + d.y * hit.t, o.z + d.z * hit.t};
@@ -566,7 +571,8 @@ __device__ __forceinline__ V3<R> shade_path(const RenderParams<R>& p, V3<R> o, V
       const V3<R> sd{ldir.x * R(-1), ldir.y * R(-1), ldir.z * R(-1)};
       const V3<R> so{hw.x + N.x * p.bias, hw.y + N.y * p.bias, hw.z + N.z * p.bias};
       ws.v[STAT_SHADOW] += popc32(ballot(lit));
-      const Hit<R> sh = trace<R, COUNT>(p, so, sd, dist, lit, true, ws);
+      const bool sh_skip = cam_skip && li < 8 && L.type != LIGHT_POINT && ((pinfo >> (24 + li)) & 1u) != 0u;
+      const Hit<R> sh = trace<R, COUNT>(p, so, sd, dist, lit, true, ws, sh_skip);
       if (lit && sh.obj < 0) {  // shadeDiffuse (shader.nim:12-17)
         const R ndl = nmax(R(0), dot4(N, R(0), sd, R(0) * R(-1)));
         local.x = local.x + Prec<R>::div(alb.x, kPi) * I.x * ndl;
@@ -675,6 +681,7 @@ __global__ __launch_bounds__(256, RTMI_MIN_WAVES) void k_render(const RenderPara
       if ((x & mask) == 0 && (y & mask) == 0) valid = false;
     }
     V3<R> acc{R(0), R(0), R(0)};
+    const unsigned pinfo = (!COUNT && p.pix_info && valid) ? p.pix_info[(size_t)y * p.width + x] : kPixCount;
     // stochastic kinds (sampling.nim:21-113): this lane's pixel table, built
     // sequentially like calcPixel's `samples` in its slice of the scratch
     R* tsx = nullptr;
@@ -703,7 +710,7 @@ __global__ __launch_bounds__(256, RTMI_MIN_WAVES) void k_render(const RenderPara
       const V3<R> o = xform<R>(p.c2w, V3<R>{R(0), R(0), R(0)}, R(1));
       const V3<R> d = xform<R>(p.c2w, dn, R(0));
       ws.v[STAT_PRIMARY] += popc32(ballot(sv));
-      const V3<R> c = shade_path<R, COUNT>(p, o, d, sv, ws);
+      const V3<R> c = shade_path<R, COUNT>(p, o, d, sv, ws, pinfo);
       if (sv) {
         if (grid_aa) {
           acc = V3<R>{acc.x + c.x, acc.y + c.y, acc.z + c.z};

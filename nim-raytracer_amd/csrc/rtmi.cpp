@@ -1818,6 +1818,18 @@ int launch(rt_scene* s, const rt_options* o, const Mapping& mp, float* d_out, hi
     s->last_lean_kind = 0;
     s->last_general = p.ngroups;
     s->last_batched = 0;
+    // this call's pixel records (the float32 path's build, one launch set):
+    // a pixel whose camera rays provably miss the mesh skips their traversal,
+    // and its shadow rays to the lights its skip bits clear skip theirs —
+    // the same answers (the traversal would find no face), so frames and
+    // Stats stay bit-exact (tests/test_gpu_parity.py)
+    if (!(o->flags & (RT_FLAG_NO_BINNING | RT_FLAG_COUNT_TRAVERSAL)) && sampler_in_pixel(o->aa_kind) && s->skippable) {
+      FastParams pf;
+      std::memset(&pf, 0, sizeof pf);
+      bool lists = false, zeroed = false;
+      if (int rc = frame_build(s, o, mp, pf, true, false, nullptr, 0, st, &lists, &zeroed)) return rc;
+      if (lists) p.pix_info = s->fr.info.p;
+    }
     const int e = rtmi_launch_render_f64(&p, blocks, st);
     if (e) return fail(RT_E_DEVICE, "render kernel launch failed: %s", hipGetErrorString((hipError_t)e));
   } else {
