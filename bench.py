@@ -307,7 +307,9 @@ def main():
     lean_k = {0: None, 1: "k_render_lean", 2: "k_render_lean1q (one-plane lean pixels)", 3: None}[kinds & 3]
     gen_k = {0: "k_render_fast<false>", 1: "k_render_gen", 2: "k_render_gen1 (one-plane general pixels)",
              3: None}[kinds >> 2 & 3]
-    kernel_desc = ("k_render<double> (fp64 parity kernel, one lane per pixel, BVH for every ray)" if fp64 else
+    kernel_desc = ("k_render_px64 (fp64 parity kernel: one pixel per wave, 64 samples side by side, camera rays "
+                   "through the pixel's face list, shadow rays through their light-grid cells, samples summed in "
+                   "sample order)" if fp64 else
                    "k_render_mix1 (one-plane scene: general pixels, then lean pixels, one merged kernel)"
                    if kinds == 15 else f"{gen_k} + {lean_k} (two-class launch)" if lean_k else gen_k)
     # after the timed region, the same steps once more with RT_FLAG_TIMING:
@@ -416,7 +418,7 @@ def main():
                      "torus": "synthetic rays over a deterministic procedural 1M-triangle torus"}[scene_name],
             "config": {
                 "workload": (f"{desc}, {W}x{H}, akGrid {m}x{m} = {m * m} spp, "
-                             + ("fp64 parity mode (k_render<double>: the reference's arithmetic, bit-exact "
+                             + ("fp64 parity mode (k_render_px64: the reference's arithmetic, bit-exact "
                                 "against the oracle), " if fp64 else "fp32, ")
                              + (f"{BAND_H}-row bands round-robin over {world} ranks (one GPU each) + RCCL gather "
                                 "to rank 0" if distributed else "one whole-frame call per step on one GPU")

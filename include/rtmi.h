@@ -220,6 +220,13 @@ typedef struct rt_options {
  * another: measured faster on the scenes here, whose reflected rays stay
  * coherent within a wave (DESIGN.md "Reflection-ray compaction"). */
 #define RT_FLAG_COMPACT 0x2000u
+/* float64 (parity) mode: render with one lane per pixel and the BVH for every
+ * ray the pixel records do not rule out. By default akGrid frames of >= 64
+ * samples per pixel render one pixel per wave (64 samples side by side; the
+ * camera rays search the pixel's face list and the shadow rays to distant
+ * lights their light-grid cells), each pixel's samples still summed in sample
+ * order. The image and Stats are the same, bit for bit. */
+#define RT_FLAG_F64_PER_LANE 0x4000u
 
 /* Stats (src/renderer/stats.nim:4-13) plus ray counts for Mray/s. */
 typedef struct rt_stats {

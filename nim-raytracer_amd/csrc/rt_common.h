@@ -148,6 +148,17 @@ struct RenderParams {
   // skips its traversal for them, and for the shadow rays of the lights
   // whose skip bit is set (the camera level only)
   const uint32_t* pix_info;
+  // k_render_px64 (one pixel per wave, float64): this call's camera-ray
+  // face lists (rt_frame.h slots: min(n, 2^slot_lg) TriFast byte offsets
+  // per pixel, n in pix_info; a TriFast offset o is TriF64 record
+  // o / 64 - tri_rec0) and the scene's light grids (rt_bins.h), or nullptr:
+  // the BVH serves those rays
+  const int32_t* pix_slots;
+  int32_t slot_lg;
+  int32_t tri_rec0;
+  const struct LightGrid* grids;
+  const int32_t* grid_off;
+  const int32_t* grid_ent;
 };
 
 // ---- float32 performance-kernel records (rt_fast.h) -------------------------
@@ -311,7 +322,9 @@ int rtmi_launch_render_f32(const rtmi::FastParams* p, unsigned subset, int block
 int rtmi_launch_wave_f32(const rtmi::FastParams* p, unsigned subset, int blocks, size_t shmem, void* stream);
 int rtmi_wave_f32_blocks_per_cu(unsigned subset, size_t shmem);
 int rtmi_launch_sec_add(float* fb, const long long* sec, size_t n, float scale, int num_cus, void* stream);
-int rtmi_launch_render_f64(const rtmi::RenderParams<double>* p, int blocks, void* stream);
+int rtmi_launch_render_f64(const rtmi::RenderParams<double>* p, int blocks, int px64, void* stream);
+int rtmi_px64_blocks_per_cu(int px64);
+int rtmi_px64_batch();
 int rtmi_render_f32_blocks_per_cu(int count, unsigned subset, size_t shmem);
 int rtmi_launch_lean_f32(const rtmi::FastParams* p, unsigned subset, int blocks, size_t shmem, void* stream);
 int rtmi_lean_f32_blocks_per_cu(unsigned subset, size_t shmem);

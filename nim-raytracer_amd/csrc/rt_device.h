@@ -39,6 +39,17 @@ __device__ __forceinline__ const RT_CONST T* cptr(const T* p) {
   return (const RT_CONST T*)(p);
 }
 
+// Kernel parameters read through a laundered pointer into the kernarg
+// segment (as rt_fast.h params()): each field is re-read with a scalar load
+// near its use instead of being pinned in SGPRs for the whole kernel (the
+// pinned float64 camera matrix and bases spilled ~150 SGPRs into VGPR lanes).
+template <class R>
+__device__ __forceinline__ const RT_CONST RenderParams<R>& rparams() {
+  const RT_CONST RenderParams<R>* q = (const RT_CONST RenderParams<R>*)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(q));
+  return *q;
+}
+
 template <class R> struct Prec;
 template <> struct Prec<float> {
   static constexpr bool exact = false;
@@ -259,7 +270,7 @@ __device__ __forceinline__ void slab2(const RT_CONST BvhNode& nd, V3<R> o, V3<R>
 }
 
 template <class R, bool COUNT>
-__device__ __forceinline__ void leaf(const RenderParams<R>& p, int first, int count, bool h,
+__device__ __forceinline__ void leaf(const RT_CONST RenderParams<R>& p, int first, int count, bool h,
                                      V3<R> o, V3<R> d, R& tbest, int& best_id, bool& active,
                                      bool early, R stop, WaveStats& ws) {
   using Tri = typename TriOf<R>::type;
@@ -282,7 +293,7 @@ __device__ __forceinline__ void leaf(const RenderParams<R>& p, int first, int co
 }
 
 template <class R, bool COUNT>
-__device__ __forceinline__ void traverse(const RenderParams<R>& p, int root, V3<R> o, V3<R> d,
+__device__ __forceinline__ void traverse(const RT_CONST RenderParams<R>& p, int root, V3<R> o, V3<R> d,
                                          bool active, bool early, R stop, R& tbest, int& best_id,
                                          WaveStats& ws) {
   if (ballot(active) == 0ull || root < 0) return;
@@ -346,6 +357,75 @@ __device__ __forceinline__ void traverse(const RenderParams<R>& p, int root, V3<
   }
 }
 
+// ---- binned face lists (k_render_px64: one pixel per wave) ------------------
+// The faces at ent[0, n) — a pixel's camera-ray list or a light-grid cell,
+// each a TriFast byte offset (rt_frame.h / rt_bins.h) — against the lanes
+// with `act`, with the traversal's rules: a face replaces the best hit when
+// t >= 0 and (t, face) is below (tbest, best_id), so the result is the
+// lexicographic minimum over the listed faces whatever their order — and a
+// list holds every face a ray of its family can hit (the builders' float64
+// proof, tests/test_bins_cpu.py), so it equals geom.nim:339-358's loop over
+// all faces. early: the shadow early exit (a lane retires on a found hit at
+// t <= stop, as in leaf()).
+template <class R>
+__device__ __forceinline__ void list_tris(const RT_CONST RenderParams<R>& p, const int32_t* ent, int n, V3<R> o, V3<R> d,
+                                          bool act, bool early, R stop, R& tbest, int& best_id) {
+  using Tri = typename TriOf<R>::type;
+  for (int k = 0; k < n; ++k) {
+    const int off = cptr(ent)[k];
+    const RT_CONST Tri& tri = cptr(p.tris)[(off >> 6) - p.tri_rec0];
+    const R t = tri_ref<R>(tri, o, d);
+    const int id = tri.id;
+    const bool acc = act && t >= R(0) && (t < tbest || (t == tbest && id < best_id));
+    if (acc) {
+      tbest = t;
+      best_id = id;
+    }
+    if (early && (k & 3) == 3) {
+      act = act && !(best_id >= 0 && tbest <= stop);
+      if (ballot(act) == 0ull) break;
+    }
+  }
+}
+
+// The mesh's closest hit for the lanes `in` (past the AABB gate) of a
+// one-pixel wave: camera rays (pix >= 0) search the pixel's list unless it
+// outgrew its slots, shadow rays to a distant light with a grid search
+// their cells (every distinct cell of the wave in turn, each with its own
+// lanes); lanes without a list take the BVH.
+template <class R, bool COUNT>
+__device__ __forceinline__ void mesh_lists(const RT_CONST RenderParams<R>& p, int root, const ORay<R>& r, bool in, bool early,
+                                           R stop, int pix, unsigned pinfo, int light, R& tbest, int& best_id,
+                                           WaveStats& ws) {
+  if (pix >= 0 && p.pix_slots) {
+    const unsigned n = pinfo & kPixCount;
+    if (n <= (1u << p.slot_lg)) {
+      list_tris<R>(p, p.pix_slots + ((size_t)pix << p.slot_lg), (int)n, r.o, r.d, in, early, stop, tbest, best_id);
+      return;
+    }
+  } else if (light >= 0 && p.grids) {
+    const RT_CONST LightGrid& G = cptr(p.grids)[light];
+    if (G.gu > 0) {
+      const R gu = r.o.x * R(G.e1[0]) + r.o.y * R(G.e1[1]) + r.o.z * R(G.e1[2]);
+      const R gv = r.o.x * R(G.e2[0]) + r.o.y * R(G.e2[1]) + r.o.z * R(G.e2[2]);
+      const R fu = (gu - R(G.u0)) * R(G.inv_h), fv = (gv - R(G.v0)) * R(G.inv_h);
+      const bool safe = fmax(fmax(fabs(r.o.x), fabs(r.o.y)), fabs(r.o.z)) <= R(G.rmax);
+      const bool on = fu >= R(0) && fu < R(G.gu) && fv >= R(0) && fv < R(G.gv);
+      const int bin = safe && on ? G.off_base + (int)fv * G.gu + (int)fu : -1;
+      const bool nohit = safe && !on;  // off the grid: no listed face, so no face at all
+      unsigned long long todo = ballot(in && bin >= 0);
+      while (todo) {
+        const int kb = __builtin_amdgcn_readlane(bin, (int)__builtin_ctzll(todo));
+        todo &= ~ballot(bin == kb);
+        const int b = cptr(p.grid_off)[kb], e = cptr(p.grid_off)[kb + 1];
+        list_tris<R>(p, p.grid_ent + G.ent_base + b, e - b, r.o, r.d, in && bin == kb, early, stop, tbest, best_id);
+      }
+      in = in && bin < 0 && !nohit;
+    }
+  }
+  traverse<R, COUNT>(p, root, r.o, r.d, in, early, stop, tbest, best_id, ws);
+}
+
 // ---- trace (renderer.nim:47-67) --------------------------------------------
 template <class R>
 struct Hit {
@@ -398,9 +478,14 @@ __device__ __forceinline__ R analytic_t(const RT_CONST DevObject<R>& ob, int typ
 // if its t beats the mesh's closest t. Once a lane holds a mesh hit at
 // t <= stop = min t (>= 0) over the analytic objects after the mesh, every
 // later comparison is decided, so the lane stops searching for a closer face.
-template <class R, bool COUNT>
-__device__ __forceinline__ Hit<R> trace(const RenderParams<R>& p, V3<R> o, V3<R> d, R t_near,
-                                        bool active, bool shadow, WaveStats& ws, bool no_mesh = false) {
+// LISTS (k_render_px64): the mesh's faces come from the binned lists
+// (mesh_lists; pix: the camera ray's pixel, -1 otherwise; light: the shadow
+// ray's light, -1 otherwise), and a mesh that no_mesh rules out is skipped
+// before its gate (it could only answer "miss": t = -inf or +inf, no update).
+template <class R, bool COUNT, bool LISTS = false>
+__device__ __forceinline__ Hit<R> trace(const RT_CONST RenderParams<R>& p, V3<R> o, V3<R> d, R t_near,
+                                        bool active, bool shadow, WaveStats& ws, bool no_mesh = false,
+                                        int pix = -1, unsigned pinfo = kPixCount, int light = -1) {
   Hit<R> h{-1, -1, t_near};
   ws.v[STAT_TESTS] += popc32(ballot(active)) * (unsigned int)p.nobj;
   const bool early = shadow && p.shadow_mesh >= 0;
@@ -430,6 +515,8 @@ __device__ __forceinline__ Hit<R> trace(const RenderParams<R>& p, V3<R> o, V3<R>
     int tri = -1;
     if (type != GEOM_MESH) {
       t = analytic_t<R>(ob, type, r);
+    } else if (LISTS && no_mesh) {
+      t = -pinf<R>();
     } else {
       r.inv = V3<R>{Prec<R>::rcp(rd.x), Prec<R>::rcp(rd.y), Prec<R>::rcp(rd.z)};
       const RT_CONST DevMesh<R>& m = cptr(p.meshes)[ob.mesh];
@@ -441,7 +528,12 @@ __device__ __forceinline__ Hit<R> trace(const RenderParams<R>& p, V3<R> o, V3<R>
       const bool in = active && gate >= R(0) && !no_mesh;
       R tb = h.t;
       int best = -1;
-      traverse<R, COUNT>(p, m.root, r.o, r.d, in, early && i == p.shadow_mesh, stop, tb, best, ws);
+      if constexpr (LISTS) {
+        if (ballot(in) != 0ull && m.root >= 0)
+          mesh_lists<R, COUNT>(p, m.root, r, in, early && i == p.shadow_mesh, stop, pix, pinfo, light, tb, best, ws);
+      } else {
+        traverse<R, COUNT>(p, m.root, r.o, r.d, in, early && i == p.shadow_mesh, stop, tb, best, ws);
+      }
       t = !(gate >= R(0)) ? -pinf<R>() : (best >= 0 ? tb : pinf<R>());
       tri = best;
     }
@@ -490,9 +582,12 @@ __device__ __forceinline__ V3<R> object_normal(const RT_CONST DevObject<R>& ob, 
 
 // One camera sample: trace + shade with the reflection recursion unrolled
 // into a loop of levels. Returns the sample colour (renderer.nim:71-127).
-template <class R, bool COUNT>
-__device__ __forceinline__ V3<R> shade_path(const RenderParams<R>& p, V3<R> o, V3<R> d, bool active,
-                                            WaveStats& ws, unsigned pinfo = kPixCount) {
+// LEVELS: the reflection levels compiled in (1: a scene without reflective
+// materials — no level can follow the camera hit; shade's recursion needs
+// depth <= maxRayDepth AND reflection > 0, renderer.nim:104).
+template <class R, bool COUNT, bool LISTS = false, int LEVELS = kMaxShadeLevels>
+__device__ __forceinline__ V3<R> shade_path(const RT_CONST RenderParams<R>& p, V3<R> o, V3<R> d, bool active,
+                                            WaveStats& ws, unsigned pinfo = kPixCount, int pix = -1) {
   constexpr R kPi = R(3.14159265358979323846);
   bool act = active;
   int depth = 1;
@@ -501,15 +596,16 @@ __device__ __forceinline__ V3<R> shade_path(const RenderParams<R>& p, V3<R> o, V
   // (1 - r)*L + r*inner folded from the innermost level outwards.
   V3<R> facc{R(0), R(0), R(0)};
   R fw = R(1);
-  V3<R> lvl_c[Prec<R>::exact ? kMaxShadeLevels : 1];
-  R lvl_r[Prec<R>::exact ? kMaxShadeLevels : 1];
+  constexpr int kLv = LEVELS > 1 ? LEVELS : 1;
+  V3<R> lvl_c[Prec<R>::exact ? kLv : 1];
+  R lvl_r[Prec<R>::exact ? kLv : 1];
   int nlev = 0;
-  for (int lev = 0; lev < kMaxShadeLevels; ++lev) {
+  for (int lev = 0; lev < LEVELS; ++lev) {
     if (ballot(act) == 0ull) break;
     // the pixel's record (camera level only): an empty camera-ray list, and
     // per distant light a skip bit for the shadow rays from its camera hits
     const bool cam_skip = lev == 0 && (pinfo & kPixCount) == 0u;
-    const Hit<R> hit = trace<R, COUNT>(p, o, d, pinf<R>(), act, false, ws, cam_skip);
+    const Hit<R> hit = trace<R, COUNT, LISTS>(p, o, d, pinf<R>(), act, false, ws, cam_skip, lev == 0 ? pix : -1, pinfo);
     if (act && hit.obj < 0) terminal = V3<R>{p.bg[0], p.bg[1], p.bg[2]};
     const bool lit = act && hit.obj >= 0;
     const V3<R> hw{o.x + d.x * hit.t, o.y + d.y * hit.t, o.z + d.z * hit.t};
@@ -572,7 +668,8 @@ __device__ __forceinline__ V3<R> shade_path(const RenderParams<R>& p, V3<R> o, V
       const V3<R> so{hw.x + N.x * p.bias, hw.y + N.y * p.bias, hw.z + N.z * p.bias};
       ws.v[STAT_SHADOW] += popc32(ballot(lit));
       const bool sh_skip = cam_skip && li < 8 && L.type != LIGHT_POINT && ((pinfo >> (24 + li)) & 1u) != 0u;
-      const Hit<R> sh = trace<R, COUNT>(p, so, sd, dist, lit, true, ws, sh_skip);
+      const Hit<R> sh = trace<R, COUNT, LISTS>(p, so, sd, dist, lit, true, ws, sh_skip, -1, kPixCount,
+                                               L.type == LIGHT_POINT ? -1 : li);
       if (lit && sh.obj < 0) {  // shadeDiffuse (shader.nim:12-17)
         const R ndl = nmax(R(0), dot4(N, R(0), sd, R(0) * R(-1)));
         local.x = local.x + Prec<R>::div(alb.x, kPi) * I.x * ndl;
@@ -586,7 +683,7 @@ __device__ __forceinline__ V3<R> shade_path(const RenderParams<R>& p, V3<R> o, V
       if (reflect) {
         // shift-register push (static indices keep it in registers)
 #pragma unroll
-        for (int k = kMaxShadeLevels - 1; k > 0; --k) {
+        for (int k = kLv - 1; k > 0; --k) {
           lvl_c[k] = lvl_c[k - 1];
           lvl_r[k] = lvl_r[k - 1];
         }
@@ -615,7 +712,7 @@ __device__ __forceinline__ V3<R> shade_path(const RenderParams<R>& p, V3<R> o, V
   if constexpr (Prec<R>::exact) {
     V3<R> c = terminal;
 #pragma unroll
-    for (int k = 0; k < kMaxShadeLevels; ++k) {
+    for (int k = 0; k < kLv; ++k) {
       if (k < nlev) {
         const R r = lvl_r[k];
         c = V3<R>{(R(1) - r) * lvl_c[k].x + r * c.x, (R(1) - r) * lvl_c[k].y + r * c.y,
@@ -645,7 +742,9 @@ __device__ __forceinline__ void flush_stats(WaveStats& ws, unsigned long long& t
 #define RTMI_MIN_WAVES 1
 #endif
 template <class R, bool COUNT>
-__global__ __launch_bounds__(256, RTMI_MIN_WAVES) void k_render(const RenderParams<R> p) {
+__global__ __launch_bounds__(256, RTMI_MIN_WAVES) void k_render(const RenderParams<R> params_by_value) {
+  (void)params_by_value;  // read through rparams()
+  const RT_CONST RenderParams<R>& p = rparams<R>();
   const int lane = (int)__lane_id();
   const long long wave = (long long)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   const long long nwaves = (long long)gridDim.x * (blockDim.x >> 6);
@@ -740,6 +839,134 @@ __global__ __launch_bounds__(256, RTMI_MIN_WAVES) void k_render(const RenderPara
       } else {
         float* q = p.fb + ((size_t)out_row * p.width + x) * 3;
         q[0] = cr; q[1] = cg; q[2] = cb;
+      }
+    }
+  }
+  if (lane < kStatSlots) p.partials[wave * kStatSlots + lane] = tot;
+}
+
+// ---- k_render_px64: float64, one pixel per wave -----------------------------
+// The parity mode's fast layout for akGrid with >= 64 samples per pixel: a
+// wave's 64 lanes trace 64 samples of ONE pixel (s = 64 it + lane), so every
+// ray of a step shares the pixel's camera-ray face list, and its shadow rays
+// a few light-grid cells (mesh_lists) — the same answers as the per-ray BVH,
+// in the reference's float64 arithmetic.
+//
+// calcPixel (renderer.nim:149-159) sums the samples in sample order; to keep
+// that sum bit for bit a wave renders P pixels at a time: step `it` of each
+// pixel j leaves its 64 sample colours in the wave's LDS row j, then lane j
+// adds row j's colours to pixel j's running sum in sample order (64
+// dependent adds, P chains side by side) before the next step overwrites
+// the rows. Rows are padded to 65 doubles so the summing lanes' reads fall
+// in different banks.
+#ifndef RTMI_PX64_WAVES
+#define RTMI_PX64_WAVES 3
+#endif
+template <int P, int LEVELS>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RTMI_PX64_WAVES))) void k_render_px64(const RenderParams<double> params_by_value) {
+  using R = double;
+  (void)params_by_value;  // read through rparams()
+  const RT_CONST RenderParams<R>& p = rparams<R>();
+  constexpr int kRow = 65;
+  __shared__ double sbuf[4][P * 3 * kRow];
+  const int lane = (int)__lane_id();
+  const int wib = (int)(threadIdx.x >> 6);
+  double* buf = sbuf[wib];
+  const long long wave = (long long)blockIdx.x * (blockDim.x >> 6) + wib;
+  const long long nwaves = (long long)gridDim.x * (blockDim.x >> 6);
+  const int iters = (p.spp + 63) / 64;
+  const long long npx = (long long)p.nrows * p.ncols;
+  const long long nbatch = (npx + P - 1) / P;
+  WaveStats ws;
+#pragma unroll
+  for (int k = 0; k < kStatSlots; ++k) ws.v[k] = 0u;
+  unsigned long long tot = 0ull;
+  // the camera origin (castPrimaryRay: cameraToWorld * (0, 0, 0, 1)) is the
+  // same for every sample
+  const V3<R> o = xform<R>(p.c2w, V3<R>{R(0), R(0), R(0)}, R(1));
+
+  // pixel g of the launch: image (x, y), its output row, whether it renders
+  auto pixel_of = [&](long long g, int& x, int& y, int& out_row) -> bool {
+    const int k = (int)(g / p.ncols), j = (int)(g % p.ncols);
+    x = j * p.step;
+    bool valid = g < npx;
+    if (p.mode == 0) {
+      y = p.y0 + k * p.step;
+      out_row = y;
+    } else {
+      const int lb = k / p.band_h, rr = k % p.band_h;
+      y = (lb * p.world + p.rank) * p.band_h + rr;
+      out_row = k;
+      valid = valid && y < p.height;
+    }
+    if (p.step < p.max_step) {  // progressive refinement skip (renderer.nim:175-178)
+      const int mask = p.step * 2 - 1;
+      if ((x & mask) == 0 && (y & mask) == 0) valid = false;
+    }
+    return valid;
+  };
+
+  for (long long b = wave; b < nbatch; b += nwaves) {
+    R ax = R(0), ay = R(0), az = R(0);  // lane j < P: pixel j's sum
+    for (int it = 0; it < iters; ++it) {
+      const int s = it * 64 + lane;
+      const bool sv = s < p.spp;
+      for (int j = 0; j < P; ++j) {
+        int x, y, out_row;
+        if (!pixel_of(b * P + j, x, y, out_row)) continue;
+        const int pix = y * p.width + x;
+        const unsigned pinfo = p.pix_info ? p.pix_info[pix] : kPixCount;
+        // grid() sampling.nim:5-18, p[j*m + i]; castPrimaryRay (renderer.nim:31-44)
+        const int si = s % p.grid_m, sj = s / p.grid_m;
+        const R px = R(x) + (R(si) * p.sample_step + p.sample_off);
+        const R py = R(y) + (R(sj) * p.sample_step + p.sample_off);
+        const R cx = (Prec<R>::div(R(2) * px * p.aspect, R(p.width)) - p.aspect) * p.f;
+        const R cy = (R(1) - Prec<R>::div(R(2) * py, R(p.height))) * p.f;
+        const V3<R> dn = normalize_dir<R>(V3<R>{cx, cy, R(-1)});
+        const V3<R> d = xform<R>(p.c2w, dn, R(0));
+        ws.v[STAT_PRIMARY] += popc32(ballot(sv));
+        const V3<R> c = shade_path<R, false, true, LEVELS>(rparams<R>(), o, d, sv, ws, pinfo, pix);
+        buf[(j * 3 + 0) * kRow + lane] = c.x;
+        buf[(j * 3 + 1) * kRow + lane] = c.y;
+        buf[(j * 3 + 2) * kRow + lane] = c.z;
+      }
+      // the rows are read by other lanes of this wave: LDS operations of one
+      // wave complete in order, the barrier keeps the compiler from moving
+      // the reads above the writes
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      if (lane < P) {
+        const int nv = min(64, p.spp - it * 64);
+        const double* rx = buf + (lane * 3 + 0) * kRow;
+        const double* ry = buf + (lane * 3 + 1) * kRow;
+        const double* rz = buf + (lane * 3 + 2) * kRow;
+        for (int k = 0; k < nv; ++k) {
+          ax = ax + rx[k];
+          ay = ay + ry[k];
+          az = az + rz[k];
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    flush_stats(ws, tot, lane);
+    if (lane < P) {
+      int x, y, out_row;
+      if (pixel_of(b * P + lane, x, y, out_row)) {
+        const float cr = (float)(ax * p.inv_len), cg = (float)(ay * p.inv_len), cb = (float)(az * p.inv_len);
+        if (p.mode == 0 && p.step > 1) {
+          const int xe = min(x + p.step, p.width), ye = min(y + p.step, p.height);
+          for (int yy = y; yy < ye; ++yy)
+            for (int xx = x; xx < xe; ++xx) {
+              float* q = p.fb + ((size_t)yy * p.width + xx) * 3;
+              q[0] = cr; q[1] = cg; q[2] = cb;
+            }
+        } else {
+          float* q = p.fb + ((size_t)out_row * p.width + x) * 3;
+          q[0] = cr; q[1] = cg; q[2] = cb;
+        }
       }
     }
   }

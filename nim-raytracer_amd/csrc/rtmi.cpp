@@ -1802,7 +1802,6 @@ int launch(rt_scene* s, const rt_options* o, const Mapping& mp, float* d_out, hi
     if (int rc = clear()) return rc;
     RenderParams<double> p;
     fill_params<double>(s, s->f64, o, mp, d_out, p, &blocks);
-    if (o->flags & RT_FLAG_TIMING) HIP_TRY(hipEventRecord(s->tev[1], st));
     s->last_general = p.ngroups;
     if (p.ngroups == 0) return RT_OK;
     if (p.aa_kind >= RT_AA_JITTERED) {
@@ -1823,14 +1822,38 @@ int launch(rt_scene* s, const rt_options* o, const Mapping& mp, float* d_out, hi
     // and its shadow rays to the lights its skip bits clear skip theirs —
     // the same answers (the traversal would find no face), so frames and
     // Stats stay bit-exact (tests/test_gpu_parity.py)
-    if (!(o->flags & (RT_FLAG_NO_BINNING | RT_FLAG_COUNT_TRAVERSAL)) && sampler_in_pixel(o->aa_kind) && s->skippable) {
+    const bool binning = !(o->flags & (RT_FLAG_NO_BINNING | RT_FLAG_COUNT_TRAVERSAL));
+    bool lists = false;
+    if (binning && sampler_in_pixel(o->aa_kind) && s->skippable) {
       FastParams pf;
       std::memset(&pf, 0, sizeof pf);
-      bool lists = false, zeroed = false;
+      bool zeroed = false;
       if (int rc = frame_build(s, o, mp, pf, true, false, nullptr, 0, st, &lists, &zeroed)) return rc;
       if (lists) p.pix_info = s->fr.info.p;
     }
-    const int e = rtmi_launch_render_f64(&p, blocks, st);
+    // one pixel per wave (k_render_px64): akGrid with >= 64 samples per
+    // pixel; the camera rays search this call's pixel lists, the shadow rays
+    // to distant lights the scene's light grids (rt_device.h mesh_lists)
+    const int px64 = o->aa_kind == RT_AA_GRID && p.spp >= 64 && !(o->flags & (RT_FLAG_F64_PER_LANE | RT_FLAG_COUNT_TRAVERSAL))
+                         ? (s->any_reflective && o->max_ray_depth >= 1 ? 2 : 1)
+                         : 0;
+    if (px64) {
+      if (lists) {
+        p.pix_slots = s->fr.slots.p;
+        p.slot_lg = s->fr.slot_lg;
+      }
+      if (binning && s->has_grids) {
+        p.grids = s->grids.p;
+        p.grid_off = s->grid_off.p;
+        p.grid_ent = s->grid_ent.p;
+      }
+      p.tri_rec0 = (int32_t)s->num_nodes;
+      const long long nbatch = ((long long)mp.nrows * mp.ncols + rtmi_px64_batch() - 1) / rtmi_px64_batch();
+      const long long resident = (long long)std::max(1, rtmi_px64_blocks_per_cu(px64)) * s->num_cus;
+      blocks = (int)std::max(1LL, std::min({(nbatch + 3) / 4, resident, (long long)s->max_waves / 4}));
+    }
+    if (o->flags & RT_FLAG_TIMING) HIP_TRY(hipEventRecord(s->tev[1], st));  // after the per-call build
+    const int e = rtmi_launch_render_f64(&p, blocks, px64, st);
     if (e) return fail(RT_E_DEVICE, "render kernel launch failed: %s", hipGetErrorString((hipError_t)e));
   } else {
     FastParams p;

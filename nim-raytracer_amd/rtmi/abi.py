@@ -32,6 +32,7 @@ RT_FLAG_NO_MIX = 0x400
 RT_FLAG_TIMING = 0x800
 RT_FLAG_NO_OBJ_BATCH = 0x1000
 RT_FLAG_COMPACT = 0x2000
+RT_FLAG_F64_PER_LANE = 0x4000
 RT_BVH_SAH = 0
 RT_OBJ_SLASH_INDICES = 0x1
 RT_BVH_PLOC = 1

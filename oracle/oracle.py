@@ -139,7 +139,8 @@ class OracleScene:
         o = opts.to_c()
         st = abi.rt_stats()
         secs = C.c_double(0.0)
-        nthreads = nthreads or os.cpu_count() or 1
+        # the GPU box's CPU share is 16 threads (os.cpu_count() there is the whole machine's)
+        nthreads = nthreads or min(16, os.cpu_count() or 1)
         rc = lib().oracle_render_rows_mt(self.h, C.byref(o), fb.ctypes.data_as(C.POINTER(C.c_float)),
                                          rows_a.ctypes.data_as(C.POINTER(C.c_int32)), len(rows_a),
                                          step, maxStep, nthreads, C.byref(st), C.byref(secs))

@@ -20,8 +20,9 @@ import sys
 
 # the render call's kernels (a regex on the kernel name): the render kernels
 # and the per-call camera-dependent builders (rt_frame.hip)
-KERNEL = r"k_render_fast<false|k_render_lean|k_render_gen|k_render_mix1|k_frame_"
-RENDER = re.compile(r"k_render_fast<false|k_render_lean|k_render_gen|k_render_mix1")
+RENDER_RE = r"k_render_fast<false|k_render_lean|k_render_gen|k_render_mix1|k_render<double, false|k_render_px64"
+KERNEL = RENDER_RE + r"|k_frame_"
+RENDER = re.compile(RENDER_RE)
 
 
 def means(path, kernel=None):
