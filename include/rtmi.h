@@ -252,7 +252,7 @@ typedef struct rt_scene_info {
   int64_t num_bvh_nodes;       /* all meshes                             */
   int32_t max_bvh_depth;
   int32_t device;
-  int64_t device_bytes;        /* resident scene bytes in HBM            */
+  int64_t device_bytes;        /* scene bytes in HBM: geometry, BVH, bins and the per-call buffer sets */
   double build_ms;             /* host BVH build + upload wall time      */
 } rt_scene_info;
 
@@ -283,6 +283,10 @@ int rt_device_count(void);
 /* Flatten, build the per-mesh BVH and upload everything to the current
  * device. desc and all arrays it points to may be freed after return. */
 int rt_scene_create(const rt_scene_desc *desc, rt_scene **out_scene);
+/* Waits for a call still running on the scene in another thread, then frees
+ * it. No call may START on a scene once its destroy has begun (the caller's
+ * own bookkeeping: INTEGRATION.md's binding retires a replaced scene only
+ * after its in-flight renderLine calls have returned). */
 int rt_scene_destroy(rt_scene *scene);
 int rt_scene_get_info(const rt_scene *scene, rt_scene_info *out);
 
@@ -307,11 +311,9 @@ int rt_scene_set_camera(rt_scene *scene, const double camera_to_world[16],
  * step and max_step must be powers of two with max_step >= step.
  * `out` receives the summed Stats of the call (may be NULL for the _device
  * forms, which then do not synchronise the stream).
- * A call whose per-call camera-ray lists ran out of entry capacity (never
- * expected: the capacity is sized from the device count) rendered an
- * incomplete frame: the call that reads Stats (this one, or the next one
- * that does when `out` is NULL) returns RT_E_DEVICE instead of RT_OK, and
- * the next call rebuilds its buffers.
+ * The per-call camera-dependent build has no capacity failure: a pixel
+ * whose face list outgrows its slots keeps its true length and its camera
+ * rays take the BVH (the same answers).
  */
 
 /* Host framebuffer form: fb_rgb is caller memory of fb_w*fb_h*3 floats with

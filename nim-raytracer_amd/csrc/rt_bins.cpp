@@ -331,7 +331,7 @@ bool build_light_grid(const std::vector<BinTri>& tris, const double w2o[16], con
   // 16 / 32 -> 4.91 / 4.89 / 4.92 / 4.96 / 5.09 / 5.76 ms (fewer distinct
   // cells per wave, fewer lanes left to the BVH, more record reuse)
   static const double density = [] {
-    const char* e = std::getenv("RTMI_GRID_DENSITY");
+    const char* e = rtmi::diag_env("RTMI_GRID_DENSITY");
     const double v = e ? std::atof(e) : 2.0;
     return v > 0.0 ? v : 2.0;
   }();

@@ -522,7 +522,7 @@ bool build_bvh_device(const double* d_vin, const int32_t* d_fin, int64_t nf, con
   // search radius: 16 (8 and 32 traced no faster: C3 8.53 / 8.57 ms vs
   // 8.24, 1M-face torus 3.84 / 3.94 vs 3.84); RTMI_PLOC_RADIUS overrides
   static const int radius = [] {
-    const char* e = std::getenv("RTMI_PLOC_RADIUS");
+    const char* e = rtmi::diag_env("RTMI_PLOC_RADIUS");
     return e ? std::max(1, std::min(kRadius, std::atoi(e))) : 16;
   }();
   // 3. PLOC rounds: every round merges at least the globally closest pair

@@ -13,8 +13,22 @@
 //                                 (obj.nim calcNormals), looked up by face id
 #pragma once
 #include <stdint.h>
+#include <stdlib.h>
 
 namespace rtmi {
+
+// Diagnostic and A/B knobs (RTMI_* environment variables: launch shapes,
+// occupancy caps, probe modes that give wrong images on purpose) are read
+// only by libraries built with -DRTMI_DIAG (tools/build_variant.sh); the
+// production library ignores them.
+inline const char* diag_env(const char* name) {
+#ifdef RTMI_DIAG
+  return getenv(name);
+#else
+  (void)name;
+  return nullptr;
+#endif
+}
 
 enum : int32_t { GEOM_SPHERE = 0, GEOM_PLANE = 1, GEOM_BOX = 2, GEOM_MESH = 3 };
 enum : int32_t { LIGHT_DISTANT = 0, LIGHT_POINT = 1 };

@@ -469,6 +469,18 @@ __device__ __forceinline__ R analytic_t(const RT_CONST DevObject<R>& ob, int typ
   return -pinf<R>();
 }
 
+// Per-block LDS cache of k_render_px64 (scenes of <= kCacheObj objects and
+// <= kCacheLight lights): the values every sample of the frame would compute
+// the same way — each object's view of the camera origin, each distant
+// light's shadow direction in each object's space (and its reciprocals), each
+// plane's world normal — formed once per block with the same operations, so
+// the same bits.
+constexpr int kCacheObj = 16, kCacheLight = 8;
+constexpr int kCacheCamO = 0;                                 // [obj][4]: w2o * (camera origin, 1)
+constexpr int kCacheLightD = kCacheCamO + 4 * kCacheObj;      // [light][obj][8]: w2o * (-ldir, 0), 1 / that
+constexpr int kCachePlaneN = kCacheLightD + 8 * kCacheObj * kCacheLight;  // [obj][4]: o2w * (0, 1, 0, 0)
+constexpr int kCacheDoubles = kCachePlaneN + 4 * kCacheObj;
+
 // Linear closest hit over the scene's objects in order, for lanes with
 // `active`; tmin starts at t_near. Wave-uniform control flow only.
 //
@@ -482,43 +494,80 @@ __device__ __forceinline__ R analytic_t(const RT_CONST DevObject<R>& ob, int typ
 // (mesh_lists; pix: the camera ray's pixel, -1 otherwise; light: the shadow
 // ray's light, -1 otherwise), and a mesh that no_mesh rules out is skipped
 // before its gate (it could only answer "miss": t = -inf or +inf, no update).
+// cache (LISTS, or nullptr): kCache* above; cam0: o is the camera origin
+// (a camera ray); light >= 0 with the cache: d is that distant light's
+// shadow direction.
 template <class R, bool COUNT, bool LISTS = false>
 __device__ __forceinline__ Hit<R> trace(const RT_CONST RenderParams<R>& p, V3<R> o, V3<R> d, R t_near,
                                         bool active, bool shadow, WaveStats& ws, bool no_mesh = false,
-                                        int pix = -1, unsigned pinfo = kPixCount, int light = -1) {
+                                        int pix = -1, unsigned pinfo = kPixCount, int light = -1,
+                                        const R* cache = nullptr, bool cam0 = false) {
   Hit<R> h{-1, -1, t_near};
   ws.v[STAT_TESTS] += popc32(ballot(active)) * (unsigned int)p.nobj;
   const bool early = shadow && p.shadow_mesh >= 0;
+  const bool cached_o = LISTS && cache && cam0;
+  const bool cached_d = LISTS && cache && light >= 0;
+  // object i's view of the ray (to_object), from the cache where it holds it
+  auto obj_ray = [&](int i, const RT_CONST DevObject<R>& ob, ORay<R>& r) {
+    if (cached_o) {
+      const R* c = cache + kCacheCamO + 4 * i;
+      r.o = V3<R>{c[0], c[1], c[2]};
+    } else {
+      r.o = xform<R>(ob.w2o, o, R(1));
+    }
+    if (cached_d) {
+      const R* c = cache + kCacheLightD + 8 * (light * kCacheObj + i);
+      r.d = V3<R>{c[0], c[1], c[2]};
+      r.inv = V3<R>{c[4], c[5], c[6]};
+    } else {
+      r.d = xform<R>(ob.w2o, d, R(0));
+    }
+  };
   R stop = -pinf<R>();
+  R t_next = R(0);  // LISTS: the t of the object right after the mesh (the same t the main loop would form)
   if (early) {
     stop = pinf<R>();
     for (int i = p.shadow_mesh + 1; i < p.nobj; ++i) {
       const RT_CONST DevObject<R>& ob = cptr(p.objects)[i];
-      V3<R> ro, rd;
-      to_object<R>(ob, o, d, ro, rd);
       ORay<R> r;
-      r.o = ro;
-      r.d = rd;
+      if constexpr (LISTS) {
+        obj_ray(i, ob, r);
+      } else {
+        to_object<R>(ob, o, d, r.o, r.d);
+      }
       const R t = analytic_t<R>(ob, ob.type, r);
+      if (LISTS && i == p.shadow_mesh + 1) t_next = t;
       if (t >= R(0) && t < stop) stop = t;
     }
   }
   for (int i = 0; i < p.nobj; ++i) {
     const RT_CONST DevObject<R>& ob = cptr(p.objects)[i];
     const int type = ob.type;
-    V3<R> ro, rd;
-    to_object<R>(ob, o, d, ro, rd);
     ORay<R> r;
-    r.o = ro;
-    r.d = rd;
     R t;
     int tri = -1;
-    if (type != GEOM_MESH) {
-      t = analytic_t<R>(ob, type, r);
-    } else if (LISTS && no_mesh) {
+    if (LISTS && early && i == p.shadow_mesh + 1) {
+      t = t_next;
+    } else if (LISTS && type == GEOM_MESH && no_mesh) {
       t = -pinf<R>();
+    } else if (type != GEOM_MESH) {
+      if constexpr (LISTS) {
+        obj_ray(i, ob, r);
+      } else {
+        to_object<R>(ob, o, d, r.o, r.d);
+      }
+      t = analytic_t<R>(ob, type, r);
     } else {
-      r.inv = V3<R>{Prec<R>::rcp(rd.x), Prec<R>::rcp(rd.y), Prec<R>::rcp(rd.z)};
+      V3<R> rd;
+      if constexpr (LISTS) {
+        obj_ray(i, ob, r);
+        rd = r.d;
+        if (!cached_d) r.inv = V3<R>{Prec<R>::rcp(rd.x), Prec<R>::rcp(rd.y), Prec<R>::rcp(rd.z)};
+      } else {
+        to_object<R>(ob, o, d, r.o, rd);
+        r.d = rd;
+        r.inv = V3<R>{Prec<R>::rcp(rd.x), Prec<R>::rcp(rd.y), Prec<R>::rcp(rd.z)};
+      }
       const RT_CONST DevMesh<R>& m = cptr(p.meshes)[ob.mesh];
       // TriangleMesh.intersect (geom.nim:339-358): AABB gate (tmin < 0 ->
       // miss, so rays starting inside the box miss), then closest face.
@@ -587,7 +636,8 @@ __device__ __forceinline__ V3<R> object_normal(const RT_CONST DevObject<R>& ob, 
 // depth <= maxRayDepth AND reflection > 0, renderer.nim:104).
 template <class R, bool COUNT, bool LISTS = false, int LEVELS = kMaxShadeLevels>
 __device__ __forceinline__ V3<R> shade_path(const RT_CONST RenderParams<R>& p, V3<R> o, V3<R> d, bool active,
-                                            WaveStats& ws, unsigned pinfo = kPixCount, int pix = -1) {
+                                            WaveStats& ws, unsigned pinfo = kPixCount, int pix = -1,
+                                            const R* cache = nullptr) {
   constexpr R kPi = R(3.14159265358979323846);
   bool act = active;
   int depth = 1;
@@ -605,7 +655,8 @@ __device__ __forceinline__ V3<R> shade_path(const RT_CONST RenderParams<R>& p, V
     // the pixel's record (camera level only): an empty camera-ray list, and
     // per distant light a skip bit for the shadow rays from its camera hits
     const bool cam_skip = lev == 0 && (pinfo & kPixCount) == 0u;
-    const Hit<R> hit = trace<R, COUNT, LISTS>(p, o, d, pinf<R>(), act, false, ws, cam_skip, lev == 0 ? pix : -1, pinfo);
+    const Hit<R> hit = trace<R, COUNT, LISTS>(p, o, d, pinf<R>(), act, false, ws, cam_skip, lev == 0 ? pix : -1, pinfo,
+                                              -1, cache, lev == 0);
     if (act && hit.obj < 0) terminal = V3<R>{p.bg[0], p.bg[1], p.bg[2]};
     const bool lit = act && hit.obj >= 0;
     const V3<R> hw{o.x + d.x * hit.t, o.y + d.y * hit.t, o.z + d.z * hit.t};
@@ -624,6 +675,14 @@ __device__ __forceinline__ V3<R> shade_path(const RT_CONST RenderParams<R>& p, V
       const RT_CONST DevObject<R>& ob = cptr(p.objects)[oi];
       if (mine) {
         V3<R> nrm;
+        if (LISTS && cache && hit.tri < 0 && ob.type == GEOM_PLANE) {
+          // a plane's normal does not depend on the hit point: its cached N
+          const R* c = cache + kCachePlaneN + 4 * oi;
+          N = V3<R>{c[0], c[1], c[2]};
+          alb = V3<R>{ob.albedo[0], ob.albedo[1], ob.albedo[2]};
+          refl = ob.albedo[3];
+          continue;
+        }
         if (hit.tri >= 0) {
           const R* fn = p.normals + 3 * (size_t)(cptr(p.meshes)[ob.mesh].normal_base + hit.tri);
           nrm = V3<R>{fn[0], fn[1], fn[2]};
@@ -669,7 +728,7 @@ __device__ __forceinline__ V3<R> shade_path(const RT_CONST RenderParams<R>& p, V
       ws.v[STAT_SHADOW] += popc32(ballot(lit));
       const bool sh_skip = cam_skip && li < 8 && L.type != LIGHT_POINT && ((pinfo >> (24 + li)) & 1u) != 0u;
       const Hit<R> sh = trace<R, COUNT, LISTS>(p, so, sd, dist, lit, true, ws, sh_skip, -1, kPixCount,
-                                               L.type == LIGHT_POINT ? -1 : li);
+                                               L.type == LIGHT_POINT ? -1 : li, li < kCacheLight ? cache : nullptr);
       if (lit && sh.obj < 0) {  // shadeDiffuse (shader.nim:12-17)
         const R ndl = nmax(R(0), dot4(N, R(0), sd, R(0) * R(-1)));
         local.x = local.x + Prec<R>::div(alb.x, kPi) * I.x * ndl;
@@ -884,6 +943,36 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RTMI_PX64_W
   // the camera origin (castPrimaryRay: cameraToWorld * (0, 0, 0, 1)) is the
   // same for every sample
   const V3<R> o = xform<R>(p.c2w, V3<R>{R(0), R(0), R(0)}, R(1));
+  // the block's cache (kCache*): per object its view of the camera origin and,
+  // for a plane, its world normal; per distant light the shadow direction in
+  // each object's space and its reciprocals — the very operations trace() and
+  // shade_path() would apply per sample
+  __shared__ double cache[kCacheDoubles];
+  const bool use_cache = p.nobj <= kCacheObj && p.nlight <= kCacheLight;
+  if (use_cache) {
+    const int nobj = p.nobj;
+    for (int t = (int)threadIdx.x; t < nobj * (1 + p.nlight); t += (int)blockDim.x) {
+      const int i = t % nobj, l = t / nobj - 1;
+      const RT_CONST DevObject<R>& ob = cptr(p.objects)[i];
+      if (l < 0) {
+        const V3<R> ro = xform<R>(ob.w2o, o, R(1));
+        double* c = cache + kCacheCamO + 4 * i;
+        c[0] = ro.x; c[1] = ro.y; c[2] = ro.z;
+        const V3<R> n = xform<R>(ob.o2w, V3<R>{R(0), R(1), R(0)}, R(0));  // geom.nim:367-368, renderer.nim:88
+        double* cn = cache + kCachePlaneN + 4 * i;
+        cn[0] = n.x; cn[1] = n.y; cn[2] = n.z;
+      } else {
+        const RT_CONST DevLight<R>& L = cptr(p.lights)[l];
+        const V3<R> sd{R(L.v[0]) * R(-1), R(L.v[1]) * R(-1), R(L.v[2]) * R(-1)};  // shade: -lightDir
+        const V3<R> rd = xform<R>(ob.w2o, sd, R(0));
+        double* c = cache + kCacheLightD + 8 * (l * kCacheObj + i);
+        c[0] = rd.x; c[1] = rd.y; c[2] = rd.z;
+        c[4] = Prec<R>::rcp(rd.x); c[5] = Prec<R>::rcp(rd.y); c[6] = Prec<R>::rcp(rd.z);
+      }
+    }
+    __syncthreads();
+  }
+  const double* cch = use_cache ? cache : nullptr;
 
   // pixel g of the launch: image (x, y), its output row, whether it renders
   auto pixel_of = [&](long long g, int& x, int& y, int& out_row) -> bool {
@@ -925,7 +1014,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RTMI_PX64_W
         const V3<R> dn = normalize_dir<R>(V3<R>{cx, cy, R(-1)});
         const V3<R> d = xform<R>(p.c2w, dn, R(0));
         ws.v[STAT_PRIMARY] += popc32(ballot(sv));
-        const V3<R> c = shade_path<R, false, true, LEVELS>(rparams<R>(), o, d, sv, ws, pinfo, pix);
+        const V3<R> c = shade_path<R, false, true, LEVELS>(rparams<R>(), o, d, sv, ws, pinfo, pix, cch);
         buf[(j * 3 + 0) * kRow + lane] = c.x;
         buf[(j * 3 + 1) * kRow + lane] = c.y;
         buf[(j * 3 + 2) * kRow + lane] = c.z;

@@ -101,10 +101,10 @@ struct DevBinTri {
 // frame counters (one small device array). FC_HUGE0 / FC_HUGE1: the huge-face
 // list's length of calls of even / odd parity (k_frame_build1 appends to its
 // call's word and zeroes the other one, which the next call uses).
-// FC_OVERFLOW: reserved for a build that could not complete (none can now:
-// a list past its slots takes the BVH); reported by the host
-// (rtmi.cpp report_overflow).
-enum : int32_t { FC_OVERFLOW = 0, FC_HEAVY = 1, FC_LEAN = 2, FC_HUGE0 = 3, FC_HUGE1 = 4, FC_WORDS = 8 };
+// Word 0 is unused: the build has no failure mode (a list past its slots
+// keeps its true length and the render kernels take the BVH for that pixel;
+// huge faces past kHugeCap are walked by their blocks).
+enum : int32_t { FC_RESERVED = 0, FC_HEAVY = 1, FC_LEAN = 2, FC_HUGE0 = 3, FC_HUGE1 = 4, FC_WORDS = 8 };
 
 // Faces whose pixel rectangle holds more than kBigFace pixels are not walked
 // by k_frame_build1's blocks (a few large faces, e.g. a 576-face torus

@@ -463,7 +463,7 @@ extern "C" int rtmi_frame_build(const rtmi::FrameLaunch* a, void* stream) {
   hipLaunchKernelGGL(k_frame_build1, dim3(face_blocks + tile_blocks), dim3(256), 0, st, *a, face_blocks);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || a->ntiles <= 0) return (int)e;
-  static const int b2w = std::getenv("RTMI_B2_WAVES") ? std::atoi(std::getenv("RTMI_B2_WAVES")) : 4;  // diagnostic
+  static const int b2w = rtmi::diag_env("RTMI_B2_WAVES") ? std::atoi(rtmi::diag_env("RTMI_B2_WAVES")) : 4;  // diagnostic
   if (b2w == 8)
     hipLaunchKernelGGL(k_frame_build2<8>, dim3((unsigned)a->ntiles), dim3(256), 0, st, *a);
   else

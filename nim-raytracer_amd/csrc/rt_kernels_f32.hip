@@ -181,7 +181,7 @@ extern "C" int rtmi_lean_f32_blocks_per_cu(unsigned subset, size_t shmem) {
 // per item); RTMI_LEAN1Q=0 picks the latter (diagnostic A/B).
 extern "C" int rtmi_lean1_quads() {
   static const int q = [] {
-    const char* e = std::getenv("RTMI_LEAN1Q");
+    const char* e = rtmi::diag_env("RTMI_LEAN1Q");
     return e ? std::atoi(e) : 1;
   }();
   return q;

@@ -137,7 +137,7 @@ int device_of_current() {
 // Pixel-list slots per pixel, 2^lg: RTMI_SLOT_LG (A/B knob) or -1 = by image size.
 inline int slot_lg_env() {
   static const int v = [] {
-    const char* e = std::getenv("RTMI_SLOT_LG");
+    const char* e = rtmi::diag_env("RTMI_SLOT_LG");
     return e ? std::min(10, std::max(0, std::atoi(e))) : -1;
   }();
   return v;
@@ -261,6 +261,10 @@ struct rt_scene {
     int id = 0;                    // which of the two sets (test hook)
     // forget the buffers: the next call re-allocates and re-zeroes them
     void invalidate() { w = h = 0; }
+    size_t bytes() const {
+      return cnt.bytes() + slots.bytes() + lean.bytes() + heavy.bytes() + ctr.bytes() + orect.bytes() +
+             info.bytes() + omask.bytes() + status.bytes() + huge.bytes() + tiles.bytes();
+    }
     void release() {
       cnt.release(); slots.release(); lean.release(); heavy.release(); ctr.release(); orect.release();
       info.release(); omask.release(); status.release(); huge.release(); tiles.release();
@@ -622,7 +626,7 @@ extern "C" int rt_scene_create(const rt_scene_desc* d, rt_scene** out_scene) {
   if (!affine(d->camera_to_world)) return fail(RT_E_UNSUPPORTED, "camera_to_world is not affine");
   const auto t0 = std::chrono::steady_clock::now();
   // RTMI_SETUP_PROFILE=1: per-phase wall times of scene setup on stderr
-  static const bool profile = std::getenv("RTMI_SETUP_PROFILE") != nullptr;
+  static const bool profile = rtmi::diag_env("RTMI_SETUP_PROFILE") != nullptr;
   auto tp = t0;
   const auto mark = [&](const char* phase) {
     if (!profile) return;
@@ -785,7 +789,7 @@ extern "C" int rt_scene_create(const rt_scene_desc* d, rt_scene** out_scene) {
     // the build stream at the highest priority (rank 0 of 8 back to back:
     // 0.163 -> 0.161 ms); RTMI_PIPE_PRIO=0: the default priority (A/B)
     int lo = 0, hi = 0;
-    const char* pe = std::getenv("RTMI_PIPE_PRIO");
+    const char* pe = rtmi::diag_env("RTMI_PIPE_PRIO");
     if (!(pe && std::atoi(pe) == 0) && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess)
       HIP_TRY(hipStreamCreateWithPriority(&s->bstream, hipStreamNonBlocking, hi));
     else
@@ -797,7 +801,7 @@ extern "C" int rt_scene_create(const rt_scene_desc* d, rt_scene** out_scene) {
     // enough. `used` doubles as `done`, which the host waits on before
     // reading device memory and peers copy behind: system scope.
     // RTMI_EVENT_SCOPE (A/B): 0 both system scope, 2 both device scope.
-    const char* es = std::getenv("RTMI_EVENT_SCOPE");
+    const char* es = rtmi::diag_env("RTMI_EVENT_SCOPE");
     const int scope = es && *es ? std::atoi(es) : 1;
     const unsigned fb = hipEventDisableTiming | (scope >= 1 ? hipEventReleaseToDevice : 0u);
     const unsigned fu = hipEventDisableTiming | (scope >= 2 ? hipEventReleaseToDevice : 0u);
@@ -1045,9 +1049,16 @@ extern "C" int rt_scene_destroy(rt_scene* s) {
   if (!s) return fail(RT_E_INVALID, "null scene");
   int prev = device_of_current();
   if (prev != s->device) (void)hipSetDevice(s->device);
-  if (s->done) (void)hipEventSynchronize(s->done);
-  if (s->stream) (void)hipStreamSynchronize(s->stream);
-  if (s->bstream) (void)hipStreamSynchronize(s->bstream);
+  {
+    // a call still inside the library on this scene (another thread) holds
+    // s->mu: wait for it to leave before the scene goes. The caller must not
+    // start new calls on a scene it destroys (rtmi.h); the Python / Nim
+    // caches keep a per-scene count of calls in flight for that
+    std::lock_guard<std::mutex> lk(s->mu);
+    if (s->done) (void)hipEventSynchronize(s->done);
+    if (s->stream) (void)hipStreamSynchronize(s->stream);
+    if (s->bstream) (void)hipStreamSynchronize(s->bstream);
+  }
   delete s;
   if (prev >= 0 && prev != -1) (void)hipSetDevice(prev);
   return RT_OK;
@@ -1062,8 +1073,16 @@ extern "C" int rt_scene_get_info(const rt_scene* s, rt_scene_info* out) {
   out->num_bvh_nodes = s->num_nodes;
   out->max_bvh_depth = s->max_depth;
   out->device = s->device;
-  out->device_bytes = (int64_t)(s->f32.bytes() + s->f64.bytes() + s->nodes.bytes() +
-                                s->partials.bytes() + s->queue.bytes() + s->queue2.bytes());
+  // everything the scene holds on the device: the geometry and BVH of both
+  // precisions, the light grids and bins, and the per-call buffer sets
+  // (fr / fr2 are the bulk at 4K)
+  std::lock_guard<std::mutex> lk(const_cast<rt_scene*>(s)->mu);
+  out->device_bytes = (int64_t)(s->f32.bytes() + s->f64.bytes() + s->nodes.bytes() + s->partials.bytes() +
+                                s->queue.bytes() + s->queue2.bytes() + s->f64_tables.bytes() +
+                                s->fb_scratch.bytes() + s->grids.bytes() + s->grid_off.bytes() +
+                                s->grid_ent.bytes() + s->obj_grids.bytes() + s->obj_grid_mask.bytes() +
+                                s->bin_dev.bytes() + s->sat_dev.bytes() + s->objbox_dev.bytes() +
+                                s->fr.bytes() + s->fr2.bytes());
   out->build_ms = s->build_ms;
   return RT_OK;
 }
@@ -1128,7 +1147,7 @@ unsigned f32_subset(const rt_scene* s, const rt_options* o) {
 // same samples per lane, summed in the same order).
 int f32_lanes(const rt_scene* s, const rt_options* o, int spp) {
   // diagnostic A/B: RTMI_MAX_LANES caps the lanes per pixel
-  static const int max_lanes = std::getenv("RTMI_MAX_LANES") ? std::atoi(std::getenv("RTMI_MAX_LANES")) : 64;
+  static const int max_lanes = rtmi::diag_env("RTMI_MAX_LANES") ? std::atoi(rtmi::diag_env("RTMI_MAX_LANES")) : 64;
   int L = 1;
   while (L * 2 <= std::min(std::min(spp, 64), std::max(1, max_lanes))) L *= 2;
   const unsigned sub = f32_subset(s, o);
@@ -1220,7 +1239,7 @@ int order_policy() {
     // camera-dependent data is carried from one call to the next; the
     // two-class launches already hand out the expensive (general) pixels
     // before the cheap (lean) ones.
-    const char* e = std::getenv("RTMI_ORDER");
+    const char* e = rtmi::diag_env("RTMI_ORDER");
     return e ? std::atoi(e) : 0;
   }();
   return v;
@@ -1228,7 +1247,7 @@ int order_policy() {
 
 double order_quantile() {
   static const double v = [] {
-    const char* e = std::getenv("RTMI_ORDER_P");
+    const char* e = rtmi::diag_env("RTMI_ORDER_P");
     return e ? std::atof(e) : 0.5;
   }();
   return v;
@@ -1335,7 +1354,11 @@ int frame_buffers(rt_scene* s, int w, int h, hipStream_t st) {
   // lists are longer the fewer pixels it covers (the bunny: 28 faces at most
   // at 1080p, past 32 for 7 % of its pixels at 320x180); a pixel past its
   // slots takes the BVH (exact, slower)
-  const int lg = f.want_lg >= 0 ? f.want_lg : slot_lg_for(w, h);
+  int lg = f.want_lg >= 0 ? f.want_lg : slot_lg_for(w, h);
+  // slot indices are 32-bit (pixel << lg in the kernels): a requested lg
+  // (test hook / diagnostic) is clamped to keep the block below 2^31 entries
+  // and 2 GiB
+  while (lg > 0 && (((unsigned long long)w * (unsigned long long)h) << lg) + kBinPad >= (1ull << 29)) --lg;
   if (f.w == w && f.h == h && (!lists || f.slot_lg == lg)) return RT_OK;
   // an earlier call may still read the old buffers: `st` (the build stream)
   // waits on the last call that used this set (its render kernels, and the
@@ -1446,7 +1469,8 @@ int frame_build(rt_scene* s, const rt_options* o, const Mapping& mp, const FastP
   records_launch(s, o, mp, p, records, split, a.r);
   a.tile_bits = f.tiles.p;
   a.tile_cls = f.status.p;
-  a.diag = std::getenv("RTMI_DIAG_B2") ? std::atoi(std::getenv("RTMI_DIAG_B2")) : 0;
+  static const int diag_b2 = rtmi::diag_env("RTMI_DIAG_B2") ? std::atoi(rtmi::diag_env("RTMI_DIAG_B2")) : 0;
+  a.diag = diag_b2;  // diagnostic builds only (probe modes, wrong images)
   a.tiles_x = (mp.ncols + 63) / 64;
   a.ntiles = a.tiles_x * ((mp.nrows + 3) / 4);
   a.zero = zero;
@@ -1595,7 +1619,7 @@ int fill_fast(rt_scene* s, const rt_options* o, const Mapping& mp, float* fb, Fa
     const uint64_t per_item = 64ull * (uint64_t)p.iters * levels * (1ull + (uint64_t)s->nlight) *
                               (uint64_t)std::max(1, s->nobj);
     // diagnostic builds with wider counters (RTMI_DIAG_LANES): RTMI_STAT_FLUSH=1 flushes every item
-    static const int flush_env = std::getenv("RTMI_STAT_FLUSH") ? std::atoi(std::getenv("RTMI_STAT_FLUSH")) : 0;
+    static const int flush_env = rtmi::diag_env("RTMI_STAT_FLUSH") ? std::atoi(rtmi::diag_env("RTMI_STAT_FLUSH")) : 0;
     p.stat_flush = (o->flags & RT_FLAG_COUNT_TRAVERSAL) ? 1
                    : flush_env > 0 ? flush_env
                                    : (int32_t)std::min<uint64_t>(1u << 20, std::max<uint64_t>(1, 0xFFFFFFFFull / per_item));
@@ -1636,7 +1660,7 @@ int fill_fast(rt_scene* s, const rt_options* o, const Mapping& mp, float* fb, Fa
   // can hit the mesh, every light a distant light whose shadow rays from the
   // pixel provably miss it, no reflection — get a kernel of their own; not
   // for the measuring launch of a launch order or instrumented launches
-  static const char* cost_dump = std::getenv("RTMI_COST_DUMP");
+  static const char* cost_dump = rtmi::diag_env("RTMI_COST_DUMP");
   const unsigned sub = f32_subset(s, o);
   const bool want_split = !(o->flags & (RT_FLAG_NO_SPLIT | RT_FLAG_COUNT_TRAVERSAL)) && !p.cost && !cost_dump &&
                           s->nlight <= 8 && rtmi_lean_f32_blocks_per_cu(sub, f32_table_lds(s, o)) > 0;
@@ -1768,7 +1792,7 @@ void fill_params(rt_scene* s, const PrecisionData<R>& pd, const rt_options* o, c
 // (k_render_mix1). RTMI_MIX=0/1 forces it (diagnostic A/B); by default:
 // always.
 bool mix_policy() {
-  static const int force = std::getenv("RTMI_MIX") ? std::atoi(std::getenv("RTMI_MIX")) : -1;
+  static const int force = rtmi::diag_env("RTMI_MIX") ? std::atoi(rtmi::diag_env("RTMI_MIX")) : -1;
   return force != 0;
 }
 
@@ -1868,7 +1892,7 @@ int launch(rt_scene* s, const rt_options* o, const Mapping& mp, float* d_out, hi
     if (p.ngroups == 0) return RT_OK;
     // diagnostic (tools/cost_map.py): RTMI_COST_DUMP=<file> records every
     // pixel group's duration (s_memtime cycles) of this launch into <file>
-    static const char* cost_dump = std::getenv("RTMI_COST_DUMP");
+    static const char* cost_dump = rtmi::diag_env("RTMI_COST_DUMP");
     DevBuf<unsigned> dbg_cost;
     if (cost_dump && !measuring && !p.cost) {
       if (dbg_cost.alloc((size_t)p.ngroups) == RT_OK) p.cost = dbg_cost.p;
@@ -1897,8 +1921,8 @@ int launch(rt_scene* s, const rt_options* o, const Mapping& mp, float* d_out, hi
           gen ? std::min<long long>((long long)(gen1 ? rtmi_gen1_f32_blocks_per_cu(p.nlight) : gbpc) * s->num_cus, blocks)
               : blocks;
       // diagnostic: RTMI_GEN_WAVES_CAP / RTMI_LEAN_WAVES_CAP = resident waves per SIMD each kernel may take
-      static const int gen_cap = std::getenv("RTMI_GEN_WAVES_CAP") ? std::atoi(std::getenv("RTMI_GEN_WAVES_CAP")) : 0;
-      static const int lean_cap = std::getenv("RTMI_LEAN_WAVES_CAP") ? std::atoi(std::getenv("RTMI_LEAN_WAVES_CAP")) : 0;
+      static const int gen_cap = rtmi::diag_env("RTMI_GEN_WAVES_CAP") ? std::atoi(rtmi::diag_env("RTMI_GEN_WAVES_CAP")) : 0;
+      static const int lean_cap = rtmi::diag_env("RTMI_LEAN_WAVES_CAP") ? std::atoi(rtmi::diag_env("RTMI_LEAN_WAVES_CAP")) : 0;
       const long long hcap2 = gen_cap > 0 ? std::min<long long>(hcap, (long long)gen_cap * s->num_cus) : hcap;
       const int hb = (int)std::max(1LL, std::min<long long>(hcap2, ((long long)p.ngroups + 3) / 4));
       ph.order = s->fr.heavy.p;
@@ -1915,7 +1939,7 @@ int launch(rt_scene* s, const rt_options* o, const Mapping& mp, float* d_out, hi
       // N = 4 0.278 -> 0.265 ms, profiles/r4/ab/r4t_*)
       const long long lwaves4 =
           4LL * std::min<long long>((long long)rtmi_lean1_f32_blocks_per_cu(p.nlight, 4) * s->num_cus, s->max_waves / 4);
-      static const int lp_env = std::getenv("RTMI_LEAN_LP") ? std::atoi(std::getenv("RTMI_LEAN_LP")) : 0;  // diagnostic: 4 / 16
+      static const int lp_env = rtmi::diag_env("RTMI_LEAN_LP") ? std::atoi(rtmi::diag_env("RTMI_LEAN_LP")) : 0;  // diagnostic: 4 / 16
       const int lp = !(lean1 && rtmi_lean1_quads())
                          ? 64
                          : (lp_env == 4 || lp_env == 16 ? lp_env : ((long long)(p.ngroups + 15) / 16 >= lwaves4 ? 4 : 16));
@@ -1946,12 +1970,12 @@ int launch(rt_scene* s, const rt_options* o, const Mapping& mp, float* d_out, hi
         const long long mcap = (long long)rtmi_mix1_f32_blocks_per_cu(p.nlight, lp) * s->num_cus;
         const int mb = (int)std::max(1LL, std::min<long long>(std::min<long long>(mcap, blocks),
                                                               ((long long)p.ngroups + lruns + 3) / 4));
-        static const int shard_cap = std::getenv("RTMI_SHARDS") ? std::atoi(std::getenv("RTMI_SHARDS")) : 0;  // diagnostic
+        static const int shard_cap = rtmi::diag_env("RTMI_SHARDS") ? std::atoi(rtmi::diag_env("RTMI_SHARDS")) : 0;  // diagnostic
         pm.shards = std::min(shard_cap > 0 ? std::min(shard_cap, kQueueShards) : kQueueShards, mb);
         pm.shards2 = pm.shards;
         // diagnostic (RTMI_PIPE_GRID=<percent>): a pipelined call's grid capped,
         // leaving CU slots to the next call's build
-        static const int pipe_grid = std::getenv("RTMI_PIPE_GRID") ? std::atoi(std::getenv("RTMI_PIPE_GRID")) : 0;
+        static const int pipe_grid = rtmi::diag_env("RTMI_PIPE_GRID") ? std::atoi(rtmi::diag_env("RTMI_PIPE_GRID")) : 0;
         const int mbl = s->pipe && pipe_grid > 0 ? std::max(1, (int)((long long)mb * pipe_grid / 100)) : mb;
         const int e = rtmi_launch_mix1_f32(&pm, p.nlight, lp, mbl, st);
         if (e) return fail(RT_E_DEVICE, "render kernel launch failed: %s", hipGetErrorString((hipError_t)e));
@@ -1963,13 +1987,13 @@ int launch(rt_scene* s, const rt_options* o, const Mapping& mp, float* d_out, hi
       // general kernel first on the caller's stream, the lean kernel on
       // the scene's aux stream (forked after the caller's earlier work,
       // joined before its later work)
-      static const bool serial = std::getenv("RTMI_SPLIT_SERIAL") != nullptr;  // diagnostic: one stream
+      static const bool serial = rtmi::diag_env("RTMI_SPLIT_SERIAL") != nullptr;  // diagnostic: one stream
       hipStream_t sl = serial ? st : s->aux;
       if (!serial) {
         HIP_TRY(hipEventRecord(s->fork, st));
         HIP_TRY(hipStreamWaitEvent(s->aux, s->fork, 0));
       }
-      static const bool lean_first = std::getenv("RTMI_LEAN_FIRST") != nullptr;  // diagnostic
+      static const bool lean_first = rtmi::diag_env("RTMI_LEAN_FIRST") != nullptr;  // diagnostic
       auto launch_lean = [&]() {
         return lean1 ? rtmi_launch_lean1_f32(&pl, p.nlight, lp, lb, sl) : rtmi_launch_lean_f32(&pl, sub, lb, shmem, sl);
       };
@@ -2062,28 +2086,10 @@ int flush_reduce(rt_scene* s, hipStream_t st) {
   return RT_OK;
 }
 
-// A camera-ray list fill that ran out of entry capacity (FC_OVERFLOW, set by
-// rt_frame.hip's fill passes, kept until reported here) left lists with
-// unwritten entries: the frame of that call is wrong, so the call that reads
-// Stats fails (RT_E_DEVICE) instead of returning RT_OK, and the frame
-// buffers are invalidated so the next call re-reads its entry count.
-// Reported once: the flag is cleared here (the caller has waited for the
-// scene's calls; the scene mutex is held).
-int report_overflow(rt_scene* s, int32_t flag) {
-  if (!flag) return RT_OK;
-  s->fr.invalidate();
-  const int32_t zero = 0;
-  HIP_TRY(hipMemcpy(s->fr.ctr.p + FC_OVERFLOW, &zero, sizeof zero, hipMemcpyHostToDevice));
-  return fail(RT_E_DEVICE, "camera-ray list entries overflowed their buffer (the frame is incomplete)");
-}
-
 int read_stats(rt_scene* s, hipStream_t st, rt_stats* out) {
   unsigned long long h[kStatSlots];
-  int32_t ovf = 0;
   HIP_TRY(hipMemcpyAsync(h, s->acc(), sizeof h, hipMemcpyDeviceToHost, st));
-  if (s->fr.ctr.p) HIP_TRY(hipMemcpyAsync(&ovf, s->fr.ctr.p + FC_OVERFLOW, sizeof ovf, hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
-  if (int rc = report_overflow(s, ovf)) return rc;
   out->num_primary_rays = h[STAT_PRIMARY];
   // renderer.nim:54-56 counts one test per object per trace call, and every
   // trace call is a primary, shadow or reflection ray: the float32 kernel
@@ -2316,7 +2322,6 @@ int last_lists(rt_scene* s, int64_t* lean, int64_t* general) {
   int32_t c[FC_WORDS];
   HIP_TRY(hipEventSynchronize(s->done));
   HIP_TRY(hipMemcpy(c, s->fr.ctr.p, sizeof c, hipMemcpyDeviceToHost));
-  if (int rc = report_overflow(s, c[FC_OVERFLOW])) return rc;
   *lean = c[FC_LEAN];
   *general = c[FC_HEAVY];
   return RT_OK;
@@ -2418,6 +2423,19 @@ extern "C" int64_t rtmi_test_frame_lists(rt_scene* s, int32_t* off, int32_t* ent
     off[p + 1] = (int32_t)n;
   }
   return std::min<int64_t>(n, ent_cap);
+}
+
+// Test hook: the last call's pixel records (w*h words, rt_frame.h: list
+// length | shadow skip bits << 24; only the call's pixels are defined).
+extern "C" int rtmi_test_pixel_info(rt_scene* s, uint32_t* info) {
+  if (!s || !info) return fail(RT_E_INVALID, "null argument");
+  std::lock_guard<std::mutex> lk(s->mu);
+  DeviceGuard g(s->device);
+  const rt_scene::Frame& f = s->fr;
+  if (!f.info.p || f.w == 0) return fail(RT_E_INVALID, "no per-call records yet");
+  HIP_TRY(hipEventSynchronize(s->done));
+  HIP_TRY(hipMemcpy(info, f.info.p, (size_t)f.w * (size_t)f.h * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  return RT_OK;
 }
 
 // The host builders (rt_bins.cpp build_pixel_bins + build_shadow_skips) on

@@ -195,6 +195,19 @@ def _shape_key(scene: Scene):
     return tuple(parts)
 
 
+class _Entry:
+    """One cached device copy: the DeviceScene, what it was built from, and
+    the renderLine calls running on it (renders happen outside the cache's
+    lock, so a replaced or invalidated copy is closed by whichever comes
+    last: the replacement, or the last of those calls)."""
+    __slots__ = ("ds", "shape", "cam", "fov", "users", "retired")
+
+    def __init__(self, ds, shape, cam, fov):
+        self.ds, self.shape, self.cam, self.fov = ds, shape, cam, fov
+        self.users = 0
+        self.retired = False
+
+
 class _DeviceCache:
     """The Nim binding's `deviceScene` in Python: one device
     copy per Scene, created on first use, re-created when the shape key
@@ -203,36 +216,86 @@ class _DeviceCache:
     150-153). Re-entrant like renderLine (the pool calls it from
     countProcessors() threads at once, workerpool.nim:72-99): lookups,
     creation and camera pushes hold one lock; the render call itself runs
-    outside it (the library serialises calls per scene)."""
+    outside it (the library serialises calls per scene), counted in its
+    entry, and a copy that is replaced or invalidated meanwhile is destroyed
+    only once its last call has returned (no use after free). Entries are
+    keyed weakly: when a Scene is collected, its device copy is released
+    (the cache no longer keeps every Scene and its GPU buffers
+    alive)."""
 
     def __init__(self):
-        self._lock = threading.Lock()
-        self._entries = {}  # id(scene) -> [scene, DeviceScene, shape key, camera bytes, fov]
+        # re-entrant: a Scene collected while this thread holds the lock runs
+        # its weakref callback (_collected) on this thread
+        self._lock = threading.RLock()
+        self._entries = {}  # id(scene) -> (weakref to the scene, _Entry)
 
-    def get(self, scene: Scene, device=0) -> "DeviceScene":
+    def _drop(self, e):
+        # under the lock: retire e; close it now if no call is running on it
+        e.retired = True
+        return e.ds if e.users == 0 else None
+
+    def acquire(self, scene: Scene, device=0):
+        """(DeviceScene, entry) with the entry's call count raised; pass the
+        entry to release() when the call has returned."""
+        import weakref
         shape = _shape_key(scene)
         cam = np.asarray(scene.cameraToWorld, np.float64).tobytes()
         fov = float(scene.fov)
+        stale = None
         with self._lock:
-            e = self._entries.get(id(scene))
-            if e is not None and e[0] is scene:
-                if e[2] != shape:  # geometry / materials / lights changed
-                    e[1].close()
-                    e[1] = DeviceScene(scene, device)
-                    e[2], e[3], e[4] = shape, cam, fov
-                elif e[3] != cam or e[4] != fov:  # the camera moved: the next call renders it
-                    e[1].set_camera(scene.cameraToWorld, fov)
-                    e[3], e[4] = cam, fov
-                return e[1]
-            ds = DeviceScene(scene, device)
-            self._entries[id(scene)] = [scene, ds, shape, cam, fov]
-            return ds
+            key = id(scene)
+            item = self._entries.get(key)
+            e = item[1] if item is not None and item[0]() is scene else None
+            if e is not None and e.shape != shape:  # geometry / materials / lights changed
+                stale = self._drop(e)
+                e = None
+            if e is None:
+                ds = DeviceScene(scene, device)
+                ds.scene = weakref.proxy(scene)  # the cache must not keep the Scene alive
+                e = _Entry(ds, shape, cam, fov)
+                self._entries[key] = (weakref.ref(scene, lambda _r, k=key: self._collected(k)), e)
+            elif e.cam != cam or e.fov != fov:  # the camera moved: the next call renders it
+                e.ds.set_camera(scene.cameraToWorld, fov)
+                e.cam, e.fov = cam, fov
+            e.users += 1
+        if stale is not None:
+            stale.close()
+        return e.ds, e
+
+    def release(self, e):
+        with self._lock:
+            e.users -= 1
+            last = e.retired and e.users == 0
+        if last:
+            e.ds.close()
+
+    def get(self, scene: Scene, device=0) -> "DeviceScene":
+        """The device copy (for calls the caller keeps in step with
+        invalidate() itself; renderLine uses acquire / release)."""
+        ds, e = self.acquire(scene, device)
+        self.release(e)
+        return ds
 
     def invalidate(self, scene: Scene):
         with self._lock:
-            e = self._entries.pop(id(scene), None)
-        if e is not None:
-            e[1].close()
+            item = self._entries.pop(id(scene), None)
+            stale = self._drop(item[1]) if item is not None else None
+        if stale is not None:
+            stale.close()
+
+    def _collected(self, key):
+        with self._lock:
+            item = self._entries.get(key)
+            if item is None or item[0]() is not None:
+                return
+            del self._entries[key]
+            stale = self._drop(item[1])
+        if stale is not None:
+            stale.close()
+
+    def __len__(self):
+        with self._lock:
+            return len(self._entries)
 
 
 _cache = _DeviceCache()
@@ -252,8 +315,13 @@ def renderLine(scene, opts: Options, fb, y, step=1, maxStep=1) -> Stats:
     """renderer.nim:162-211 — one scanline (and its step x step blocks).
     `scene` is the reference's Scene (its device copy is cached and kept in
     step with the Scene's camera, as the Nim binding does) or a DeviceScene."""
-    ds = scene if isinstance(scene, DeviceScene) else deviceScene(scene)
-    return ds.render_lines(opts, fb, y, y + 1, step, maxStep)
+    if isinstance(scene, DeviceScene):
+        return scene.render_lines(opts, fb, y, y + 1, step, maxStep)
+    ds, e = _cache.acquire(scene)
+    try:
+        return ds.render_lines(opts, fb, y, y + 1, step, maxStep)
+    finally:
+        _cache.release(e)
 
 
 def render_frame(scene: DeviceScene, opts: Options, fb=None):

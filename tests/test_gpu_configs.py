@@ -20,8 +20,10 @@ silhouette than the float64 one changes one hit and its two shadow rays).
   C3  bunny + ground, 256 spp: the whole 480x270 frame, the WHOLE 1920x1080
       frame with the benchmarked launch's own Stats, and 8 full rows of it
       rendered by per-row calls — through k_render_mix1, the benchmarked kernel
-  C4  bunny, 3840x2160, 1024 spp on one GPU: properties + 2 oracle rows
-  C5  1M-triangle torus, 3840x2160, 4096 spp on one GPU: properties + 1 row
+  C4  bunny, 3840x2160, 1024 spp on one GPU: properties + 16 oracle rows
+      spread over the mesh, its shadow and the horizon
+  C5  1M-triangle torus, 3840x2160, 4096 spp on one GPU: properties + 16
+      oracle rows likewise
 """
 import numpy as np
 import pytest
@@ -202,15 +204,44 @@ def _properties(ds, o, st_expected_primary):
     return img.cpu().numpy(), sa
 
 
+def _spread_rows(ds, o, n=16):
+    """n rows of the 4K frame spread over what it shows: the rows where the
+    camera rays can hit the mesh (this call's pixel lists, rt_frame.h), rows
+    of the mesh's shadow on the ground (pixels whose shadow rays are not
+    provably clear: no skip bit) and the horizon / sky — a coverage of the
+    frame's pixel classes, chosen from the call's own pixel records."""
+    import ctypes as C
+    from rtmi._lib import check, lib
+    info = np.zeros((o.height, o.width), np.uint32)
+    f = lib().rtmi_test_pixel_info
+    f.argtypes = [C.c_void_p, C.POINTER(C.c_uint32)]
+    check(f(ds.h, info.ctypes.data_as(C.POINTER(C.c_uint32))))
+    cnt = (info & 0x00FFFFFF).astype(np.int64)
+    skip = info >> 24
+    mesh_rows = np.nonzero((cnt > 0).any(axis=1))[0]
+    shadow_rows = np.nonzero(((cnt == 0) & (skip != 3)).any(axis=1))[0]
+    picks = set()
+    for rows_of, k in ((mesh_rows, 8), (shadow_rows, 5)):
+        if len(rows_of):
+            picks.update(int(r) for r in rows_of[np.linspace(0, len(rows_of) - 1, k).round().astype(int)])
+    for r in np.linspace(0, o.height - 1, n + 2).round().astype(int)[1:-1]:  # horizon / sky / open ground
+        if len(picks) >= n:
+            break
+        picks.add(int(r))
+    return sorted(picks)[:n]
+
+
 def test_c4_4k_1024spp(gpu):
     """C4 (bunny, 3840x2160, 1024 spp) on one GPU: determinism, ray
-    accounting, finite non-negative output, and 2 full rows at 1024 spp
-    against the oracle."""
+    accounting, finite non-negative output, and 16 full rows at 1024 spp —
+    through the bunny, its shadow and the horizon — against the oracle, with
+    all counters."""
     sc = scenes.mesh_bunny()
     o = _opts(3840, 2160, 32)
     ds = DeviceScene(sc)
     img, st = _properties(ds, o, 3840 * 2160 * 1024)
-    rows = [1000, 1240]
+    rows = _spread_rows(ds, o)
+    assert len(rows) == 16
     ref, rst = _oracle_rows(sc, o, rows)
     _check(img[rows], ref[rows], "C4 rows", frac=0.9999, fine_frac=0.998, mean_tol=2e-6)
     _counts_close(_row_stats(ds, o, rows), rst)
@@ -218,13 +249,37 @@ def test_c4_4k_1024spp(gpu):
 
 def test_c5_torus_4k_4096spp(gpu):
     """C5 (1,000,000-triangle torus, 3840x2160, 4096 spp) on one GPU:
-    determinism, ray accounting, and one full row at 4096 spp against the
-    oracle."""
+    determinism, ray accounting, and 16 full rows at 4096 spp — through the
+    torus, its shadow and the horizon — against the oracle, with all
+    counters."""
     sc = scenes.torus_scene()
     o = _opts(3840, 2160, 64)
     ds = DeviceScene(sc)
     img, st = _properties(ds, o, 3840 * 2160 * 4096)
-    rows = [1150]
+    rows = _spread_rows(ds, o)
+    assert len(rows) == 16
     ref, rst = _oracle_rows(sc, o, rows)
-    _check(img[rows], ref[rows], "C5 row", frac=0.9999, fine_frac=0.98)
+    _check(img[rows], ref[rows], "C5 rows", frac=0.9999, fine_frac=0.98)
     _counts_close(_row_stats(ds, o, rows), rst)
+
+
+def test_c4_4k_eight_ranks_equal_single_call(gpu):
+    """C4's layout at full size: 8 ranks (rt_multi: per-rank scenes, 4-row
+    bands dealt round-robin, copies into devices[0] and the un-interleave —
+    here all on device 0) render the 3840x2160, 1024-spp frame bit-identical
+    to one whole-frame call, with the same Stats."""
+    import torch
+    from rtmi.renderer import MultiDeviceScene
+    sc = scenes.mesh_bunny()
+    o = _opts(3840, 2160, 32)
+    ref = torch.zeros(3840 * 2160 * 3, dtype=torch.float32, device="cuda")
+    ds = DeviceScene(sc)
+    sref = ds.render_device(o, ref)
+    ds.close()
+    ms = MultiDeviceScene(sc, devices=[0] * 8, band_h=4)
+    try:
+        out = torch.zeros_like(ref)
+        assert ms.render_frame_device(o, out) == sref
+        assert torch.equal(out, ref)
+    finally:
+        ms.close()

@@ -127,6 +127,63 @@ def test_threaded_renderline_fp32_c3_scene(gpu):
         invalidateScene(sc)
 
 
+def test_invalidate_during_threaded_renderline(gpu):
+    """invalidateScene / a geometry edit while pool threads are
+    inside renderLine must not free the device copy under them. 6 threads
+    render scanlines in a loop while the main thread invalidates the Scene
+    and edits a box 20 times; every scanline either renders (the rows of the
+    last pass equal the oracle's frame) or raises nothing — no fault, no
+    error — and the replaced copies are all released."""
+    import gc
+    import weakref
+    from rtmi import renderer
+    from rtmi.scene import Box
+    sc = scenes.boxes2()
+    opts = Options(width=64, height=36, antialias=Antialias(akGrid, 2), bias=BIAS, precision=Precision.fp64)
+    fb = np.zeros((36, 64, 3), np.float32)
+    stop = threading.Event()
+    errs = []
+    copies = []
+
+    def worker(k):
+        try:
+            while not stop.is_set():
+                for y in range(k, 36, 6):
+                    renderLine(sc, opts, fb, y)
+        except Exception as e:  # noqa: BLE001
+            errs.append(repr(e))
+
+    ts = [threading.Thread(target=worker, args=(k,)) for k in range(6)]
+    [t.start() for t in ts]
+    box = next(o.geometry for o in sc.objects if isinstance(o.geometry, Box))
+    try:
+        for i in range(20):
+            copies.append(weakref.ref(deviceScene(sc)))
+            if i % 2:
+                invalidateScene(sc)
+            else:
+                box.vmax = box.vmax + np.array([0.0, 0.01, 0.0])
+    finally:
+        stop.set()
+        [t.join() for t in ts]
+    assert not errs, errs[:3]
+    fb[:] = 0
+    for y in range(36):
+        renderLine(sc, opts, fb, y)
+    ref, _ = _oracle(sc, opts)
+    assert np.array_equal(fb, ref)
+    invalidateScene(sc)
+    gc.collect()
+    assert all(r() is None or not r().h.value for r in copies)  # every retired copy was destroyed
+    n = len(renderer._cache)
+    tmp = scenes.boxes2()
+    renderLine(tmp, opts, fb, 0)
+    assert len(renderer._cache) == n + 1
+    del tmp
+    gc.collect()
+    assert len(renderer._cache) == n  # a collected Scene releases its device copy
+
+
 def _slot_lg(ds, lg=-1):
     f = lib().rtmi_test_slot_lg
     f.restype = C.c_int

@@ -36,6 +36,12 @@ def variants():
     v["lean_nolights"] = (s, o)
     v["boxes2_c2"] = (scenes.boxes2(), Options(width=1920, height=1080, antialias=Antialias(akGrid, 8),
                                                bias=1e-4, precision=Precision.fp32))
+    # fallback-kernel scenes: mesh + spheres / boxes /
+    # rotations + point light + reflection, two meshes
+    for nm in ("mesh-mix", "two-meshes"):
+        v[nm.replace("-", "_") + "_64"] = (scenes.SCENES[nm](), Options(width=1920, height=1080,
+                                                                         antialias=Antialias(akGrid, 8), bias=1e-4,
+                                                                         maxRayDepth=5, precision=Precision.fp32))
     sel = os.environ.get("ABLATE", "")
     return {k: x for k, x in v.items() if not sel or k in sel.split(",")}
 
