@@ -13,9 +13,10 @@
 #                    python tools/pmc_summary.py gpurun_out/$OUT/pmc_<cfg> <workload key>)
 #   ab               interleaved A/B of bench.py over library builds: for $AB_REPS reps,
 #                    each variant in $AB_VARIANTS (base = the in-tree librtmi.so, else
-#                    tools/ab/<v>.so from tools/build_variant.sh) with --config $AB_CONFIG
-#                    $AB_ARGS; prints ms_per_step / kernel_ms per run
-#   py:SCRIPT[:ARGS] python SCRIPT ARGS (a measurement tool), stdout -> py_<name>.out
+#                    tools/ab/<v>.so from tools/build_variant.sh; v@K=V,K2=V2 runs it
+#                    with those environment variables, e.g. a RTMI_DIAG build's knobs)
+#                    with --config $AB_CONFIG $AB_ARGS; prints ms_per_step / kernel_ms
+#   py:SCRIPT[:ARG]  python SCRIPT ARG $PY_ARGS (a measurement tool), stdout -> py_<name>.out
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
@@ -54,16 +55,18 @@ for st in ${STAGES:-tests}; do
       echo "pmc $c$sfx done" ;;
     ab)
       for i in $(seq ${AB_REPS:-2}); do
-        for v in ${AB_VARIANTS:-base}; do
+        for spec in ${AB_VARIANTS:-base}; do
+          v=${spec%%@*}; envs=""; [ "$spec" != "$v" ] && envs=${spec#*@}
+          tag=$(echo "$spec" | tr '@=,' '___')
           L=""; [ $v != base ] && L=tools/ab/$v.so
-          RTMI_LIB=$L timeout -k 10 $T python bench.py --config ${AB_CONFIG:-C3} --no-cpu ${AB_ARGS:---steps 20 --warmup 3} \
-            > $O/ab_${v}_$i.json 2> $O/ab_${v}_$i.err || { tail -20 $O/ab_${v}_$i.err; exit 1; }
-          echo "$v $i $(grep -o '"ms_per_step": [0-9.]*' $O/ab_${v}_$i.json) $(grep -o '"kernel_ms": [0-9.]*' $O/ab_${v}_$i.json)"
+          env RTMI_LIB=$L ${envs//,/ } timeout -k 10 $T python bench.py --config ${AB_CONFIG:-C3} --no-cpu \
+            ${AB_ARGS:---steps 20 --warmup 3} > $O/ab_${tag}_$i.json 2> $O/ab_${tag}_$i.err || { tail -20 $O/ab_${tag}_$i.err; exit 1; }
+          echo "$spec $i $(grep -o '"ms_per_step": [0-9.]*' $O/ab_${tag}_$i.json) $(grep -o '"kernel_ms": [0-9.]*' $O/ab_${tag}_$i.json)"
         done
       done ;;
     py)
       n=$(basename "$cfg" .py)
-      timeout -k 10 ${PY_TIMEOUT:-600} python -u $cfg $prec > $O/py_$n.out 2> $O/py_$n.err || { tail -20 $O/py_$n.err; exit 1; }
+      timeout -k 10 ${PY_TIMEOUT:-600} python -u $cfg $prec ${PY_ARGS:-} > $O/py_$n.out 2> $O/py_$n.err || { tail -20 $O/py_$n.err; exit 1; }
       tail -${PY_TAIL:-20} $O/py_$n.out ;;
     *) echo "unknown stage $st"; exit 2 ;;
   esac

@@ -1,29 +1,63 @@
-"""Per-rank render time of the band-sharded C3 frame, simulated on one GPU:
-for N in 1,2,4,8 every rank's rt_render_bands_device call is timed (HIP
-events, median of REPS) and the slowest rank is the N-GPU render time (the
-all-gather + unshard come on top). Also each rank's back-to-back rate
-(REPS calls issued without a host sync, total / REPS): a rank's step loop,
-where a call's per-call build overlaps the previous call's render
-(rt_scene bstream). Prints one JSON line per band height."""
+"""N-GPU projection of a BASELINE config's band-sharded frame, simulated on one GPU.
+
+    CONFIG=C3|C4|C5 REPS=5 BANDS=4 python tools/scaling_sim.py
+
+For N in 1, 2, 4, 8 every rank's rt_render_bands_device call is timed (HIP
+events, median of REPS: `world{N}_max_ms`, the slowest rank) and called REPS
+times back to back with no host sync (`world{N}_b2b_max_ms`: a rank's step
+loop, where a call's per-call build overlaps the previous call's render —
+rt_scene bstream). On top of the slowest rank, bench.py's N-GPU step also
+runs on rank 0: the on-GPU un-interleave of the gathered bands
+(`unshard_ms`, measured here for the N-rank layout) and the RCCL gather,
+which overlaps the next frame's render (bench.py gathers frame k while
+frame k+1 renders) and so only shows when it takes longer than a render:
+`gather_model_ms` = the bytes rank 0 receives / (N - 1 xGMI links x
+LINK_GBS, default 50 GB/s per link and direction — a conservative figure
+for MI355X's ~153 GB/s links). The projection:
+    step_N = b2b_max_N + unshard_N + max(0, gather_N - b2b_max_N)
+and `projected_speedup_8` = step_1 / step_8 (step_1 = the whole-frame call).
+Prints one JSON line per band height.
+"""
 import json
 import os
 import sys
 
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "nim-raytracer_amd"))
+REPO = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
+sys.path.insert(0, os.path.join(REPO, "nim-raytracer_amd"))
+sys.path.insert(0, REPO)
 import torch  # noqa: E402
 
-from rtmi import Antialias, Options, Precision, akGrid, scenes  # noqa: E402
+from bench import CONFIGS, _scene  # noqa: E402
+from rtmi import Antialias, Options, Precision, akGrid  # noqa: E402
 from rtmi.dist import band_rows  # noqa: E402
-from rtmi.renderer import DeviceScene  # noqa: E402
+from rtmi.renderer import DeviceScene, unshard_bands_device  # noqa: E402
 
-W, H, M = 1920, 1080, 16
+CFG = os.environ.get("CONFIG", "C3")
+name, W, H, M, _desc = CONFIGS[CFG]
 REPS = int(os.environ.get("REPS", "5"))
-ds = DeviceScene(scenes.mesh_bunny())
+LINK_GBS = float(os.environ.get("LINK_GBS", "50"))
+ds = DeviceScene(_scene(name))
 opts = Options(width=W, height=H, antialias=Antialias(akGrid, M), bias=1e-4, precision=Precision.fp32,
                flags=int(os.environ.get("RTMI_FLAGS", "0"), 0))
 stream = torch.cuda.current_stream()
-for band_h in [int(b) for b in os.environ.get("BANDS", "16,8,4").split(",")]:
-    res = {"band_h": band_h}
+
+
+def timed(fn, reps):
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record(stream)
+    for _ in range(reps):
+        fn()
+    b.record(stream)
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / reps
+
+
+fb = torch.zeros(W * H * 3, dtype=torch.float32, device="cuda")
+for band_h in [int(b) for b in os.environ.get("BANDS", "4").split(",")]:
+    res = {"config": CFG, "width": W, "height": H, "spp": M * M, "band_h": band_h, "reps": REPS,
+           "link_gbs_model": LINK_GBS}
+    ds.render_device(opts, fb, stream=stream, stats=False)
+    res["whole_frame_b2b_ms"] = round(timed(lambda: ds.render_device(opts, fb, stream=stream, stats=False), REPS), 4)
     for world in (1, 2, 4, 8):
         rows = band_rows(H, band_h, world)
         buf = torch.zeros(rows * W * 3, dtype=torch.float32, device="cuda")
@@ -33,25 +67,28 @@ for band_h in [int(b) for b in os.environ.get("BANDS", "16,8,4").split(",")]:
             for _ in range(2):  # warm: the first launch of a mapping measures its launch order
                 ds.render_bands_device(opts, buf, band_h, rank, world, stream=stream, stats=False)
             for _ in range(REPS):
-                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                a.record(stream)
-                ds.render_bands_device(opts, buf, band_h, rank, world, stream=stream, stats=False)
-                b.record(stream)
-                torch.cuda.synchronize()
-                ts.append(a.elapsed_time(b))
+                ts.append(timed(lambda: ds.render_bands_device(opts, buf, band_h, rank, world, stream=stream,
+                                                               stats=False), 1))
             per.append(sorted(ts)[len(ts) // 2])
-            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            a.record(stream)
-            for _ in range(REPS):
-                ds.render_bands_device(opts, buf, band_h, rank, world, stream=stream, stats=False)
-            b.record(stream)
-            torch.cuda.synchronize()
-            b2b.append(a.elapsed_time(b) / REPS)
+            b2b.append(timed(lambda: ds.render_bands_device(opts, buf, band_h, rank, world, stream=stream,
+                                                            stats=False), REPS))
             if rank == 0:
                 res[f"world{world}_split"] = list(ds.last_split())
-        res[f"world{world}_max_ms"] = round(max(per), 3)
-        res[f"world{world}_mean_ms"] = round(sum(per) / world, 3)
-        res[f"world{world}_b2b_max_ms"] = round(max(b2b), 4)
+        gathered = torch.zeros(world * rows * W * 3, dtype=torch.float32, device="cuda")
+        unshard = timed(lambda: unshard_bands_device(gathered, fb, W, H, band_h, world, stream=stream), REPS)
+        recv_bytes = (world - 1) * rows * W * 12
+        gather = recv_bytes / (max(1, world - 1) * LINK_GBS * 1e9) * 1e3 if world > 1 else 0.0
+        b2b_max = max(b2b)
+        step = b2b_max + (unshard if world > 1 else 0.0) + max(0.0, gather - b2b_max)
+        res[f"world{world}_max_ms"] = round(max(per), 4)
+        res[f"world{world}_mean_ms"] = round(sum(per) / world, 4)
+        res[f"world{world}_b2b_max_ms"] = round(b2b_max, 4)
+        res[f"world{world}_unshard_ms"] = round(unshard, 4)
+        res[f"world{world}_gather_model_ms"] = round(gather, 4)
+        res[f"world{world}_step_ms"] = round(step, 4)
     res["render_speedup_8"] = round(res["world1_max_ms"] / res["world8_max_ms"], 2)
     res["b2b_speedup_8"] = round(res["world1_b2b_max_ms"] / res["world8_b2b_max_ms"], 2)
+    res["projected_speedup_8"] = round(res["whole_frame_b2b_ms"] / res["world8_step_ms"], 2)
+    for w in (2, 4):
+        res[f"projected_speedup_{w}"] = round(res["whole_frame_b2b_ms"] / res[f"world{w}_step_ms"], 2)
     print(json.dumps(res), flush=True)
