@@ -41,6 +41,7 @@ constexpr double kPixelMargin = 0.05;
 struct BinTri {
   double v[3][3];
   int32_t rec;
+  int32_t face;  // the face's index in its mesh (TriFast.id)
 };
 
 // Pixel lists: off[y * w + x] .. off[y * w + x + 1] index ent[] (record byte

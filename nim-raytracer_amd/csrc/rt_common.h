@@ -298,7 +298,36 @@ struct FastParams {
   float* rq;
   long long* sec;
   int64_t sec_base;
+  // shadow-ray records (LTri) of the distant lights whose bit is set in
+  // lrec_mask: every float32 shadow test against the mesh for such a light —
+  // cell lists, BVH leaves, batched or one-sample paths alike — reads the
+  // face's record at lrec_base + light * lrec_stride + (its TriFast byte
+  // offset), so every path forms the same t and the same verdict
+  uint64_t lrec_base;
+  int64_t lrec_stride;
+  uint32_t lrec_mask;
+  int32_t pad_lrec;
 };
+// A face's shadow-ray test for one distant light (fixed direction d, mesh
+// object space), prepared in float64 by the host (rtmi.cpp make_ltri): with
+// c = (o - v0) x d the single-sided Moller-Trumbore test (geom.nim:283-336)
+// is u = e2.c / det, v = -e1.c / det, t = (o - v0).nn / -det, nn = -(e1 x e2),
+// det = nn.d — all three affine in the ray origin o alone:
+//   u = p.o + cu, v = q.o + cv, t = tv.o + ct
+// (p = (d x e2) / det, q = (d x -e1) / det, tv = nn / -det); a face with
+// det < 1e-6 for this light can never pass (p = q = 0, cu = cv = -1). The
+// hit test is then 9 FMAs and min(u, v, 1 - (u + v)) >= 0.
+struct alignas(16) LTri {
+  float p[3];
+  float cu;
+  float q[3];
+  float cv;
+  float tv[3];
+  float ct;
+  int32_t id;    // the face's index (TriFast.id)
+  int32_t pad[3];
+};
+static_assert(sizeof(LTri) == 64, "LTri must be 64 bytes (one scalar load, TriFast-sized offsets)");
 // reflection queue of a k_render_wave wave: up to 63 rays left over plus a
 // pass's 64 new ones; fields ro xyz, rd xyz, weight, dst * 16 + depth
 constexpr int kReflQueue = 128, kReflFields = 8;

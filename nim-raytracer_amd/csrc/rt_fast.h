@@ -243,6 +243,54 @@ __device__ __forceinline__ void tri_test(const TR& T, F3 o, F3 d, unsigned long 
   tc = acc ? ts : tc;
 }
 
+// Shadow-ray tests on a face's LTri record for the ray's distant light
+// (rt_common.h): u, v, t are affine in the ray origin, so a test is 9 FMAs
+// and the barycentric range in one min (u >= 0, v >= 0, u + v <= 1; the
+// det >= 1e-6 cull is folded into the record). Every float32 path tests a
+// shadow ray to a light with records this way (list searches, BVH leaves,
+// batched and one-sample loops), so they all form the same t bit for bit.
+struct LRegs {
+  float p[3], cu, q[3], cv, tv[3], ct;
+  unsigned int id;
+};
+__device__ __forceinline__ LRegs load_ltri(const RT_CONST LTri* t) {
+  using V16 = unsigned int __attribute__((ext_vector_type(16)));
+  const V16 r = *(const RT_CONST V16*)t;
+  asm volatile("" ::"s"(r[13]), "s"(r[14]), "s"(r[15]));
+  LRegs L;
+  L.p[0] = __uint_as_float(r[0]), L.p[1] = __uint_as_float(r[1]), L.p[2] = __uint_as_float(r[2]);
+  L.cu = __uint_as_float(r[3]);
+  L.q[0] = __uint_as_float(r[4]), L.q[1] = __uint_as_float(r[5]), L.q[2] = __uint_as_float(r[6]);
+  L.cv = __uint_as_float(r[7]);
+  L.tv[0] = __uint_as_float(r[8]), L.tv[1] = __uint_as_float(r[9]), L.tv[2] = __uint_as_float(r[10]);
+  L.ct = __uint_as_float(r[11]);
+  L.id = r[12];
+  return L;
+}
+// t of the hit, or -1 (no hit: outside the face, or det culled)
+template <class LR>
+__device__ __forceinline__ float ltri_t(const LR& L, F3 o) {
+  const float u = __builtin_fmaf(L.p[0], o.x, __builtin_fmaf(L.p[1], o.y, __builtin_fmaf(L.p[2], o.z, L.cu)));
+  const float v = __builtin_fmaf(L.q[0], o.x, __builtin_fmaf(L.q[1], o.y, __builtin_fmaf(L.q[2], o.z, L.cv)));
+  const float t = __builtin_fmaf(L.tv[0], o.x, __builtin_fmaf(L.tv[1], o.y, __builtin_fmaf(L.tv[2], o.z, L.ct)));
+  const float g = fminf(fminf(u, v), 1.0f - (u + v));
+  return g >= 0.0f ? t : -1.0f;
+}
+template <class LR>
+__device__ __forceinline__ void ltri_test(const LR& L, F3 o, unsigned long long& key, float& tc) {
+  const float ts = ltri_t(L, o);
+  const unsigned long long k = tkey(ts, (unsigned int)L.id);
+  const bool acc = k < key;
+  key = acc ? k : key;
+  tc = acc ? ts : tc;
+}
+// the records of shadow rays to distant light `light` (byte offsets are the
+// faces' TriFast offsets), or nullptr when the light has none
+__device__ __forceinline__ const char* lrec_of(KP p, int light) {
+  if (light < 0 || light >= 32 || !((p->lrec_mask >> light) & 1u)) return nullptr;
+  return (const char*)(p->lrec_base + (uint64_t)light * (uint64_t)p->lrec_stride);
+}
+
 // A record of the float32 tree (FastParams.tree) at a byte offset: one scalar
 // base + a 32-bit SGPR offset (s_load ... soffset), no 64-bit address
 // arithmetic on the traversal's dependent chain.
@@ -254,7 +302,17 @@ __device__ __forceinline__ const RT_CONST T* rec(KP p, int off) {
 // Leaf: the n (1..kLeafMax, wave-uniform) triangles starting at byte offset
 // `first` of the tree.
 __device__ __forceinline__ void leaf(KP p, int first, int n, F3 o, F3 d, unsigned long long& key,
-                                     float& tc) {
+                                     float& tc, const char* lb = nullptr) {
+  if (lb) {  // a shadow ray to a light with LTri records
+    const RT_CONST LTri* l = (const RT_CONST LTri*)(lb + (unsigned)first);
+    ltri_test(load_ltri(l), o, key, tc);
+#pragma unroll
+    for (int k = 1; k < kLeafMax; ++k) {
+      if (k >= n) break;
+      ltri_test(load_ltri(l + k), o, key, tc);
+    }
+    return;
+  }
   const RT_CONST TriFast* t = rec<TriFast>(p, first);
   tri_test(load_tri(t), o, d, key, tc);
 #pragma unroll
@@ -296,7 +354,8 @@ __device__ __forceinline__ SlabRay slab_ray(F3 o, F3 d) {
 // take no part (never entered, retired, or done by a bin search).
 template <bool COUNT>
 __device__ __forceinline__ void traverse(KP p, int root, F3 o, F3 d, SlabRay sr, bool early, float stop,
-                                         unsigned long long& key, float& tc, Stats32& ws) {
+                                         unsigned long long& key, float& tc, Stats32& ws,
+                                         const char* lb = nullptr) {
   if (bal(tc >= 0.0f) == 0ull) return;
   RT_STAMP(t_enter);
   const F3 ni = sr.ni, oi = sr.oi;
@@ -334,7 +393,7 @@ __device__ __forceinline__ void traverse(KP p, int root, F3 o, F3 d, SlabRay sr,
           ws.v[STAT_TRI_FETCH] += (unsigned int)nd.n0;
           ws.v[STAT_LANE_TRIS] += pc(m0) * (unsigned int)nd.n0;
         }
-        leaf(p, nd.c0, nd.n0, o, d, key, tc);
+        leaf(p, nd.c0, nd.n0, o, d, key, tc, lb);
         if (early) tc = tc <= stop ? -1.0f : tc;
       }
       m0 = 0ull;
@@ -345,7 +404,7 @@ __device__ __forceinline__ void traverse(KP p, int root, F3 o, F3 d, SlabRay sr,
           ws.v[STAT_TRI_FETCH] += (unsigned int)nd.n1;
           ws.v[STAT_LANE_TRIS] += pc(m1) * (unsigned int)nd.n1;
         }
-        leaf(p, nd.c1, nd.n1, o, d, key, tc);
+        leaf(p, nd.c1, nd.n1, o, d, key, tc, lb);
         if (early) tc = tc <= stop ? -1.0f : tc;
       }
       m1 = 0ull;
@@ -390,7 +449,8 @@ __device__ __forceinline__ void traverse(KP p, int root, F3 o, F3 d, SlabRay sr,
 // ent is padded, so the four-record read-ahead stays inside the array.
 template <bool COUNT>
 __device__ __forceinline__ void list_search(KP p, const int32_t* ent, int b, int e, F3 o, F3 d, bool early,
-                                            float stop, unsigned long long& key, float& tc, Stats32& ws) {
+                                            float stop, unsigned long long& key, float& tc, Stats32& ws,
+                                            const char* lb = nullptr) {
   if constexpr (COUNT) {
     ws.v[STAT_TRI_FETCH] += (unsigned int)(e - b);
     ws.v[STAT_LANE_TRIS] += pc(bal(tc >= 0.0f)) * (unsigned int)(e - b);
@@ -398,8 +458,12 @@ __device__ __forceinline__ void list_search(KP p, const int32_t* ent, int b, int
 #ifdef RTMI_DIAG_NOLIST
   return;  // diagnostic build only: the binned searches' share of the frame
 #endif
+  auto test = [&](int off) {
+    if (lb) ltri_test(load_ltri((const RT_CONST LTri*)(lb + (unsigned)off)), o, key, tc);
+    else tri_test(load_tri(rec<TriFast>(p, off)), o, d, key, tc);
+  };
   if (early && b < e) {  // a light cell's first face alone (the one covering most of the cell)
-    tri_test(load_tri(rec<TriFast>(p, cp(ent)[b])), o, d, key, tc);
+    test(cp(ent)[b]);
     tc = tc <= stop ? -1.0f : tc;
     if (bal(tc >= 0.0f) == 0ull) return;
     ++b;
@@ -407,10 +471,10 @@ __device__ __forceinline__ void list_search(KP p, const int32_t* ent, int b, int
   for (int k = b; k < e; k += 4) {
     const RT_CONST int32_t* q = cp(ent) + k;
     const int r0 = q[0], r1 = q[1], r2 = q[2], r3 = q[3];
-    tri_test(load_tri(rec<TriFast>(p, r0)), o, d, key, tc);
-    if (k + 1 < e) tri_test(load_tri(rec<TriFast>(p, r1)), o, d, key, tc);
-    if (k + 2 < e) tri_test(load_tri(rec<TriFast>(p, r2)), o, d, key, tc);
-    if (k + 3 < e) tri_test(load_tri(rec<TriFast>(p, r3)), o, d, key, tc);
+    test(r0);
+    if (k + 1 < e) test(r1);
+    if (k + 2 < e) test(r2);
+    if (k + 3 < e) test(r3);
     if (early) {
       tc = tc <= stop ? -1.0f : tc;
       if (bal(tc >= 0.0f) == 0ull) break;
@@ -521,6 +585,7 @@ __device__ __forceinline__ unsigned long long mesh_search(KP p, const FObj& ob, 
                                                           int bin, const int32_t* boff, const int32_t* bent,
                                                           bool nohit, int light, Stats32& ws) {
   const bool ex = early && i == p->shadow_mesh;
+  const char* lb = shadow ? lrec_of(p, light) : nullptr;  // distant-light shadow rays: LTri records
   float stop = -1.0f;
   if (ex) {
     RT_STAMP(t_st0);
@@ -563,17 +628,17 @@ __device__ __forceinline__ unsigned long long mesh_search(KP p, const FObj& ob, 
       const unsigned long long mk = bal(bin == kb);
       todo &= ~mk;
       if (boff) {  // a light-grid cell
-        list_search<COUNT>(p, bent, cp(boff)[kb], cp(boff)[kb + 1], ro, rd, ex, stop, key, tc, ws);
+        list_search<COUNT>(p, bent, cp(boff)[kb], cp(boff)[kb + 1], ro, rd, ex, stop, key, tc, ws, lb);
       } else {     // a pixel list (rt_frame.h slots); past its slots the BVH serves the pixel
         const int n = (int)(at(p->pix_cnt, kb) & kPixCount), b = kb << p->slot_lg;
         if (n > (1 << p->slot_lg)) ovf |= mk;
-        else list_search<COUNT>(p, bent, b, b + n, ro, rd, ex, stop, key, tc, ws);
+        else list_search<COUNT>(p, bent, b, b + n, ro, rd, ex, stop, key, tc, ws, lb);
       }
     }
     // done: binned lanes (their bin was searched) and lanes off the grid
     tc = (lane_in(todo | ovf) || !(bin >= 0 || nohit)) ? tc : -1.0f;
   }
-  traverse<COUNT>(p, ob.root, ro, rd, sr, ex, stop, key, tc, ws);
+  traverse<COUNT>(p, ob.root, ro, rd, sr, ex, stop, key, tc, ws, lb);
   return key;
 }
 
@@ -1620,6 +1685,15 @@ __device__ __forceinline__ void tri_test_t(const TR& T, F3 o, F3 d, float& best,
   tc = acc ? ts : tc;
 }
 
+// tri_test_t on a face's LTri record (shadow rays to a light with records)
+template <class LR>
+__device__ __forceinline__ void ltri_test_t(const LR& L, F3 o, float& best, float& tc) {
+  const float ts = ltri_t(L, o);
+  const bool acc = __float_as_uint(ts) < __float_as_uint(best);
+  best = acc ? ts : best;
+  tc = acc ? ts : tc;
+}
+
 // The faces listed at ent[b, e) against the rays of the batch's samples
 // whose bit is set in fl (wave-uniform), each face record fetched once for
 // all of them. Camera rays (KEY): list_search's (t, face) key. Shadow rays
@@ -1636,11 +1710,15 @@ __device__ __forceinline__ void tri_test_t(const TR& T, F3 o, F3 d, float& best,
 #ifndef RTMI_LDS_STAGE
 #define RTMI_LDS_STAGE 1
 #endif
+// Shadow searches (!KEY) test the light's LTri records at lb (lrec_of:
+// every light with a grid has them), camera searches (KEY) the TriFast
+// records of the tree.
 template <int S, bool KEY>
 __device__ __forceinline__ int list_search_batch(KP p, const int32_t* ent, int b, int e, unsigned fl,
                                                   const F3 (&ro)[S], const F3 (&rd)[S], const float (&stop)[S],
                                                   const unsigned long long (&own)[S], unsigned long long (&key)[S],
-                                                  float (&best)[S], float (&tc)[S], unsigned* diag = nullptr) {
+                                                  float (&best)[S], float (&tc)[S], unsigned* diag = nullptr,
+                                                  const char* lb = nullptr) {
   const int b_in = b;  // returns the number of faces tested (diagnostics)
   auto lanes = [&]() {
     if (diag) {
@@ -1653,13 +1731,13 @@ __device__ __forceinline__ int list_search_batch(KP p, const int32_t* ent, int b
     // a cell's first face alone: it is the one covering most of the cell
     // (rt_bins.cpp), so lanes in the umbra retire after one test
     if (b < e) {
-      const TriRegs T = load_tri(rec<TriFast>(p, cp(ent)[b]));
+      const LRegs T = load_ltri((const RT_CONST LTri*)(lb + (unsigned)cp(ent)[b]));
       lanes();
       unsigned long long left = 0ull;
 #pragma unroll
       for (int k = 0; k < S; ++k)
         if ((fl >> k) & 1u) {
-          tri_test_t(T, ro[k], rd[k], best[k], tc[k]);
+          ltri_test_t(T, ro[k], best[k], tc[k]);
           tc[k] = tc[k] <= stop[k] ? -1.0f : tc[k];
           left |= bal(tc[k] >= 0.0f) & own[k];
         }
@@ -1686,32 +1764,50 @@ __device__ __forceinline__ int list_search_batch(KP p, const int32_t* ent, int b
     if constexpr (kStage) {
       const int lane = (int)__lane_id(), j = lane >> 4, w = lane & 15;
       const int rj = j == 0 ? r[0] : j == 1 ? r[1] : j == 2 ? r[2] : r[3];
-      const unsigned int* src = (const unsigned int*)((const char*)p->tree + (unsigned)rj);
+      const unsigned int* src = (const unsigned int*)((KEY ? (const char*)p->tree : lb) + (unsigned)rj);
       ((unsigned int*)stage)[lane] = k0 + j < e ? src[w] : 0u;
       __builtin_amdgcn_wave_barrier();
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       if (j > 0 && k0 + j >= e) break;
-      TriRegs T;
-      if constexpr (kStage) {
-        const uint4 a = stage[4 * j + 0], bq = stage[4 * j + 1], c = stage[4 * j + 2], d4 = stage[4 * j + 3];
-        T.v0[0] = __uint_as_float(a.x), T.v0[1] = __uint_as_float(a.y), T.v0[2] = __uint_as_float(a.z);
-        T.id = a.w;
-        T.e2[0] = __uint_as_float(bq.x), T.e2[1] = __uint_as_float(bq.y), T.e2[2] = __uint_as_float(bq.z);
-        T.e1n[0] = __uint_as_float(c.x), T.e1n[1] = __uint_as_float(c.y), T.e1n[2] = __uint_as_float(c.z);
-        T.nn[0] = __uint_as_float(d4.x), T.nn[1] = __uint_as_float(d4.y), T.nn[2] = __uint_as_float(d4.z);
-      } else {
-        (void)stage;
-        T = load_tri(rec<TriFast>(p, r[j]));
-      }
-      lanes();
-#pragma unroll
-      for (int k = 0; k < S; ++k)
-        if ((fl >> k) & 1u) {
-          if constexpr (KEY) tri_test(T, ro[k], rd[k], key[k], tc[k]);
-          else tri_test_t(T, ro[k], rd[k], best[k], tc[k]);
+      if constexpr (KEY) {
+        TriRegs T;
+        if constexpr (kStage) {
+          const uint4 a = stage[4 * j + 0], bq = stage[4 * j + 1], c = stage[4 * j + 2], d4 = stage[4 * j + 3];
+          T.v0[0] = __uint_as_float(a.x), T.v0[1] = __uint_as_float(a.y), T.v0[2] = __uint_as_float(a.z);
+          T.id = a.w;
+          T.e2[0] = __uint_as_float(bq.x), T.e2[1] = __uint_as_float(bq.y), T.e2[2] = __uint_as_float(bq.z);
+          T.e1n[0] = __uint_as_float(c.x), T.e1n[1] = __uint_as_float(c.y), T.e1n[2] = __uint_as_float(c.z);
+          T.nn[0] = __uint_as_float(d4.x), T.nn[1] = __uint_as_float(d4.y), T.nn[2] = __uint_as_float(d4.z);
+        } else {
+          (void)stage;
+          T = load_tri(rec<TriFast>(p, r[j]));
         }
+        lanes();
+#pragma unroll
+        for (int k = 0; k < S; ++k)
+          if ((fl >> k) & 1u) tri_test(T, ro[k], rd[k], key[k], tc[k]);
+      } else {
+        LRegs T;
+        if constexpr (kStage) {
+          const uint4 a = stage[4 * j + 0], bq = stage[4 * j + 1], c = stage[4 * j + 2], d4 = stage[4 * j + 3];
+          T.p[0] = __uint_as_float(a.x), T.p[1] = __uint_as_float(a.y), T.p[2] = __uint_as_float(a.z);
+          T.cu = __uint_as_float(a.w);
+          T.q[0] = __uint_as_float(bq.x), T.q[1] = __uint_as_float(bq.y), T.q[2] = __uint_as_float(bq.z);
+          T.cv = __uint_as_float(bq.w);
+          T.tv[0] = __uint_as_float(c.x), T.tv[1] = __uint_as_float(c.y), T.tv[2] = __uint_as_float(c.z);
+          T.ct = __uint_as_float(c.w);
+          T.id = d4.x;
+        } else {
+          (void)stage;
+          T = load_ltri((const RT_CONST LTri*)(lb + (unsigned)r[j]));
+        }
+        lanes();
+#pragma unroll
+        for (int k = 0; k < S; ++k)
+          if ((fl >> k) & 1u) ltri_test_t(T, ro[k], best[k], tc[k]);
+      }
     }
     if constexpr (!KEY) {
       unsigned long long left = 0ull;
@@ -1989,7 +2085,7 @@ __device__ __forceinline__ bool gen_batch(KP p, const GroupPix& gp, int it0, con
           wi.v[STAT_TRI_FETCH] += (unsigned)(cp(p->grid_off)[kb + 1] - cp(p->grid_off)[kb]) * (unsigned)__builtin_popcount(fl);
 #endif
           list_search_batch<S, false>(p, bent, cp(p->grid_off)[kb], cp(p->grid_off)[kb + 1], fl, ro, rd, stop,
-                                      own, unused, best, tc);
+                                      own, unused, best, tc, nullptr, lrec_of(p, li));
         }
 #pragma unroll
         for (int k = 0; k < S; ++k) {  // found => 0 <= t < ts: the hit counts
@@ -2330,12 +2426,12 @@ __device__ __forceinline__ bool gen1_batch(KP p, const GroupPix& gp, int pu, int
 #ifdef RTMI_DIAG_LANES
               unsigned dl = 0u;
               const int nt = list_search_batch<1, false>(q, bent, cp(q->grid_off)[kb], cp(q->grid_off)[kb + 1], 1u, ro_c,
-                                                         rd_c, stop_c, own_c, key_c, best_c, tc_c, &dl);
+                                                         rd_c, stop_c, own_c, key_c, best_c, tc_c, &dl, lrec_of(q, li));
               wi.v[STAT_NODE_FETCH] += (unsigned)nt;
               wi.v[STAT_LANE_NODES] += dl;
 #else
               (void)list_search_batch<1, false>(q, bent, cp(q->grid_off)[kb], cp(q->grid_off)[kb + 1], 1u, ro_c, rd_c,
-                                                stop_c, own_c, key_c, best_c, tc_c);
+                                                stop_c, own_c, key_c, best_c, tc_c, nullptr, lrec_of(q, li));
 #endif
               // back: slot 0 in place, sample 1's rays from the lane they moved to
               const float b1 = __int_as_float(__builtin_amdgcn_ds_bpermute(to << 2, __float_as_int(best_c[0])));
@@ -2352,12 +2448,12 @@ __device__ __forceinline__ bool gen1_batch(KP p, const GroupPix& gp, int pu, int
 #ifdef RTMI_DIAG_LANES  // diagnostic: shadow face tests (x flagged samples) and the lanes still searching
           unsigned dl = 0u;
           const int nt = list_search_batch<S, false>(q, bent, cp(q->grid_off)[kb], cp(q->grid_off)[kb + 1], fl, ro, rd,
-                                                     stop, own, unused, best, tc, &dl);
+                                                     stop, own, unused, best, tc, &dl, lrec_of(q, li));
           wi.v[STAT_NODE_FETCH] += (unsigned)nt * (unsigned)__builtin_popcount(fl);
           wi.v[STAT_LANE_NODES] += dl;
 #else
           const int nt = list_search_batch<S, false>(q, bent, cp(q->grid_off)[kb], cp(q->grid_off)[kb + 1], fl, ro, rd,
-                                                     stop, own, unused, best, tc);
+                                                     stop, own, unused, best, tc, nullptr, lrec_of(q, li));
 #endif
 #ifdef RTMI_DIAG_GEN_COUNT
           wi.v[STAT_NODE_FETCH] += 1u;                                      // diagnostic: cells searched

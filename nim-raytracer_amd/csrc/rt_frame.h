@@ -95,7 +95,7 @@ __host__ __device__ inline int frame_row(const FrameRows& r, int k) {
 struct DevBinTri {
   double v[3][3];
   int32_t rec;
-  int32_t pad;
+  int32_t face;
 };
 
 // frame counters (one small device array). FC_HUGE0 / FC_HUGE1: the huge-face

@@ -151,6 +151,42 @@ inline int slot_lg_for(int w, int h) {
   return lg;
 }
 
+// LTri (rt_common.h) of face v for the shadow direction d (mesh object
+// space, float64): p, q, tv rounded to float32 first, the constants formed
+// from the ROUNDED vectors (u(v0) = 0 up to the float64 sum), so each affine
+// function keeps its zero at the face's vertex.
+static void make_ltri(const double v[3][3], const double d[3], int32_t face, LTri* out) {
+  double e1[3], e2[3], cr[3], nn[3], p[3], q[3], me1[3];
+  for (int k = 0; k < 3; ++k) {
+    e1[k] = v[1][k] - v[0][k];
+    e2[k] = v[2][k] - v[0][k];
+    me1[k] = -e1[k];
+  }
+  rtmi::bg::cross3(e1, e2, cr);
+  for (int k = 0; k < 3; ++k) nn[k] = -cr[k];
+  const double det = rtmi::bg::dot3(nn, d);
+  std::memset(out, 0, sizeof *out);
+  out->id = face;
+  if (!(det >= 1e-6)) {  // geom.nim:306: never passes for this light
+    out->cu = out->cv = out->ct = -1.0f;
+    return;
+  }
+  rtmi::bg::cross3(d, e2, p);
+  rtmi::bg::cross3(d, me1, q);
+  double pr[3], qr[3], tr[3];
+  for (int k = 0; k < 3; ++k) {
+    out->p[k] = (float)(p[k] / det);
+    out->q[k] = (float)(q[k] / det);
+    out->tv[k] = (float)(nn[k] / -det);
+    pr[k] = out->p[k];
+    qr[k] = out->q[k];
+    tr[k] = out->tv[k];
+  }
+  out->cu = (float)-rtmi::bg::dot3(pr, v[0]);
+  out->cv = (float)-rtmi::bg::dot3(qr, v[0]);
+  out->ct = (float)-rtmi::bg::dot3(tr, v[0]);
+}
+
 struct rt_scene {
   std::mutex mu;
   int device = 0;
@@ -230,6 +266,11 @@ struct rt_scene {
   double mesh_o2w[16], mesh_w2o[16];
   bool binnable = false;
   DevBuf<LightGrid> grids;         // per light (gu == 0: none)
+  // per light with a grid: every face's shadow-test record for that light's
+  // fixed direction (rt_common.h LTri, leaf order, ntri per light)
+  DevBuf<LTri> lrec;
+  int64_t lrec_ntri = 0;
+  uint32_t lrec_mask = 0;          // the lights that have records
   DevBuf<int32_t> grid_off, grid_ent;
   bool has_grids = false;
   // shadow skips (rt_bins.h): scenes of the one mesh and planes
@@ -295,6 +336,7 @@ struct rt_scene {
     f64_tables.release();
     fb_scratch.release();
     grids.release();
+    lrec.release();
     grid_off.release();
     grid_ent.release();
     obj_grids.release();
@@ -902,6 +944,7 @@ extern "C" int rt_scene_create(const rt_scene_desc* d, rt_scene** out_scene) {
         for (int v = 0; v < 3; ++v)
           for (int k = 0; k < 3; ++k) t.v[v][k] = md.vertices[3 * (size_t)fi[v] + k];
         t.rec = (int32_t)((nnodes + base + i) * (int64_t)sizeof(TriFast));
+        t.face = order[(size_t)i];
       }
     });
     std::memcpy(s->mesh_o2w, ob.object_to_world, sizeof s->mesh_o2w);
@@ -944,6 +987,30 @@ extern "C" int rt_scene_create(const rt_scene_desc* d, rt_scene** out_scene) {
     if (any) {
       if ((rc = s->grids.upload(gh)) || (rc = s->grid_off.upload(goff)) || (rc = s->grid_ent.upload(gent))) return rc;
       s->has_grids = true;
+      // the shadow-test records of the lights with a grid (the float32
+      // kernels' every shadow ray to such a light tests these, on every path)
+      {
+        const size_t nt = (size_t)ntri;  // indexed like the TriFast records: byte offset / 64 - nnodes
+        std::vector<LTri> lr((size_t)d->num_lights * nt);
+        for (int li = 0; li < d->num_lights; ++li) {
+          if (gh[(size_t)li].gu <= 0) continue;
+          const double* dir = d->lights[li].dir;
+          double sd[3], ld[3];
+          for (int k = 0; k < 3; ++k) sd[k] = -dir[k];
+          bg::xform_dir(s->mesh_w2o, sd, ld);  // the shadow direction in the mesh's object space
+          parallel_for((int64_t)nt, [&](int64_t b, int64_t e) {
+            for (int64_t i = b; i < e; ++i) {
+              const BinTri& t = s->bin_tris[(size_t)i];
+              const int64_t slot = (int64_t)t.rec / (int64_t)sizeof(TriFast) - nnodes;
+              make_ltri(t.v, ld, t.face, &lr[(size_t)li * nt + (size_t)slot]);
+            }
+          });
+        }
+        if ((rc = s->lrec.upload(lr))) return rc;
+        s->lrec_ntri = (int64_t)nt;
+        for (int li = 0; li < d->num_lights && li < 32; ++li)
+          if (gh[(size_t)li].gu > 0) s->lrec_mask |= 1u << li;
+      }
       // shadow skips: every other object a plane
       s->skippable = true;
       for (int i = 0; i < d->num_objects; ++i) {
@@ -1626,6 +1693,13 @@ int fill_fast(rt_scene* s, const rt_options* o, const Mapping& mp, float* fb, Fa
   }
   // binned searches (rt_bins.h): camera rays when a wave spans at most 4
   // pixels (>= 16 samples per pixel), shadow rays to distant lights
+  // the shadow-ray records: on every path (binned or not), so every path
+  // tests a distant light's shadow rays with the same arithmetic
+  if (s->lrec.p) {
+    p.lrec_base = (uint64_t)(uintptr_t)s->lrec.p - (uint64_t)s->num_nodes * sizeof(TriFast);
+    p.lrec_stride = s->lrec_ntri * (int64_t)sizeof(LTri);
+    p.lrec_mask = s->lrec_mask;
+  }
   const bool binning = !(o->flags & RT_FLAG_NO_BINNING);
   if (binning) {
     if (s->has_grids) {
