@@ -2584,6 +2584,20 @@ __device__ __forceinline__ void finish_item(KP p, const GroupPix& gp, F3 acc, in
   }
 }
 
+// k_render_fast's item order: shard k hands out runs of RTMI_FAST_RUN
+// consecutive pixel groups (k, k + shards, ... in runs), so a run of tiles —
+// 32 pixels of a row for the 2 x 2 tiles of a 16-lane-per-pixel launch, i.e.
+// three whole 128-B framebuffer lines — is written by waves of ONE XCD (the
+// shard's blocks, blockIdx % shards), and a shard's waves share its pixels'
+// object masks in their XCD's L2. Scheduling only (C2: 0.805 -> 0.794 ms,
+// HBM 213 -> 87 MB per call).
+#ifndef RTMI_FAST_RUN
+#define RTMI_FAST_RUN 16
+#endif
+__device__ __forceinline__ int fast_item(int qj, int shards, int shard) {
+  return (qj / RTMI_FAST_RUN * shards + shard) * RTMI_FAST_RUN + qj % RTMI_FAST_RUN;
+}
+
 template <bool COUNT, unsigned F>
 // (the instrumented COUNT launch — bench.py's one traversal-counting call —
 // carries more counters: 4 waves per SIMD keeps it spill-free too)
@@ -2625,7 +2639,7 @@ k_render_fast(const FastParams params_by_value) {
   int qj_next2 = 0;
   if (__lane_id() == 0) qj_next2 = (int)atomicAdd(head, 1u);
 #endif
-  int g = qj * p->shards + shard;
+  int g = fast_item(qj, p->shards, shard);
   int nflush = 0;
   const int ngroups = list_items(p->list_n, p->ngroups, 1);
   while (g < ngroups) {
@@ -2733,7 +2747,7 @@ k_render_fast(const FastParams params_by_value) {
 #else
     if (lane == 0) qj_next = (int)atomicAdd(head, 1u);
 #endif
-    g = qj * p->shards + shard;
+    g = fast_item(qj, p->shards, shard);
   }
   p = params();
   const int lane = (int)__lane_id();

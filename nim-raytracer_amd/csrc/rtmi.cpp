@@ -2499,6 +2499,16 @@ extern "C" int64_t rtmi_test_frame_lists(rt_scene* s, int32_t* off, int32_t* ent
   return std::min<int64_t>(n, ent_cap);
 }
 
+// Test hook: the LTri record (rt_common.h) of triangle v9 (v0, v1, v2 as 9
+// doubles, mesh object space) for the shadow direction d (float64), as
+// rt_scene_create builds it; out: 16 words.
+extern "C" int rtmi_test_ltri(const double* v9, const double* d, int32_t face, void* out) {
+  if (!v9 || !d || !out) return fail(RT_E_INVALID, "null argument");
+  const double v[3][3] = {{v9[0], v9[1], v9[2]}, {v9[3], v9[4], v9[5]}, {v9[6], v9[7], v9[8]}};
+  make_ltri(v, d, face, (LTri*)out);
+  return RT_OK;
+}
+
 // Test hook: the last call's pixel records (w*h words, rt_frame.h: list
 // length | shadow skip bits << 24; only the call's pixels are defined).
 extern "C" int rtmi_test_pixel_info(rt_scene* s, uint32_t* info) {

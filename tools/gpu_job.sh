@@ -7,7 +7,7 @@
 # nothing runs after a failure (outputs under gpurun_out/$OUT):
 #   tests            pytest -m gpu over $TESTS (default: tests)
 #   bench:CFG[:fp64] one bench.py line (--config CFG, $BENCH_ARGS) -> bench_<cfg>[_fp64].json
-#   prof:CFG[:fp64]  rocprofv3 --kernel-trace --stats of that bench command -> prof_<cfg>/
+#   prof:CFG[:fp64]  rocprofv3 --kernel-trace --stats of that bench command ($PROF_ARGS) -> prof_<cfg>/
 #   pmc:CFG[:fp64]   three PMC passes (FETCH_SIZE / WRITE_SIZE / SQ issue counters),
 #                    one counter group per run -> pmc_<cfg>[_fp64]/ (summarise on the CPU:
 #                    python tools/pmc_summary.py gpurun_out/$OUT/pmc_<cfg> <workload key>)
@@ -41,7 +41,7 @@ for st in ${STAGES:-tests}; do
       cat $O/bench_$c$sfx.json ;;
     prof)
       timeout -k 10 $T rocprofv3 --kernel-trace --stats -d $O/prof_$c$sfx -o p -f csv -- python3 bench.py --config ${cfg:-C3} $pa \
-        --steps ${PROF_STEPS:-5} --warmup 1 --no-cpu > $O/prof_$c$sfx.json 2> $O/prof_$c$sfx.err || { tail -20 $O/prof_$c$sfx.err; exit 1; }
+        --steps ${PROF_STEPS:-5} --warmup 1 --no-cpu ${PROF_ARGS:-} > $O/prof_$c$sfx.json 2> $O/prof_$c$sfx.err || { tail -20 $O/prof_$c$sfx.err; exit 1; }
       cat $O/prof_$c$sfx.json ;;
     pmc)
       P=$O/pmc_$c$sfx
