@@ -918,11 +918,13 @@ __global__ __launch_bounds__(256, RTMI_MIN_WAVES) void k_render(const RenderPara
 // dependent adds, P chains side by side) before the next step overwrites
 // the rows. Rows are padded to 65 doubles so the summing lanes' reads fall
 // in different banks.
+// (the reflective instantiation — LEVELS > 1, shade_path's per-level state
+// — runs at 2 waves per SIMD: at 3 it spilled 71 VGPRs, 336 B per lane)
 #ifndef RTMI_PX64_WAVES
 #define RTMI_PX64_WAVES 3
 #endif
 template <int P, int LEVELS>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RTMI_PX64_WAVES))) void k_render_px64(const RenderParams<double> params_by_value) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVELS > 1 ? 2 : RTMI_PX64_WAVES))) void k_render_px64(const RenderParams<double> params_by_value) {
   using R = double;
   (void)params_by_value;  // read through rparams()
   const RT_CONST RenderParams<R>& p = rparams<R>();

@@ -2571,6 +2571,9 @@ __device__ __forceinline__ void finish_item(KP p, const GroupPix& gp, F3 acc, in
   if (gp.valid && gp.sub == 0) {
     if (p->aa_kind != 0) acc = f3(acc.x * p->inv_len, acc.y * p->inv_len, acc.z * p->inv_len);
     if (p->mode == 0 && p->step > 1) {
+      // (every field re-read here: the progressive fill is rare, and operands
+      // kept from the test above stayed live across the caller's item loop)
+      p = params();
       const int xe = min(gp.x + p->step, p->width), ye = min(gp.y + p->step, p->height);
       for (int yy = gp.y; yy < ye; ++yy)
         for (int xx = gp.x; xx < xe; ++xx) {
@@ -3224,6 +3227,7 @@ template <int RUN = 1>
 struct WorkQ {
   unsigned int* queue;
   int shards, n, cur, left, lo, len, qj_next, head;
+
   __device__ __forceinline__ void bounds() {
 #if RTMI_XCD_CHUNK
     lo = (int)(((long long)cur * n) / shards);
@@ -3236,10 +3240,14 @@ struct WorkQ {
     len = n;
 #endif
   }
+  // (scalar at once: the compiler's atomic optimizer already waits for the
+  // atomic and reads its result with readfirstlane where it is issued, so a
+  // per-lane copy bought no latency hiding — it only held a VGPR across the
+  // item, which k_render_mix1 spilled)
   __device__ __forceinline__ int reserve() {
     int q = 0;
     if (__lane_id() == 0) q = (int)atomicAdd(queue + head * kQueueStride, 1u);
-    return q;
+    return __builtin_amdgcn_readfirstlane(q);
   }
   __device__ __forceinline__ int item(int qj) const {
 #if RTMI_XCD_CHUNK
@@ -3726,7 +3734,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RTMI_GEN1_W
   KP p = params();
   __shared__ float lds[4][kLdsSlots][64];  // shade_path's scratch (the fallback)
   __shared__ unsigned long long lds_tot[4][kStatSlots];
-  const int wib = (int)(threadIdx.x >> 6);
+  // the wave's index in its block as a scalar (from threadIdx.x it stayed a
+  // VGPR live across the whole item loop and spilled, as did the LDS address
+  // of lds_tot[wib] formed from it)
+  const int wib = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   LdsF* ls = (LdsF*)&lds[wib][0][__lane_id()];
   if (__lane_id() < (unsigned)kStatSlots) lds_tot[wib][__lane_id()] = 0ull;
   Stats32 ws;
@@ -3737,7 +3748,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RTMI_GEN1_W
   p = params();
   const int lane = (int)__lane_id();
   flush_stats(ws, lds_tot[wib], lane);
-  const int wave = (int)(blockIdx.x * (blockDim.x >> 6) + threadIdx.x / 64u);
+  const int wave = (int)(blockIdx.x * 4u) + wib;  // (256-thread blocks)
   if (lane < kStatSlots) p->partials[(size_t)wave * kStatSlots + lane] = lds_tot[wib][lane];
 }
 
@@ -3755,7 +3766,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RTMI_GEN1_W
   KP p = params();
   __shared__ float lds[4][kLdsSlots][64];
   __shared__ unsigned long long lds_tot[4][kStatSlots];
-  const int wib = (int)(threadIdx.x >> 6);
+  // the wave's index in its block as a scalar (from threadIdx.x it stayed a
+  // VGPR live across the whole item loop and spilled, as did the LDS address
+  // of lds_tot[wib] formed from it)
+  const int wib = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   LdsF* ls = (LdsF*)&lds[wib][0][__lane_id()];
   if (__lane_id() < (unsigned)kStatSlots) lds_tot[wib][__lane_id()] = 0ull;
   Stats32 ws;
@@ -3769,7 +3783,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RTMI_GEN1_W
   p = params();
   const int lane = (int)__lane_id();
   flush_stats(ws, lds_tot[wib], lane);
-  const int wave = (int)(blockIdx.x * (blockDim.x >> 6) + threadIdx.x / 64u);
+  const int wave = (int)(blockIdx.x * 4u) + wib;  // (256-thread blocks)
   if (lane < kStatSlots) p->partials[(size_t)wave * kStatSlots + lane] = lds_tot[wib][lane];
 }
 
