@@ -236,6 +236,7 @@ struct alignas(16) FLight {
 // light l (l < 8). kPixCount alone: nothing known about the pixel.
 constexpr uint32_t kPixCount = 0x00FFFFFFu;
 
+struct LTri;
 struct FastParams {
   const FObj* objs;
   const FObjX* objx;
@@ -307,6 +308,11 @@ struct FastParams {
   int64_t lrec_stride;
   uint32_t lrec_mask;
   int32_t pad_lrec;
+  // the same records in light-grid entry order: grid_rec[e] is the LTri of
+  // the face grid_ent[e] names (for its grid's light), so a cell search reads
+  // its faces' records straight from the cell's range — one load per step
+  // instead of the entry, then the record it names; nullptr: via grid_ent
+  const LTri* grid_rec;
 };
 // A face's shadow-ray test for one distant light (fixed direction d, mesh
 // object space), prepared in float64 by the host (rtmi.cpp make_ltri): with

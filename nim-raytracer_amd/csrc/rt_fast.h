@@ -291,6 +291,15 @@ __device__ __forceinline__ const char* lrec_of(KP p, int light) {
   return (const char*)(p->lrec_base + (uint64_t)light * (uint64_t)p->lrec_stride);
 }
 
+#ifndef RTMI_GRID_REC
+#define RTMI_GRID_REC 1
+#endif
+// The cell-ordered records of a light's grid, aligned with its entries
+// (p->grid_ent + G.ent_base): list_search_batch's lb under RTMI_GRID_REC.
+__device__ __forceinline__ const char* grid_rec_of(KP p, int light, const LightGrid& G) {
+  return RTMI_GRID_REC ? (const char*)(p->grid_rec + G.ent_base) : lrec_of(p, light);
+}
+
 // A record of the float32 tree (FastParams.tree) at a byte offset: one scalar
 // base + a 32-bit SGPR offset (s_load ... soffset), no 64-bit address
 // arithmetic on the traversal's dependent chain.
@@ -1712,13 +1721,21 @@ __device__ __forceinline__ void ltri_test_t(const LR& L, F3 o, float& best, floa
 #endif
 // Shadow searches (!KEY) test the light's LTri records at lb (lrec_of:
 // every light with a grid has them), camera searches (KEY) the TriFast
-// records of the tree.
+// records of the tree. RTMI_GRID_REC (default 1): a shadow search reads the
+// records in entry order instead, lb = the cell-ordered copy aligned with
+// `ent` (grid_rec_of: entry k's record at lb + 64 k) — one load per step,
+// not the entries and then the records they name; 0 for the A/B.
 template <int S, bool KEY>
 __device__ __forceinline__ int list_search_batch(KP p, const int32_t* ent, int b, int e, unsigned fl,
                                                   const F3 (&ro)[S], const F3 (&rd)[S], const float (&stop)[S],
                                                   const unsigned long long (&own)[S], unsigned long long (&key)[S],
                                                   float (&best)[S], float (&tc)[S], unsigned* diag = nullptr,
                                                   const char* lb = nullptr) {
+  constexpr bool kCellRec = !KEY && RTMI_GRID_REC;
+  // the record of entry k
+  auto rec_at = [&](int k) -> const char* {
+    return kCellRec ? lb + (size_t)(unsigned)k * sizeof(LTri) : lb + (unsigned)cp(ent)[k];
+  };
   const int b_in = b;  // returns the number of faces tested (diagnostics)
   auto lanes = [&]() {
     if (diag) {
@@ -1731,7 +1748,7 @@ __device__ __forceinline__ int list_search_batch(KP p, const int32_t* ent, int b
     // a cell's first face alone: it is the one covering most of the cell
     // (rt_bins.cpp), so lanes in the umbra retire after one test
     if (b < e) {
-      const LRegs T = load_ltri((const RT_CONST LTri*)(lb + (unsigned)cp(ent)[b]));
+      const LRegs T = load_ltri((const RT_CONST LTri*)rec_at(b));
       lanes();
       unsigned long long left = 0ull;
 #pragma unroll
@@ -1759,13 +1776,21 @@ __device__ __forceinline__ int list_search_batch(KP p, const int32_t* ent, int b
   uint4* stage = nullptr;
 #endif
   for (int k0 = b; k0 < e; k0 += 4) {
-    const RT_CONST int32_t* q = cp(ent) + k0;
-    const int r[4] = {q[0], q[1], q[2], q[3]};
+    int r[4] = {0, 0, 0, 0};
+    if constexpr (!kCellRec) {
+      const RT_CONST int32_t* q = cp(ent) + k0;
+      r[0] = q[0], r[1] = q[1], r[2] = q[2], r[3] = q[3];
+    }
     if constexpr (kStage) {
       const int lane = (int)__lane_id(), j = lane >> 4, w = lane & 15;
-      const int rj = j == 0 ? r[0] : j == 1 ? r[1] : j == 2 ? r[2] : r[3];
-      const unsigned int* src = (const unsigned int*)((KEY ? (const char*)p->tree : lb) + (unsigned)rj);
-      ((unsigned int*)stage)[lane] = k0 + j < e ? src[w] : 0u;
+      if constexpr (kCellRec) {  // the step's four records are 256 contiguous bytes
+        const unsigned int* src = (const unsigned int*)rec_at(k0);
+        ((unsigned int*)stage)[lane] = k0 + j < e ? src[lane] : 0u;
+      } else {
+        const int rj = j == 0 ? r[0] : j == 1 ? r[1] : j == 2 ? r[2] : r[3];
+        const unsigned int* src = (const unsigned int*)((KEY ? (const char*)p->tree : lb) + (unsigned)rj);
+        ((unsigned int*)stage)[lane] = k0 + j < e ? src[w] : 0u;
+      }
       __builtin_amdgcn_wave_barrier();
     }
 #pragma unroll
@@ -1801,7 +1826,7 @@ __device__ __forceinline__ int list_search_batch(KP p, const int32_t* ent, int b
           T.id = d4.x;
         } else {
           (void)stage;
-          T = load_ltri((const RT_CONST LTri*)(lb + (unsigned)r[j]));
+          T = load_ltri((const RT_CONST LTri*)(kCellRec ? rec_at(k0 + j) : lb + (unsigned)r[j]));
         }
         lanes();
 #pragma unroll
@@ -2085,7 +2110,7 @@ __device__ __forceinline__ bool gen_batch(KP p, const GroupPix& gp, int it0, con
           wi.v[STAT_TRI_FETCH] += (unsigned)(cp(p->grid_off)[kb + 1] - cp(p->grid_off)[kb]) * (unsigned)__builtin_popcount(fl);
 #endif
           list_search_batch<S, false>(p, bent, cp(p->grid_off)[kb], cp(p->grid_off)[kb + 1], fl, ro, rd, stop,
-                                      own, unused, best, tc, nullptr, lrec_of(p, li));
+                                      own, unused, best, tc, nullptr, grid_rec_of(p, li, G));
         }
 #pragma unroll
         for (int k = 0; k < S; ++k) {  // found => 0 <= t < ts: the hit counts
@@ -2426,12 +2451,12 @@ __device__ __forceinline__ bool gen1_batch(KP p, const GroupPix& gp, int pu, int
 #ifdef RTMI_DIAG_LANES
               unsigned dl = 0u;
               const int nt = list_search_batch<1, false>(q, bent, cp(q->grid_off)[kb], cp(q->grid_off)[kb + 1], 1u, ro_c,
-                                                         rd_c, stop_c, own_c, key_c, best_c, tc_c, &dl, lrec_of(q, li));
+                                                         rd_c, stop_c, own_c, key_c, best_c, tc_c, &dl, grid_rec_of(q, li, G));
               wi.v[STAT_NODE_FETCH] += (unsigned)nt;
               wi.v[STAT_LANE_NODES] += dl;
 #else
               (void)list_search_batch<1, false>(q, bent, cp(q->grid_off)[kb], cp(q->grid_off)[kb + 1], 1u, ro_c, rd_c,
-                                                stop_c, own_c, key_c, best_c, tc_c, nullptr, lrec_of(q, li));
+                                                stop_c, own_c, key_c, best_c, tc_c, nullptr, grid_rec_of(q, li, G));
 #endif
               // back: slot 0 in place, sample 1's rays from the lane they moved to
               const float b1 = __int_as_float(__builtin_amdgcn_ds_bpermute(to << 2, __float_as_int(best_c[0])));
@@ -2448,12 +2473,12 @@ __device__ __forceinline__ bool gen1_batch(KP p, const GroupPix& gp, int pu, int
 #ifdef RTMI_DIAG_LANES  // diagnostic: shadow face tests (x flagged samples) and the lanes still searching
           unsigned dl = 0u;
           const int nt = list_search_batch<S, false>(q, bent, cp(q->grid_off)[kb], cp(q->grid_off)[kb + 1], fl, ro, rd,
-                                                     stop, own, unused, best, tc, &dl, lrec_of(q, li));
+                                                     stop, own, unused, best, tc, &dl, grid_rec_of(q, li, G));
           wi.v[STAT_NODE_FETCH] += (unsigned)nt * (unsigned)__builtin_popcount(fl);
           wi.v[STAT_LANE_NODES] += dl;
 #else
           const int nt = list_search_batch<S, false>(q, bent, cp(q->grid_off)[kb], cp(q->grid_off)[kb + 1], fl, ro, rd,
-                                                     stop, own, unused, best, tc, nullptr, lrec_of(q, li));
+                                                     stop, own, unused, best, tc, nullptr, grid_rec_of(q, li, G));
 #endif
 #ifdef RTMI_DIAG_GEN_COUNT
           wi.v[STAT_NODE_FETCH] += 1u;                                      // diagnostic: cells searched

@@ -269,6 +269,7 @@ struct rt_scene {
   // per light with a grid: every face's shadow-test record for that light's
   // fixed direction (rt_common.h LTri, leaf order, ntri per light)
   DevBuf<LTri> lrec;
+  DevBuf<LTri> grec;               // lrec in light-grid entry order (FastParams.grid_rec)
   int64_t lrec_ntri = 0;
   uint32_t lrec_mask = 0;          // the lights that have records
   DevBuf<int32_t> grid_off, grid_ent;
@@ -337,6 +338,7 @@ struct rt_scene {
     fb_scratch.release();
     grids.release();
     lrec.release();
+    grec.release();
     grid_off.release();
     grid_ent.release();
     obj_grids.release();
@@ -1008,6 +1010,20 @@ extern "C" int rt_scene_create(const rt_scene_desc* d, rt_scene** out_scene) {
         }
         if ((rc = s->lrec.upload(lr))) return rc;
         s->lrec_ntri = (int64_t)nt;
+        // the cell-ordered copy: entry e of light li's grid -> its face's record
+        std::vector<LTri> gr(gent.size());
+        for (int li = 0; li < d->num_lights; ++li) {
+          if (gh[(size_t)li].gu <= 0) continue;
+          const LightGridHost& lg = s->grid_host[(size_t)li];
+          const size_t e0 = (size_t)gh[(size_t)li].ent_base, ne = lg.ent.size();
+          parallel_for((int64_t)ne, [&](int64_t b, int64_t e) {
+            for (int64_t k = b; k < e; ++k) {
+              const int64_t slot = (int64_t)gent[e0 + (size_t)k] / (int64_t)sizeof(TriFast) - nnodes;
+              gr[e0 + (size_t)k] = lr[(size_t)li * nt + (size_t)slot];
+            }
+          });
+        }
+        if ((rc = s->grec.upload(gr))) return rc;
         for (int li = 0; li < d->num_lights && li < 32; ++li)
           if (gh[(size_t)li].gu > 0) s->lrec_mask |= 1u << li;
       }
@@ -1149,7 +1165,7 @@ extern "C" int rt_scene_get_info(const rt_scene* s, rt_scene_info* out) {
                                 s->fb_scratch.bytes() + s->grids.bytes() + s->grid_off.bytes() +
                                 s->grid_ent.bytes() + s->obj_grids.bytes() + s->obj_grid_mask.bytes() +
                                 s->bin_dev.bytes() + s->sat_dev.bytes() + s->objbox_dev.bytes() +
-                                s->fr.bytes() + s->fr2.bytes());
+                                s->lrec.bytes() + s->grec.bytes() + s->fr.bytes() + s->fr2.bytes());
   out->build_ms = s->build_ms;
   return RT_OK;
 }
@@ -1699,6 +1715,7 @@ int fill_fast(rt_scene* s, const rt_options* o, const Mapping& mp, float* fb, Fa
     p.lrec_base = (uint64_t)(uintptr_t)s->lrec.p - (uint64_t)s->num_nodes * sizeof(TriFast);
     p.lrec_stride = s->lrec_ntri * (int64_t)sizeof(LTri);
     p.lrec_mask = s->lrec_mask;
+    p.grid_rec = s->grec.p;
   }
   const bool binning = !(o->flags & RT_FLAG_NO_BINNING);
   if (binning) {
