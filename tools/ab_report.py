@@ -1,5 +1,7 @@
-"""Summarise tools/gpu_ab_scenes.sh logs: per scene, each variant's minimum over
-the repetitions of one scene_times field (default render_ms).
+"""Summarise per-scene A/B logs (ab_<variant>_<rep>.log files of
+`<scene> {scene_times dict}` lines, as tools/scene_times.py prints them): per
+scene, each variant's minimum over the repetitions of one scene_times field
+(default render_ms).
 
     python tools/ab_report.py gpurun_out/ab [render_ms|setup_ms|call_ms]
 """
