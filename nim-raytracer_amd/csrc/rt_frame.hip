@@ -211,8 +211,17 @@ __global__ __launch_bounds__(256) void k_frame_build1(const FrameLaunch a, int f
 
 // ---- k_frame_build2: huge faces, records, counters, lean / general lists --
 
-// Tiles per block of k_frame_lists.
-constexpr int kChunkTiles = 16;
+// Tiles per block of k_frame_lists, by launch size: every block sums the
+// counts of all earlier tiles (~ntiles^2 / (2 chunk) loads per launch, L2
+// hits) and then writes its chunk's pixels, so small launches want small
+// chunks (more blocks, each chunk's records and writes short) and large ones
+// large chunks (the summing grows with the square of the tiles). Measured
+// (C3, interleaved A/Bs, `profiles/r5/ab/r5aa_*`, `r5ab_*`): rank 0 of 8
+// (1,012 tiles) back to back 0.142 ms with 16 tiles per block, 0.137 with 4,
+// 0.136 with 2 or 1; the whole 1080p frame (8,100 tiles) 0.823 ms with 16,
+// 0.816 with 4. 4K frames (32,400 tiles) keep 16. RTMI_LISTS_CHUNK=1|2|4|16
+// forces one (diagnostic builds).
+__host__ __forceinline__ int lists_chunk(int ntiles) { return ntiles <= 2048 ? 2 : ntiles <= 8192 ? 4 : 16; }
 
 // The class of a launch pixel: 1 lean (empty list, every light skipped), 2
 // general, 0 not drawn (a progressive pass skips it).
@@ -302,13 +311,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W))) void k
 }
 
 // k_frame_lists: the lean / general lists (two-class launches) in tile
-// order. One block per chunk of kChunkTiles tiles: its offsets are the sum of
+// order. One block per chunk of kChunkTiles tiles (above): its offsets are the sum of
 // every earlier tile's counts (k_frame_build2's tile_cls), summed by the
 // block itself — each block re-reads the earlier counts (8,100 x 8 B at
 // 1080p, L2-resident) instead of waiting on other blocks: no inter-block
 // hand-off, no spin, no scan launch. Then each thread loads its pixel's
 // record in each of the chunk's tiles (all loads in flight), and the chunk's
 // pixels are written at their offsets (wave ballots, mbcnt ranks).
+template <int kChunkTiles>
 __global__ __launch_bounds__(256) void k_frame_lists(const FrameLaunch a) {
   __shared__ unsigned long long wpart[4];
   __shared__ unsigned long long wsum[kChunkTiles][4];
@@ -469,8 +479,18 @@ extern "C" int rtmi_frame_build(const rtmi::FrameLaunch* a, void* stream) {
   else
     hipLaunchKernelGGL(k_frame_build2<4>, dim3((unsigned)a->ntiles), dim3(256), 0, st, *a);
   if ((e = hipGetLastError()) != hipSuccess || !a->r.split) return (int)e;
-  const int nchunks = (a->ntiles + kChunkTiles - 1) / kChunkTiles;
-  hipLaunchKernelGGL(k_frame_lists, dim3((unsigned)nchunks), dim3(256), 0, st, *a);
+  static const int chunk_env = rtmi::diag_env("RTMI_LISTS_CHUNK") ? std::atoi(rtmi::diag_env("RTMI_LISTS_CHUNK")) : 0;
+  const int chunk = chunk_env == 1 || chunk_env == 2 || chunk_env == 4 || chunk_env == 16 ? chunk_env
+                                                                                          : lists_chunk(a->ntiles);
+  const int nchunks = (a->ntiles + chunk - 1) / chunk;
+  if (chunk == 1)
+    hipLaunchKernelGGL(k_frame_lists<1>, dim3((unsigned)nchunks), dim3(256), 0, st, *a);
+  else if (chunk == 2)
+    hipLaunchKernelGGL(k_frame_lists<2>, dim3((unsigned)nchunks), dim3(256), 0, st, *a);
+  else if (chunk == 4)
+    hipLaunchKernelGGL(k_frame_lists<4>, dim3((unsigned)nchunks), dim3(256), 0, st, *a);
+  else
+    hipLaunchKernelGGL(k_frame_lists<16>, dim3((unsigned)nchunks), dim3(256), 0, st, *a);
   return (int)hipGetLastError();
 }
 
