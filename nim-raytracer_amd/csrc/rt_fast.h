@@ -1180,6 +1180,21 @@ template <int CTRL, int ROWS>
 __device__ __forceinline__ float dpp_add(float v) {
   return v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, ROWS, 0xf, false));
 }
+// OR of a 32-bit value over the wave (the DPP tree of wave_total; lanes a
+// row shift or broadcast does not reach contribute 0, the identity)
+template <int CTRL, int ROWS>
+__device__ __forceinline__ unsigned dpp_or(unsigned v) {
+  return v | (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROWS, 0xf, false);
+}
+__device__ __forceinline__ unsigned wave_or(unsigned v) {
+  v = dpp_or<0x111, 0xf>(v);
+  v = dpp_or<0x112, 0xf>(v);
+  v = dpp_or<0x114, 0xf>(v);
+  v = dpp_or<0x118, 0xf>(v);
+  v = dpp_or<0x142, 0xa>(v);
+  v = dpp_or<0x143, 0xc>(v);
+  return (unsigned)__builtin_amdgcn_readlane((int)v, 63);
+}
 __device__ __forceinline__ float wave_total(float v) {
   v = dpp_add<0x111, 0xf>(v);  // row_shr:1
   v = dpp_add<0x112, 0xf>(v);  // row_shr:2
@@ -1343,7 +1358,7 @@ constexpr int kLeanBatch = RTMI_LEAN_BATCH;
 // object mask either way holds every object a shadow ray can hit, so frames
 // and Stats do not change.
 #ifndef RTMI_OB_CELLS_JOINT
-#define RTMI_OB_CELLS_JOINT 1
+#define RTMI_OB_CELLS_JOINT 2
 #endif
 template <unsigned F, int S = kLeanBatch, bool OB = false>
 __device__ __forceinline__ void lean_batch(KP p, const GroupPix& gp, int it0, const LdsF* tb, Acc& acc,
@@ -1530,7 +1545,27 @@ __device__ __forceinline__ void lean_batch(KP p, const GroupPix& gp, int it0, co
           const RT_CONST LightGrid& G = cp(p->obj_grids)[li];
           unsigned long long m = p->obj_off_grid;
           bool every = false;
-#if RTMI_OB_CELLS_JOINT
+#if RTMI_OB_CELLS_JOINT == 2
+          // every lane loads its samples' cell masks (vector loads, one round
+          // trip), ORed over the wave by DPP — instead of one scalar load per
+          // distinct cell, each waited for in turn. No cap on the distinct
+          // cells: their union is a subset of "every object" and, the masks
+          // being conservative, tests every object a ray can hit.
+          unsigned long long mine = 0ull;
+#pragma unroll
+          for (int k = 0; k < S; ++k) {
+            const bool lk = lane_in(litm[k]);
+            const F3 q = so[k];
+            const float gu = __builtin_fmaf(q.x, G.e1[0], __builtin_fmaf(q.y, G.e1[1], q.z * G.e1[2]));
+            const float gv = __builtin_fmaf(q.x, G.e2[0], __builtin_fmaf(q.y, G.e2[1], q.z * G.e2[2]));
+            const float fu = (gu - G.u0) * G.inv_h, fv = (gv - G.v0) * G.inv_h;
+            const bool safe = fmaxf(fmaxf(fabsf(q.x), fabsf(q.y)), fabsf(q.z)) <= G.rmax;
+            const bool on = fu >= 0.0f && fu < (float)G.gu && fv >= 0.0f && fv < (float)G.gv;
+            if (lk && safe && on) mine |= p->obj_grid_mask[G.off_base + (int)fv * G.gu + (int)fu];
+            every = every || bal(lk && !safe) != 0ull;
+          }
+          m |= ((unsigned long long)wave_or((unsigned)(mine >> 32)) << 32) | wave_or((unsigned)mine);
+#elif RTMI_OB_CELLS_JOINT
           // the distinct cells of all S samples' origins, each mask loaded
           // once (the samples of a pixel's lanes mostly share their cells:
           // per sample the same cells were walked S times)
@@ -2740,13 +2775,26 @@ k_render_fast(const FastParams params_by_value) {
       unsigned long long cmask = p->nobj >= 64 ? ~0ull : ((1ull << p->nobj) - 1ull);
       if (p->obj_pix) {
         const int pix = gp.valid ? gp.y * p->width + gp.x : -1;
-        unsigned long long todo = bal(pix >= 0), m = 0ull;
-        for (int k = 0; k < 8 && todo != 0ull; ++k) {
-          const int kp = __builtin_amdgcn_readlane(pix, (int)__builtin_ctzll(todo));
-          todo &= ~bal(pix == kp);
-          m |= cp(p->obj_pix)[kp];
+        if (L >= 8) {
+          // <= 8 pixels per wave, pixel q's lanes from q L: every lane loads
+          // its own pixel's mask (one vector load, one round trip for the
+          // wave's pixels) and the pixels' first lanes are ORed — instead of
+          // one scalar load per distinct pixel, each waited for in turn
+          const unsigned long long mine = pix >= 0 ? p->obj_pix[pix] : 0ull;
+          unsigned long long m = 0ull;
+          for (int q = 0; q < 64; q += L)
+            m |= ((unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)(unsigned)(mine >> 32), q) << 32) |
+                 (unsigned)__builtin_amdgcn_readlane((int)(unsigned)mine, q);
+          cmask = m;
+        } else {
+          unsigned long long todo = bal(pix >= 0), m = 0ull;
+          for (int k = 0; k < 8 && todo != 0ull; ++k) {
+            const int kp = __builtin_amdgcn_readlane(pix, (int)__builtin_ctzll(todo));
+            todo &= ~bal(pix == kp);
+            m |= cp(p->obj_pix)[kp];
+          }
+          cmask = todo == 0ull ? m : cmask;
         }
-        cmask = todo == 0ull ? m : cmask;
       }
       int it = 0;
       if (!(p->flags & RT_DEV_FLAG_NO_OBJ_BATCH))
