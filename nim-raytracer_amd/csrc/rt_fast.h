@@ -3317,10 +3317,16 @@ struct WorkQ {
   // atomic and reads its result with readfirstlane where it is issued, so a
   // per-lane copy bought no latency hiding — it only held a VGPR across the
   // item, which k_render_mix1 spilled)
+  // RTMI_QSCALAR=0 (A/B): the per-lane copy again (with the atomic
+  // optimiser off — Makefile F32_FLAGS — a true prefetch): C3 equal, one
+  // spilled VGPR in k_render_mix1 (profiles/r5/ab/r5af_*)
+#ifndef RTMI_QSCALAR
+#define RTMI_QSCALAR 1
+#endif
   __device__ __forceinline__ int reserve() {
     int q = 0;
     if (__lane_id() == 0) q = (int)atomicAdd(queue + head * kQueueStride, 1u);
-    return __builtin_amdgcn_readfirstlane(q);
+    return RTMI_QSCALAR ? __builtin_amdgcn_readfirstlane(q) : q;
   }
   __device__ __forceinline__ int item(int qj) const {
 #if RTMI_XCD_CHUNK

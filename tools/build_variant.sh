@@ -9,7 +9,7 @@ cd "$(dirname "$0")/../nim-raytracer_amd"
 set -- "$1" "-DRTMI_DIAG $2"
 make -s -j8 >/dev/null
 mkdir -p ../tools/ab build/var/$1
-F="-O3 -std=c++17 -fPIC ${F32_FLAGS--ffp-contract=fast -Xclang -target-feature -Xclang -packed-fp32-ops} $2"
+F="-O3 -std=c++17 -fPIC ${F32_FLAGS--ffp-contract=fast -Xclang -target-feature -Xclang -packed-fp32-ops -mllvm -amdgpu-atomic-optimizer-strategy=None} $2"
 /opt/rocm/bin/hipcc --offload-arch=gfx950 $F -c csrc/rt_kernels_f32.hip -o build/var/$1/main.o 2> >(grep -v "packed-fp32-ops. is not a recognized" >&2) &
 for k in $(seq 0 15); do
   /opt/rocm/bin/hipcc --offload-arch=gfx950 $F -DRTMI_PART=$k -c csrc/rt_kernels_f32_part.hip -o build/var/$1/part$k.o 2> >(grep -v "packed-fp32-ops. is not a recognized" >&2) &

@@ -19,7 +19,7 @@ if "--filter" in args:
 src = [a for a in args if not a.startswith("-")] or ["csrc/rt_kernels_f32.hip"]
 defs = [a for a in args if a.startswith("-")]
 cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=fast", "-Xclang",
-       "-target-feature", "-Xclang", "-packed-fp32-ops", "--cuda-device-only",
+       "-target-feature", "-Xclang", "-packed-fp32-ops", "-mllvm", "-amdgpu-atomic-optimizer-strategy=None", "--cuda-device-only",
        "-Rpass-analysis=kernel-resource-usage", "-c", src[0], "-o", "/dev/null"] + defs
 out = subprocess.run(cmd, capture_output=True, text=True, cwd="/root/repo/nim-raytracer_amd").stderr
 rows, cur = [], None
