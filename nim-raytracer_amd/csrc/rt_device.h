@@ -1046,6 +1046,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVELS > 1 
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      // empty the 32-bit wave counters every 16 steps, as k_render does every
+      // 64 samples: STAT_TESTS grows by 64 x nobj per trace, P pixels x
+      // (1 + lights) x levels traces per step
+      if ((it & 15) == 15) flush_stats(ws, tot, lane);
     }
     flush_stats(ws, tot, lane);
     if (lane < P) {

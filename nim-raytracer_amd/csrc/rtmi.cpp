@@ -993,7 +993,16 @@ extern "C" int rt_scene_create(const rt_scene_desc* d, rt_scene** out_scene) {
       // kernels' every shadow ray to such a light tests these, on every path)
       {
         const size_t nt = (size_t)ntri;  // indexed like the TriFast records: byte offset / 64 - nnodes
-        std::vector<LTri> lr((size_t)d->num_lights * nt);
+        // every slot starts as the culled sentinel make_ltri writes for a face
+        // that can never pass (u = v = t = -1): an all-zero record would read
+        // as a hit at t = 0 (u = v = 0 passes min(u, v, 1-u-v) >= 0) if a
+        // future path read a slot of another mesh's face or of a light with
+        // no grid
+        LTri culled;
+        std::memset(&culled, 0, sizeof culled);
+        culled.cu = culled.cv = culled.ct = -1.0f;
+        culled.id = -1;
+        std::vector<LTri> lr((size_t)d->num_lights * nt, culled);
         for (int li = 0; li < d->num_lights; ++li) {
           if (gh[(size_t)li].gu <= 0) continue;
           const double* dir = d->lights[li].dir;
@@ -1011,7 +1020,7 @@ extern "C" int rt_scene_create(const rt_scene_desc* d, rt_scene** out_scene) {
         if ((rc = s->lrec.upload(lr))) return rc;
         s->lrec_ntri = (int64_t)nt;
         // the cell-ordered copy: entry e of light li's grid -> its face's record
-        std::vector<LTri> gr(gent.size());
+        std::vector<LTri> gr(gent.size(), culled);
         for (int li = 0; li < d->num_lights; ++li) {
           if (gh[(size_t)li].gu <= 0) continue;
           const LightGridHost& lg = s->grid_host[(size_t)li];

@@ -9,6 +9,7 @@ dispatch. `scene` is the reference's Scene (renderLine caches its device copy,
 as the Nim binding in INTEGRATION.md does) or a DeviceScene: the Scene flattened and
 uploaded once (BVH built) — the Nim shim in INTEGRATION.md does the same.
 """
+import contextlib
 import ctypes as C
 import threading
 
@@ -270,11 +271,25 @@ class _DeviceCache:
             e.ds.close()
 
     def get(self, scene: Scene, device=0) -> "DeviceScene":
-        """The device copy (for calls the caller keeps in step with
-        invalidate() itself; renderLine uses acquire / release)."""
+        """The device copy, NOT held: for single-threaded callers that keep
+        it in step with invalidate() themselves. A concurrent
+        invalidateScene, shape change or collection of the Scene may close
+        the returned copy while it is in use; threaded callers use held()
+        (or renderLine, which holds the copy for each call)."""
         ds, e = self.acquire(scene, device)
         self.release(e)
         return ds
+
+    @contextlib.contextmanager
+    def held(self, scene: Scene, device=0):
+        """`with held(scene) as ds:` the device copy, kept open until the
+        block ends (acquire / release around it) even if another thread
+        invalidates or replaces it meanwhile."""
+        ds, e = self.acquire(scene, device)
+        try:
+            yield ds
+        finally:
+            self.release(e)
 
     def invalidate(self, scene: Scene):
         with self._lock:
@@ -302,8 +317,15 @@ _cache = _DeviceCache()
 
 
 def deviceScene(scene: Scene, device=0) -> "DeviceScene":
-    """The cached device copy of `scene` (INTEGRATION.md deviceScene)."""
+    """The cached device copy of `scene` (INTEGRATION.md deviceScene).
+    Single-threaded use only: the copy is not held (see heldDeviceScene)."""
     return _cache.get(scene, device)
+
+
+def heldDeviceScene(scene: Scene, device=0):
+    """Context manager: the cached device copy of `scene`, held open for the
+    block (safe against a concurrent invalidateScene / Scene edit)."""
+    return _cache.held(scene, device)
 
 
 def invalidateScene(scene: Scene):
@@ -544,5 +566,5 @@ def _stream(stream):
     return C.c_void_p(int(stream.cuda_stream) or None)
 
 
-__all__ = ["DeviceScene", "RtmiError", "band_rows", "device_count", "deviceScene", "initRenderer", "invalidateScene",
+__all__ = ["DeviceScene", "RtmiError", "band_rows", "device_count", "deviceScene", "heldDeviceScene", "initRenderer", "invalidateScene",
            "ppm_encode_device", "renderLine", "render_frame", "unshard_bands_device", "write_ppm_device"]

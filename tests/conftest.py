@@ -29,3 +29,18 @@ def gpu():
     assert n > 0, "no GPU visible to librtmi.so"
     renderer.initRenderer(0)
     return 0
+
+
+@pytest.fixture(scope="session")
+def c3_oracle_frame(oracle_mod):
+    """The same-BVH oracle's WHOLE 1920x1080, 256-spp C3 frame (bunny + ground,
+    bias 1e-4) and its Stats, computed once per session (~14 s on the GPU
+    box's 16 host threads) and shared by the float32 whole-frame tolerance
+    test and the float64 whole-frame bit-exact test."""
+    import numpy as np
+    from rtmi import Antialias, Options, Precision, akGrid, scenes
+    opts = Options(width=1920, height=1080, antialias=Antialias(akGrid, 16), bias=1e-4, precision=Precision.fp64)
+    fb = np.zeros((1080, 1920, 3), np.float32)
+    _, st, _ = oracle_mod.OracleScene(scenes.mesh_bunny(), bvh=True).render(opts, rows=list(range(1080)), fb=fb,
+                                                                            nthreads=16)
+    return fb, st

@@ -25,6 +25,9 @@ CASES = {
     "boxes2_grid2": dict(scene="boxes2", w=96, h=54, aa=1, m=2, bias=1e-4, depth=5),
     "reflection": dict(scene="spheres-reflection", w=96, h=64, aa=0, m=1, bias=1e-4, depth=5),
     "bunny": dict(scene="mesh-bunny", w=64, h=48, aa=0, m=1, bias=1e-4, depth=5),
+    # src/raytracer.nim:43-54's live configuration, verbatim: mesh-bunny.nim
+    # (teapot.obj), 300x200, akNone, bias 1e-8, maxRayDepth 5
+    "teapot_live": dict(scene="mesh-teapot", w=300, h=200, aa=0, m=1, bias=1e-8, depth=5),
 }
 
 

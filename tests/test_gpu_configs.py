@@ -156,7 +156,7 @@ def test_c3_256spp_whole_frame(gpu):
     _counts_close(st, rst)
 
 
-def test_c3_1080p_whole_frame(gpu):
+def test_c3_1080p_whole_frame(gpu, c3_oracle_frame):
     """C3 exactly as benchmarked: one 1920x1080, 256-spp call (k_render_mix1,
     the per-call device build included) against the same-BVH oracle's whole
     frame (~14 s on 16 host threads), every pixel, and that call's own Stats
@@ -167,7 +167,7 @@ def test_c3_1080p_whole_frame(gpu):
     got, st = _gpu(ds, o)
     assert ds.last_lean_kernel() == 3 | 3 << 2, ds.last_lean_kernel()
     assert st.numPrimaryRays == 1920 * 1080 * 256
-    ref, rst = _oracle_rows(sc, o, list(range(1080)))
+    ref, rst = c3_oracle_frame
     _check(got, ref, "C3 1080p whole frame", frac=0.9999, fine_frac=0.999, mean_tol=1e-6)
     _counts_close(st, rst)
 

@@ -135,7 +135,7 @@ def test_bunny_fixture():
     assert tris.shape == (69451, 3, 3)
 
 
-@pytest.mark.parametrize("name", ["c1_spheres_warm3", "boxes2_grid2", "reflection", "bunny"])
+@pytest.mark.parametrize("name", ["c1_spheres_warm3", "boxes2_grid2", "reflection", "bunny", "teapot_live"])
 def test_oracle_matches_committed_golden(oracle_mod, name):
     """Regression pin: the committed golden images (tests/golden/make_golden.py)."""
     import json

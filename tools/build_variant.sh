@@ -3,7 +3,10 @@
 # (built with -DRTMI_DIAG: the RTMI_* diagnostic / A/B environment knobs are
 # read only by such builds, rt_common.h diag_env)
 # (the kernel TUs — float32 main + the 16 specialisation parts, the float64
-# kernels, the per-call build and the host launch code — rebuilt with the flags)
+# kernels, the per-call build and the host launch code — and every TU that
+# reads a diag_env knob (rt_bins.cpp: RTMI_GRID_DENSITY, rt_bvh_gpu.hip:
+# RTMI_PLOC_RADIUS) rebuilt with the flags; ADVICE r5: linking the normal
+# rt_bins.o made the density knob a no-op in diagnostic builds)
 set -e
 cd "$(dirname "$0")/../nim-raytracer_amd"
 set -- "$1" "-DRTMI_DIAG $2"
@@ -17,5 +20,7 @@ done
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off $2 -c csrc/rt_frame.hip -o build/var/$1/frame.o &
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off $2 -c csrc/rt_kernels_f64.hip -o build/var/$1/f64.o &
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-result -ffp-contract=off $2 -c csrc/rtmi.cpp -o build/var/$1/rtmi.o &
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-result -ffp-contract=off $2 -c csrc/rt_bins.cpp -o build/var/$1/bins.o &
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-result -ffp-contract=off $2 -c csrc/rt_bvh_gpu.hip -o build/var/$1/bvh_gpu.o &
 wait
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ../tools/ab/$1.so build/var/$1/main.o build/var/$1/part*.o build/var/$1/f64.o build/rt_kernels_io.o build/var/$1/rtmi.o build/rt_bvh.o build/rt_bvh_gpu.o build/rt_queue.o build/rt_obj.o build/rt_multi.o build/rt_bins.o build/var/$1/frame.o
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ../tools/ab/$1.so build/var/$1/main.o build/var/$1/part*.o build/var/$1/f64.o build/rt_kernels_io.o build/var/$1/rtmi.o build/rt_bvh.o build/var/$1/bvh_gpu.o build/rt_queue.o build/rt_obj.o build/rt_multi.o build/var/$1/bins.o build/var/$1/frame.o
