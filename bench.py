@@ -82,6 +82,8 @@ def parse():
     ap.add_argument("--grid", type=int, default=None, help="akGrid m (spp = m*m)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-extra", action="store_true",
+                    help="skip the fp64_parity / bvh_path sub-measurements after the timed region")
     ap.add_argument("--bvh", default="sah", choices=["sah", "ploc"],
                     help="mesh BVH builder: host binned SAH (default) or device PLOC")
     ap.add_argument("--flags", type=int, default=0, help="rt_options.flags (1 = any-hit shadows)")
@@ -147,6 +149,84 @@ CLOCK_GHZ = 2.4        # peak engine clock
 VALU_CYCLES = 2        # a wave64 VALU instruction issues over 2 cycles per SIMD (MI355X_MICROARCH.md)
 VALU_PEAK_GINST = SIMDS * CLOCK_GHZ / VALU_CYCLES   # 1228.8 G wave64 VALU instructions / s
 SALU_PEAK_GINST = CUS * CLOCK_GHZ                   # one scalar unit per CU, one instruction per cycle
+
+
+F64_VALU_CYCLES = 4    # FP64 FMA/MUL/ADD/TRANS: half the FP32 rate (78.6 vs 157.3 TF spec) = 4 cycles per wave64
+F64_COUNTERS = ("SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_TRANS_F64")
+
+
+def issue_roofline(c, sec):
+    """Issue-bound roofline of a render call from its per-call PMC counters
+    `c` over `sec` seconds. When the F64 op counts are present the issue
+    time is weighted: an F64 VALU instruction occupies its SIMD 4 cycles,
+    every other VALU instruction 2 (MI355X_MICROARCH.md: 64 FP32 FLOP/clk/SIMD,
+    FP64 at half that), and frac = issue cycles / (SIMDs x clock x sec)."""
+    out = {}
+    if "SQ_INSTS_VALU" not in c:
+        return out
+    ach = c["SQ_INSTS_VALU"] / sec / 1e9
+    out["achieved"] = round(ach, 1)
+    out["frac"] = round(ach / VALU_PEAK_GINST, 4)
+    if all(k in c for k in F64_COUNTERS):
+        f64 = sum(c[k] for k in F64_COUNTERS)
+        cycles = (c["SQ_INSTS_VALU"] - f64) * VALU_CYCLES + f64 * F64_VALU_CYCLES
+        out["f64_valu_share"] = round(f64 / c["SQ_INSTS_VALU"], 4)
+        out["frac_f64_weighted"] = round(cycles / (SIMDS * CLOCK_GHZ * 1e9 * sec), 4)
+        out["f64_definition"] = ("frac_f64_weighted = (2 x non-F64 VALU + 4 x F64 VALU instructions, PMC "
+                                 "SQ_INSTS_VALU and SQ_INSTS_VALU_{FMA,MUL,ADD,TRANS}_F64) / (1024 SIMDs x "
+                                 f"{CLOCK_GHZ} GHz x kernel time): the SIMD issue cycles the F64 mix needs")
+    if "SQ_INSTS_SALU" in c:
+        out["salu_frac"] = round(c["SQ_INSTS_SALU"] / sec / 1e9 / SALU_PEAK_GINST, 4)
+    return out
+
+
+def sub_measure(ds, opts, fb, stream, steps, warmup, key):
+    """Time `steps` whole-frame calls of `opts` after `warmup` (barrier +
+    synchronize around them, one event pair on the call stream), then one
+    RT_FLAG_TIMING pass for the render kernels' time; PMC roofline from the
+    committed summary under `key` when its sources match."""
+    import dataclasses
+
+    import torch
+
+    from rtmi.abi import RT_FLAG_TIMING
+    st = ds.render_device(opts, fb, stream=stream, stats=True)
+    for _ in range(warmup):
+        ds.render_device(opts, fb, stream=stream, stats=False)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(steps):
+        ds.render_device(opts, fb, stream=stream, stats=False)
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    topts = dataclasses.replace(opts, flags=opts.flags | RT_FLAG_TIMING)
+    rms = []
+    for _ in range(steps):
+        ds.render_device(topts, fb, stream=stream, stats=False)
+        rms.append(ds.last_timing()[1])
+    render_ms = sum(rms) / len(rms)
+    rays = st.numPrimaryRays + st.numShadowRays
+    out = {"value": round(rays * steps / el / 1e6, 2), "unit": "Mray/s", "steps": steps, "warmup": warmup,
+           "ms_per_step": round(el / steps * 1e3, 3), "call_ms": round(ev0.elapsed_time(ev1) / steps, 4),
+           "kernel_ms": round(render_ms, 4), "primary_rays_per_frame": st.numPrimaryRays,
+           "shadow_rays_per_frame": st.numShadowRays}
+    pmc = load_pmc(key)
+    if pmc is not None:
+        c = pmc["counters_mean_per_dispatch"]
+        sec = render_ms * 1e-3
+        roof = issue_roofline(c, sec)
+        if "hbm_bytes_per_launch" in pmc:
+            roof["traffic"] = int(pmc["hbm_bytes_per_launch"])
+            roof["hbm_gbs"] = round(pmc["hbm_bytes_per_launch"] / sec / 1e9, 1)
+            roof["hbm_frac"] = round(pmc["hbm_bytes_per_launch"] / sec / 1e9 / HBM_PEAK_GBS, 4)
+        roof["pmc"] = f"profiles/pmc_summary.json[{key}] (sources {pmc['source_hash']})"
+        out["roofline"] = roof
+    else:
+        out["roofline"] = {"pmc": f"no PMC summary [{key}] for these native sources"}
+    return out
 
 
 def load_pmc(workload_key):
@@ -354,24 +434,40 @@ def main():
         torch.cuda.synchronize()
         frame_check = {"bit_identical_to_single_call_frame": bool(torch.equal(ref, fb))}
 
+    # outside the timed region, one GPU only: the same frame in the parity
+    # mode the Nim binding runs (float64, bit-exact against the oracle:
+    # tests/test_gpu_px64.py::test_px64_full_c3_frame) and on the BVH path
+    # that every scene outside the list envelope takes (RT_FLAG_NO_BINNING:
+    # k_render_fast<false>, a per-ray wave-coherent BVH traversal for every
+    # camera and shadow ray) — each timed like the headline, fewer steps
+    extra = {}
+    if not distributed and not fp64 and not args.flags and not args.no_extra and args.config in ("C2", "C3"):
+        k_extra = max(2, min(args.steps, 5))
+        base_key = f"{args.config.lower()}_{W}x{H}_m{m}_world{world}"
+        o64 = dataclasses.replace(opts, precision=Precision.fp64)
+        extra["fp64_parity"] = sub_measure(ds, o64, fb, stream, k_extra, 1, base_key + "_fp64")
+        extra["fp64_parity"]["kernel"] = ("k_render_px64 (float64, one pixel per wave, samples summed in sample "
+                                          "order): the reference's arithmetic, bit-exact against the oracle")
+        obvh = dataclasses.replace(opts, flags=opts.flags | RT_FLAG_NO_BINNING)
+        extra["bvh_path"] = sub_measure(ds, obvh, fb, stream, k_extra, 1, base_key + f"_flags{RT_FLAG_NO_BINNING}")
+        extra["bvh_path"]["kernel"] = ("k_render_fast<false> with RT_FLAG_NO_BINNING: every camera and shadow ray "
+                                       "through the BVH (wave-coherent traversal, fp32), no per-pixel or light-cell "
+                                       "lists — the path of scenes outside the one-mesh / one-plane envelope")
+
     value = rays_frame * args.steps / elapsed / 1e6
     # SURVEY 8(d)'s per-ray BVH byte model over this launch's rays (what a
     # per-ray BVH tracer would read; these kernels skip most of it)
     bvh_model_bytes = (counters["lane_node_visits"] * 2 * SURVEY_BOX_BYTES
                        + counters["lane_tri_tests"] * SURVEY_TRI_BYTES + rows * W * PIXEL_BYTES)
-    workload_key = f"{args.config.lower()}_{W}x{H}_m{m}_world{world}" + ("_fp64" if fp64 else "")
+    workload_key = (f"{args.config.lower()}_{W}x{H}_m{m}_world{world}" + ("_fp64" if fp64 else "")
+                    + (f"_flags{args.flags}" if args.flags else ""))
     pmc = load_pmc(workload_key)
     roof = {"bound": "issue", "achieved": None, "peak": VALU_PEAK_GINST, "unit": "G wave64 VALU inst/s",
             "frac": None, "traffic": None}
     if pmc is not None:
         c = pmc["counters_mean_per_dispatch"]
         sec = render_ms * 1e-3
-        if "SQ_INSTS_VALU" in c:
-            ach = c["SQ_INSTS_VALU"] / sec / 1e9
-            roof["achieved"] = round(ach, 1)
-            roof["frac"] = round(ach / VALU_PEAK_GINST, 4)
-        if "SQ_INSTS_SALU" in c:
-            roof["salu_frac"] = round(c["SQ_INSTS_SALU"] / sec / 1e9 / SALU_PEAK_GINST, 4)
+        roof.update(issue_roofline(c, sec))
         if "hbm_bytes_per_launch" in pmc:
             roof["traffic"] = int(pmc["hbm_bytes_per_launch"])
             roof["hbm_gbs"] = round(pmc["hbm_bytes_per_launch"] / sec / 1e9, 1)
@@ -441,6 +537,7 @@ def main():
         }
         if frame_check is not None:
             out["frame_check"] = frame_check
+        out.update(extra)
         if world == 1 and not args.no_cpu:
             # the reference's brute-force mesh loop is infeasible past ~200k
             # triangles (~1e11 triangle tests per 4K row): same-BVH only there

@@ -49,6 +49,9 @@ struct alignas(16) DevObject {
   R o2w[16];
   R prm[8];      // sphere: prm[0] = r; box: prm[0..2] = vmin, prm[4..6] = vmax
   R albedo[4];   // rgb, reflection
+  R albp[4];     // albedo / PI (rgb), formed by the host in R: the IEEE quotient
+                 // shadeDiffuse's `albedo / PI` gives (shader.nim:15), read by
+                 // the float64 kernels instead of dividing per sample
   int32_t type;
   int32_t mesh;
   int32_t xf;          // XF_* classification of world_to_object
@@ -117,6 +120,26 @@ struct alignas(16) TriF64 {
 };
 static_assert(sizeof(TriF64) == 80, "TriF64 must be 80 bytes");
 
+// A face's float64 shadow-ray record for one distant light (the parity
+// kernel's light-cell searches, k_render_px64 mesh_lists): the values
+// rayTriangleIntersectFast forms from the ray direction alone (geom.nim:
+// 296-306: pvec = dir x v0v2, det = v0v1 . pvec, invDet = 1 / det) are fixed
+// for a distant light's shadow rays, so k_build_sh64 forms them once per
+// (light, grid entry) with tri_ref's operations on the light's object-space
+// direction — the same bits a per-ray test forms — and a test reads them.
+// Stored in light-grid entry order (a cell's faces are one contiguous run).
+struct alignas(16) ShTri64 {
+  double v0[3];
+  double e1[3];
+  double e2[3];
+  double pvec[3];
+  double det;
+  double inv_det;
+  int32_t id;
+  int32_t pad[3];
+};
+static_assert(sizeof(ShTri64) == 128, "ShTri64 must be 128 bytes");
+
 template <class R> struct TriOf;
 template <> struct TriOf<float> { using type = TriF32; };
 template <> struct TriOf<double> { using type = TriF64; };
@@ -173,6 +196,13 @@ struct RenderParams {
   const struct LightGrid* grids;
   const int32_t* grid_off;
   const int32_t* grid_ent;
+  // k_render_px64's lean samples (rt_device.h px64_lean_sample): the plane of
+  // a one-mesh + one-plane scene whose lights are all distant (<= 8) and whose
+  // plane does not reflect, when this call has pixel records; -1 otherwise
+  int32_t lean_plane;
+  // the float64 shadow records (ShTri64) of the distant lights with a grid,
+  // in grid entry order (index = G.ent_base + entry), or nullptr
+  const ShTri64* sh64;
 };
 
 // ---- float32 performance-kernel records (rt_fast.h) -------------------------
@@ -374,6 +404,9 @@ int rtmi_launch_sec_add(float* fb, const long long* sec, size_t n, float scale, 
 int rtmi_launch_render_f64(const rtmi::RenderParams<double>* p, int blocks, int px64, void* stream);
 int rtmi_px64_blocks_per_cu(int px64);
 int rtmi_px64_batch();
+int rtmi_build_sh64(const rtmi::DevObject<double>* objects, int mesh_obj, const rtmi::DevLight<double>* lights,
+                    int light, const int32_t* ent, int n, const rtmi::TriF64* tris, int tri_rec0,
+                    rtmi::ShTri64* out, void* stream);
 int rtmi_render_f32_blocks_per_cu(int count, unsigned subset, size_t shmem);
 int rtmi_launch_lean_f32(const rtmi::FastParams* p, unsigned subset, int blocks, size_t shmem, void* stream);
 int rtmi_lean_f32_blocks_per_cu(unsigned subset, size_t shmem);

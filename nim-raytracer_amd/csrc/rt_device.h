@@ -99,6 +99,27 @@ __device__ __forceinline__ V3<R> xform(const M& m, V3<R> v, R w) {
   return r;
 }
 
+// glm Mat4 * Vec4 for an object's matrix of host class xf (DevObject.xf;
+// XF_IDENTITY / XF_TRANSLATE: both object matrices have an identity 3x3
+// block). In exact mode the literal sum of such a matrix collapses bit for
+// bit: row x is (((0 + 1*v.x) + 0*v.y) + 0*v.z) + m[12]*w, and with v.y, v.z
+// finite the signed-zero products leave the partial sum 0 + v.x unchanged
+// (it is never -0), so the row is (0 + v.x) + m[12] for a point and 0 + v.x
+// for a direction (m[12]*0 is another signed zero). The callers pass only
+// values that are finite on every lane whose result is used (ray origins and
+// directions, hit points of hits, normals); 2-3 float64 operations per row
+// instead of 8.
+template <class R, bool POINT, class M>
+__device__ __forceinline__ V3<R> xform_xf(int xf, const M& m, V3<R> v) {
+  if constexpr (Prec<R>::exact) {
+    if (xf != XF_GENERAL) {
+      if constexpr (POINT) return V3<R>{(R(0) + v.x) + m[12], (R(0) + v.y) + m[13], (R(0) + v.z) + m[14]};
+      return V3<R>{R(0) + v.x, R(0) + v.y, R(0) + v.z};
+    }
+  }
+  return xform<R>(m, v, POINT ? R(1) : R(0));
+}
+
 // vec4 dot with explicit w terms (exact mode keeps the literal sum order).
 template <class R>
 __device__ __forceinline__ R dot4(V3<R> a, R aw, V3<R> b, R bw) {
@@ -197,6 +218,14 @@ __device__ __forceinline__ R sphere_ref(R radius, const ORay<R>& r) {
 // Plane.intersect (geom.nim:240-248): y = 0, n = (0,1,0,0).
 template <class R>
 __device__ __forceinline__ R plane_ref(const ORay<R>& r) {
+  if constexpr (Prec<R>::exact) {
+    // the literal dot4 sums with n = (0, 1, 0, 0) collapse exactly (as in
+    // xform_xf: for finite x / z components the signed-zero terms leave
+    // 0 + y unchanged): dot(n, d) = 0 + d.y, dot(o, n) = 0 + o.y
+    const R denom = R(0) + r.d.y;
+    if (fabs(denom) > R(1e-6)) return Prec<R>::div(-(R(0) + r.o.y), denom);
+    return -pinf<R>();
+  }
   const V3<R> n{R(0), R(1), R(0)};
   const R denom = dot4(n, R(0), r.d, R(0));
   if (fabs(denom) > R(1e-6)) {
@@ -367,10 +396,70 @@ __device__ __forceinline__ void traverse(const RT_CONST RenderParams<R>& p, int 
 // proof, tests/test_bins_cpu.py), so it equals geom.nim:339-358's loop over
 // all faces. early: the shadow early exit (a lane retires on a found hit at
 // t <= stop, as in leaf()).
+// A TriF64 record's fields read from an LDS slice (list_tris' staging).
+struct TriView {
+  const double* v0;
+  const double* e1;
+  const double* e2;
+};
+
+#ifndef RTMI_PX64_STAGE_CAM
+#define RTMI_PX64_STAGE_CAM 0  // measured slower: 20 VGPR spills at 3 waves (r6g)
+#endif
 template <class R>
 __device__ __forceinline__ void list_tris(const RT_CONST RenderParams<R>& p, const int32_t* ent, int n, V3<R> o, V3<R> d,
                                           bool act, bool early, R stop, R& tbest, int& best_id) {
   using Tri = typename TriOf<R>::type;
+  if constexpr (Prec<R>::exact && RTMI_PX64_STAGE_CAM) {
+    // LDS staging of the float64 records (80 B = 10 doubles): the list's
+    // entries are loaded 64 at a time into a VGPR, four records = 40 doubles
+    // are one vector load into the wave's LDS slice, read back as broadcasts,
+    // and the next four load while these are tested
+    __shared__ double stage_t[4][2][64];
+    const int lane = (int)__lane_id();
+    double* slice = &stage_t[(threadIdx.x >> 6) & 3][0][0];
+    const double* recs = (const double*)p.tris;
+    const int rec0 = p.tri_rec0;
+    const int ngroups = (n + 3) >> 2;
+    const int jl = lane / 10, fl = lane - 10 * jl;  // this lane's record of a group and its double
+    int entv = lane < n ? ent[lane] : 0;
+    int chunk = 0;
+    auto fetch = [&](int g) -> double {
+      const int k = 4 * g + jl;
+      if ((4 * g) >> 6 != chunk) {  // the next 64 entries (lists past 64 faces)
+        chunk = (4 * g) >> 6;
+        entv = 64 * chunk + lane < n ? ent[64 * chunk + lane] : 0;
+      }
+      const int off = __shfl(entv, k & 63);
+      return lane < 40 && k < n ? recs[(size_t)((off >> 6) - rec0) * 10 + fl] : 0.0;
+    };
+    double pre = fetch(0);
+    for (int g = 0; g < ngroups; ++g) {
+      double* buf = slice + (g & 1) * 64;
+      buf[lane] = pre;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      if (g + 1 < ngroups) pre = fetch(g + 1);
+      const int jn = min(4, n - 4 * g);
+      for (int j = 0; j < jn; ++j) {
+        const double* f = buf + 10 * j;  // TriF64: v0, e1, e2, id
+        const TriView tv{f, f + 3, f + 6};
+        const R t = tri_ref<R>(tv, o, d);
+        const int id = ((const int32_t*)(f + 9))[0];
+        const bool acc = act && t >= R(0) && (t < tbest || (t == tbest && id < best_id));
+        if (acc) {
+          tbest = t;
+          best_id = id;
+        }
+        if (early && j == 3) {
+          act = act && !(best_id >= 0 && tbest <= stop);
+          if (ballot(act) == 0ull) return;
+        }
+      }
+    }
+    return;
+  }
   for (int k = 0; k < n; ++k) {
     const int off = cptr(ent)[k];
     const RT_CONST Tri& tri = cptr(p.tris)[(off >> 6) - p.tri_rec0];
@@ -384,6 +473,73 @@ __device__ __forceinline__ void list_tris(const RT_CONST RenderParams<R>& p, con
     if (early && (k & 3) == 3) {
       act = act && !(best_id >= 0 && tbest <= stop);
       if (ballot(act) == 0ull) break;
+    }
+  }
+}
+
+// The same search over a cell's float64 shadow records (ShTri64, one
+// distant light's fixed direction d): tri_ref's operations with pvec, det and
+// invDet read from the record (formed from the same d by k_build_sh64). A
+// face whose det fails the cull is skipped (det is the same for every lane),
+// and so are qvec / v / t when no lane's u passes (u's test decides the
+// reference's second early out; the others are order-independent predicates).
+template <class R>
+__device__ __forceinline__ void list_sh64(const ShTri64* rec, int n, V3<R> o, V3<R> d, bool act, bool early, R stop,
+                                          R& tbest, int& best_id) {
+  // LDS staging (the float32 kernels' idea, here for 128-B float64 records):
+  // four records = 64 doubles are ONE coalesced vector load (a double per
+  // lane) into the wave's LDS slice, read back as broadcasts; the next four
+  // are loaded while these are tested (two slices), so the search waits on
+  // one load per four faces, not on a scalar load per face.
+  __shared__ double stage[4][2][64];  // [wave of a 256-thread block][buffer][double]
+  const int lane = (int)__lane_id();
+  double* slice = &stage[(threadIdx.x >> 6) & 3][0][0];
+  const double* src = (const double*)rec;
+  const int nd = n * 16;
+  const int ngroups = (n + 3) >> 2;
+  double pre = lane < nd ? src[lane] : 0.0;
+  for (int g = 0; g < ngroups; ++g) {
+    double* buf = slice + (g & 1) * 64;
+    buf[lane] = pre;
+    // the slice is read by every lane of this wave: LDS operations of one
+    // wave complete in order; the barrier keeps the compiler from moving the
+    // reads above the write
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (g + 1 < ngroups) {
+      const int i = (g + 1) * 64 + lane;
+      pre = i < nd ? src[i] : 0.0;
+    }
+    const int jn = min(4, n - 4 * g);
+    for (int j = 0; j < jn; ++j) {
+      const double* f = buf + 16 * j;  // ShTri64 layout: v0, e1, e2, pvec, det, inv_det, id
+      const R det = f[12];
+      if (!(det < R(0.000001))) {
+        const R v0v1x = f[3], v0v1y = f[4], v0v1z = f[5];
+        const R v0v2x = f[6], v0v2y = f[7], v0v2z = f[8];
+        const R inv_det = f[13];
+        const R tvecx = o.x - R(f[0]), tvecy = o.y - R(f[1]), tvecz = o.z - R(f[2]);
+        const R u = (tvecx * f[9] + tvecy * f[10] + tvecz * f[11]) * inv_det;
+        const bool uok = act && !(u < R(0) || u > R(1));
+        if (ballot(uok) != 0ull) {
+          const R qvecx = tvecy * v0v1z - tvecz * v0v1y;
+          const R qvecy = tvecz * v0v1x - tvecx * v0v1z;
+          const R qvecz = tvecx * v0v1y - tvecy * v0v1x;
+          const R v = (d.x * qvecx + d.y * qvecy + d.z * qvecz) * inv_det;
+          const R t = (v0v2x * qvecx + v0v2y * qvecy + v0v2z * qvecz) * inv_det;
+          const int id = ((const int32_t*)(f + 14))[0];
+          const bool acc = uok && !(v < R(0) || u + v > R(1)) && t >= R(0) && (t < tbest || (t == tbest && id < best_id));
+          if (acc) {
+            tbest = t;
+            best_id = id;
+          }
+        }
+      }
+      if (early && j == 3) {  // every fourth face, as list_tris
+        act = act && !(best_id >= 0 && tbest <= stop);
+        if (ballot(act) == 0ull) return;
+      }
     }
   }
 }
@@ -418,7 +574,10 @@ __device__ __forceinline__ void mesh_lists(const RT_CONST RenderParams<R>& p, in
         const int kb = __builtin_amdgcn_readlane(bin, (int)__builtin_ctzll(todo));
         todo &= ~ballot(bin == kb);
         const int b = cptr(p.grid_off)[kb], e = cptr(p.grid_off)[kb + 1];
-        list_tris<R>(p, p.grid_ent + G.ent_base + b, e - b, r.o, r.d, in && bin == kb, early, stop, tbest, best_id);
+        if (Prec<R>::exact && p.sh64)
+          list_sh64<R>(p.sh64 + G.ent_base + b, e - b, r.o, r.d, in && bin == kb, early, stop, tbest, best_id);
+        else
+          list_tris<R>(p, p.grid_ent + G.ent_base + b, e - b, r.o, r.d, in && bin == kb, early, stop, tbest, best_id);
       }
       in = in && bin < 0 && !nohit;
     }
@@ -453,8 +612,8 @@ __device__ __forceinline__ void to_object(const RT_CONST DevObject<R>& ob, V3<R>
       return;
     }
   }
-  ro = xform<R>(ob.w2o, o, R(1));
-  rd = xform<R>(ob.w2o, d, R(0));
+  ro = xform_xf<R, true>(ob.xf, ob.w2o, o);
+  rd = xform_xf<R, false>(ob.xf, ob.w2o, d);
 }
 
 // t of an analytic object (plane / sphere / box) in its object space.
@@ -479,7 +638,11 @@ constexpr int kCacheObj = 16, kCacheLight = 8;
 constexpr int kCacheCamO = 0;                                 // [obj][4]: w2o * (camera origin, 1)
 constexpr int kCacheLightD = kCacheCamO + 4 * kCacheObj;      // [light][obj][8]: w2o * (-ldir, 0), 1 / that
 constexpr int kCachePlaneN = kCacheLightD + 8 * kCacheObj * kCacheLight;  // [obj][4]: o2w * (0, 1, 0, 0)
-constexpr int kCacheDoubles = kCachePlaneN + 4 * kCacheObj;
+// [light][4]: the lean plane's shading term per light (px64_lean_sample):
+// albedo/PI * lightIntensity * max(0, N . -lightDir) — sample-invariant for a
+// plane under a distant light
+constexpr int kCacheLeanTerm = kCachePlaneN + 4 * kCacheObj;
+constexpr int kCacheDoubles = kCacheLeanTerm + 4 * kCacheLight;
 
 // Linear closest hit over the scene's objects in order, for lanes with
 // `active`; tmin starts at t_near. Wave-uniform control flow only.
@@ -517,14 +680,14 @@ __device__ __forceinline__ Hit<R> trace(const RT_CONST RenderParams<R>& p, V3<R>
       const R* c = cache + kCacheCamO + 4 * i;
       ro = V3<R>{c[0], c[1], c[2]};
     } else {
-      ro = xform<R>(ob.w2o, o, R(1));
+      ro = xform_xf<R, true>(ob.xf, ob.w2o, o);
     }
     if (cached_d) {
       const R* c = cache + kCacheLightD + 8 * (light * kCacheObj + i);
       rd = V3<R>{c[0], c[1], c[2]};
       ri = V3<R>{c[4], c[5], c[6]};
     } else {
-      rd = xform<R>(ob.w2o, d, R(0));
+      rd = xform_xf<R, false>(ob.xf, ob.w2o, d);
     }
     return ORay<R>{ro, rd, ri};
   };
@@ -684,7 +847,7 @@ __device__ __forceinline__ V3<R> shade_path(const RT_CONST RenderParams<R>& p, V
           // a plane's normal does not depend on the hit point: its cached N
           const R* c = cache + kCachePlaneN + 4 * oi;
           N = V3<R>{c[0], c[1], c[2]};
-          alb = V3<R>{ob.albedo[0], ob.albedo[1], ob.albedo[2]};
+          alb = Prec<R>::exact ? V3<R>{ob.albp[0], ob.albp[1], ob.albp[2]} : V3<R>{ob.albedo[0], ob.albedo[1], ob.albedo[2]};
           refl = ob.albedo[3];
           continue;
         }
@@ -697,16 +860,18 @@ __device__ __forceinline__ V3<R> shade_path(const RT_CONST RenderParams<R>& p, V
             V3<R> dummy;
             to_object<R>(ob, hw, V3<R>{R(0), R(0), R(0)}, ho, dummy);
           } else {
-            ho = xform<R>(ob.w2o, hw, R(1));
+            ho = xform_xf<R, true>(ob.xf, ob.w2o, hw);
           }
           nrm = object_normal<R>(ob, ob.type, ho);
         }
         if constexpr (!Prec<R>::exact) {
           N = ob.xf == XF_GENERAL ? xform<R>(ob.o2w, nrm, R(0)) : nrm;
         } else {
-          N = xform<R>(ob.o2w, nrm, R(0));
+          N = xform_xf<R, false>(ob.xf, ob.o2w, nrm);
         }
-        alb = V3<R>{ob.albedo[0], ob.albedo[1], ob.albedo[2]};
+        // exact mode: albedo / PI as the host formed it (DevObject.albp, the
+        // same IEEE quotient); float mode divides as before
+        alb = Prec<R>::exact ? V3<R>{ob.albp[0], ob.albp[1], ob.albp[2]} : V3<R>{ob.albedo[0], ob.albedo[1], ob.albedo[2]};
         refl = ob.albedo[3];
       }
     }
@@ -736,9 +901,10 @@ __device__ __forceinline__ V3<R> shade_path(const RT_CONST RenderParams<R>& p, V
                                                L.type == LIGHT_POINT ? -1 : li, li < kCacheLight ? cache : nullptr);
       if (lit && sh.obj < 0) {  // shadeDiffuse (shader.nim:12-17)
         const R ndl = nmax(R(0), dot4(N, R(0), sd, R(0) * R(-1)));
-        local.x = local.x + Prec<R>::div(alb.x, kPi) * I.x * ndl;
-        local.y = local.y + Prec<R>::div(alb.y, kPi) * I.y * ndl;
-        local.z = local.z + Prec<R>::div(alb.z, kPi) * I.z * ndl;
+        const V3<R> ap = Prec<R>::exact ? alb : V3<R>{Prec<R>::div(alb.x, kPi), Prec<R>::div(alb.y, kPi), Prec<R>::div(alb.z, kPi)};
+        local.x = local.x + ap.x * I.x * ndl;
+        local.y = local.y + ap.y * I.y * ndl;
+        local.z = local.z + ap.z * I.z * ndl;
       }
     }
     const bool reflect = lit && refl > R(0) && depth <= p.max_depth;
@@ -790,6 +956,65 @@ __device__ __forceinline__ V3<R> shade_path(const RT_CONST RenderParams<R>& p, V
     (void)nlev;
     return V3<R>{facc.x + fw * terminal.x, facc.y + fw * terminal.y, facc.z + fw * terminal.z};
   }
+}
+
+// One camera sample of a LEAN pixel in k_render_px64 (RenderParams.lean_plane
+// >= 0: one mesh + one non-reflective plane, distant lights only): the
+// pixel's record says its camera rays miss the mesh (empty list) and so do
+// its shadow rays to every light (skip bits), so shade_path<double, ...,
+// LISTS> would test the mesh nowhere (t = -inf, no update) and this is the
+// rest of it — the same operations in the same order on the plane alone:
+// trace (renderer.nim:47-67) counts nobj tests per ray and the plane's hits,
+// shade (renderer.nim:71-104) adds shadeDiffuse per unshadowed light. The
+// sample-invariant values come from the block cache: the plane's view of the
+// camera origin and of each shadow direction, its normal, and each light's
+// shading term (kCacheLeanTerm: albp * ci * ndl with the same rounding as
+// the per-sample product). The compiler keeps only the y components the
+// plane test reads (plane_ref), which is what makes this path cheap.
+__device__ __forceinline__ V3<double> px64_lean_sample(const RT_CONST RenderParams<double>& p, V3<double> o,
+                                                       V3<double> d, bool active, WaveStats& ws,
+                                                       const double* cache) {
+  using R = double;
+  const int pl = p.lean_plane;
+  const RT_CONST DevObject<R>& ob = cptr(p.objects)[pl];
+  const int xf = ob.xf;
+  const unsigned nobj = (unsigned)p.nobj;
+  ws.v[STAT_TESTS] += popc32(ballot(active)) * nobj;
+  const R* co = cache + kCacheCamO + 4 * pl;
+  ORay<R> r;
+  r.o = V3<R>{co[0], co[1], co[2]};
+  r.d = xform_xf<R, false>(xf, ob.w2o, d);
+  r.inv = V3<R>{R(0), R(0), R(0)};
+  const R t = plane_ref<R>(r);
+  const bool lit = active && t >= R(0) && t < pinf<R>();
+  ws.v[STAT_HITS] += popc32(ballot(lit));
+  V3<R> terminal{R(0), R(0), R(0)};
+  if (active && !lit) terminal = V3<R>{p.bg[0], p.bg[1], p.bg[2]};
+  const R ht = lit ? t : pinf<R>();  // hit.t (t_near = inf without a hit)
+  const V3<R> hw{o.x + d.x * ht, o.y + d.y * ht, o.z + d.z * ht};
+  const R* cn = cache + kCachePlaneN + 4 * pl;
+  const V3<R> N{cn[0], cn[1], cn[2]};
+  const V3<R> so{hw.x + N.x * p.bias, hw.y + N.y * p.bias, hw.z + N.z * p.bias};
+  ORay<R> sr;
+  sr.o = xform_xf<R, true>(xf, ob.w2o, so);
+  const unsigned nlit = popc32(ballot(lit));
+  V3<R> local{R(0), R(0), R(0)};
+  for (int li = 0; li < p.nlight; ++li) {
+    ws.v[STAT_SHADOW] += nlit;
+    ws.v[STAT_TESTS] += nlit * nobj;
+    const R* cd = cache + kCacheLightD + 8 * (li * kCacheObj + pl);
+    sr.d = V3<R>{cd[0], cd[1], cd[2]};
+    sr.inv = V3<R>{cd[4], cd[5], cd[6]};
+    const R ts = plane_ref<R>(sr);
+    const bool blocked = lit && ts >= R(0) && ts < pinf<R>();
+    ws.v[STAT_HITS] += popc32(ballot(blocked));
+    if (lit && !blocked) {
+      const R* tm = cache + kCacheLeanTerm + 4 * li;
+      local = V3<R>{local.x + tm[0], local.y + tm[1], local.z + tm[2]};
+    }
+  }
+  if (lit) terminal = local;
+  return terminal;
 }
 
 // Move the wave's 32-bit counters into the per-lane 64-bit totals.
@@ -933,8 +1158,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVELS > 1 
   using R = double;
   (void)params_by_value;  // read through rparams()
   const RT_CONST RenderParams<R>& p = rparams<R>();
-  constexpr int kRow = 65;
-  __shared__ double sbuf[4][P * 3 * kRow];
+  constexpr int kRow = 66;  // 16-B aligned rows; row stride 4 banks apart: the 3P summing lanes' reads never conflict
+  __shared__ __attribute__((aligned(16))) double sbuf[4][P * 3 * kRow];
   const int lane = (int)__lane_id();
   const int wib = (int)(threadIdx.x >> 6);
   double* buf = sbuf[wib];
@@ -962,24 +1187,46 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVELS > 1 
       const int i = t % nobj, l = t / nobj - 1;
       const RT_CONST DevObject<R>& ob = cptr(p.objects)[i];
       if (l < 0) {
-        const V3<R> ro = xform<R>(ob.w2o, o, R(1));
+        const V3<R> ro = xform_xf<R, true>(ob.xf, ob.w2o, o);
         double* c = cache + kCacheCamO + 4 * i;
         c[0] = ro.x; c[1] = ro.y; c[2] = ro.z;
-        const V3<R> n = xform<R>(ob.o2w, V3<R>{R(0), R(1), R(0)}, R(0));  // geom.nim:367-368, renderer.nim:88
+        const V3<R> n = xform_xf<R, false>(ob.xf, ob.o2w, V3<R>{R(0), R(1), R(0)});  // geom.nim:367-368, renderer.nim:88
         double* cn = cache + kCachePlaneN + 4 * i;
         cn[0] = n.x; cn[1] = n.y; cn[2] = n.z;
       } else {
         const RT_CONST DevLight<R>& L = cptr(p.lights)[l];
         const V3<R> sd{R(L.v[0]) * R(-1), R(L.v[1]) * R(-1), R(L.v[2]) * R(-1)};  // shade: -lightDir
-        const V3<R> rd = xform<R>(ob.w2o, sd, R(0));
+        const V3<R> rd = xform_xf<R, false>(ob.xf, ob.w2o, sd);
         double* c = cache + kCacheLightD + 8 * (l * kCacheObj + i);
         c[0] = rd.x; c[1] = rd.y; c[2] = rd.z;
         c[4] = Prec<R>::rcp(rd.x); c[5] = Prec<R>::rcp(rd.y); c[6] = Prec<R>::rcp(rd.z);
       }
     }
     __syncthreads();
+    // the lean plane's per-light shading terms (shade_path's product, same
+    // operands: the cached normal, -lightDir, albedo / PI, color * intensity)
+    if (p.lean_plane >= 0 && (int)threadIdx.x < p.nlight) {
+      const int l = (int)threadIdx.x;
+      const RT_CONST DevObject<R>& ob = cptr(p.objects)[p.lean_plane];
+      const RT_CONST DevLight<R>& L = cptr(p.lights)[l];
+      const double* cn = cache + kCachePlaneN + 4 * p.lean_plane;
+      const V3<R> N{cn[0], cn[1], cn[2]};
+      const V3<R> ldir{L.v[0], L.v[1], L.v[2]};
+      const V3<R> sd{ldir.x * R(-1), ldir.y * R(-1), ldir.z * R(-1)};
+      const V3<R> I{L.ci[0], L.ci[1], L.ci[2]};
+      const R ndl = nmax(R(0), dot4(N, R(0), sd, R(0) * R(-1)));
+      double* tm = cache + kCacheLeanTerm + 4 * l;
+      tm[0] = ob.albp[0] * I.x * ndl;
+      tm[1] = ob.albp[1] * I.y * ndl;
+      tm[2] = ob.albp[2] * I.z * ndl;
+    }
+    __syncthreads();
   }
   const double* cch = use_cache ? cache : nullptr;
+  // a lean pixel: empty camera-ray list and every light's skip bit set
+  // (the reflective instantiation keeps the general path only: it runs at 2
+  // waves per SIMD on its register budget)
+  const unsigned lean_need = LEVELS == 1 && use_cache && p.lean_plane >= 0 ? ((1u << p.nlight) - 1u) << 24 : 0u;
 
   // pixel g of the launch: image (x, y), its output row, whether it renders
   auto pixel_of = [&](long long g, int& x, int& y, int& out_row) -> bool {
@@ -1003,25 +1250,56 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVELS > 1 
   };
 
   for (long long b = wave; b < nbatch; b += nwaves) {
-    R ax = R(0), ay = R(0), az = R(0);  // lane j < P: pixel j's sum
+    // the batch's pixels, pixel j in lane j < P (its image position, output
+    // row and record), read back by readlane: one pixel_of per pixel and
+    // batch instead of one per pixel and step
+    int bx = 0, by = 0, brow = 0;
+    unsigned binfo = kPixCount;
+    bool bok = false;
+    if (lane < P) {
+      bok = pixel_of(b * P + lane, bx, by, brow);
+      if (bok && p.pix_info) binfo = p.pix_info[by * p.width + bx];
+    }
+    const unsigned long long okm = ballot(bok);
+    // lane 3j + c < 3P: component c of pixel j's running sum (sample order)
+    R acc = R(0);
     for (int it = 0; it < iters; ++it) {
       const int s = it * 64 + lane;
       const bool sv = s < p.spp;
+      const int si = s % p.grid_m, sj = s / p.grid_m;
+      // castPrimaryRay's y term depends on the row and the sample only: the
+      // batch's pixels usually share a row, so it is formed once per row
+      int cy_row = -1;
+      R cy = R(0);
       for (int j = 0; j < P; ++j) {
-        int x, y, out_row;
-        if (!pixel_of(b * P + j, x, y, out_row)) continue;
+        if (!((okm >> j) & 1ull)) continue;
+        const int x = __builtin_amdgcn_readlane(bx, j), y = __builtin_amdgcn_readlane(by, j);
+        const unsigned pinfo = (unsigned)__builtin_amdgcn_readlane((int)binfo, j);
         const int pix = y * p.width + x;
-        const unsigned pinfo = p.pix_info ? p.pix_info[pix] : kPixCount;
         // grid() sampling.nim:5-18, p[j*m + i]; castPrimaryRay (renderer.nim:31-44)
-        const int si = s % p.grid_m, sj = s / p.grid_m;
         const R px = R(x) + (R(si) * p.sample_step + p.sample_off);
-        const R py = R(y) + (R(sj) * p.sample_step + p.sample_off);
+        if (y != cy_row) {
+          const R py = R(y) + (R(sj) * p.sample_step + p.sample_off);
+          cy = (R(1) - Prec<R>::div(R(2) * py, R(p.height))) * p.f;
+          cy_row = y;
+        }
         const R cx = (Prec<R>::div(R(2) * px * p.aspect, R(p.width)) - p.aspect) * p.f;
-        const R cy = (R(1) - Prec<R>::div(R(2) * py, R(p.height))) * p.f;
         const V3<R> dn = normalize_dir<R>(V3<R>{cx, cy, R(-1)});
         const V3<R> d = xform<R>(p.c2w, dn, R(0));
         ws.v[STAT_PRIMARY] += popc32(ballot(sv));
-        const V3<R> c = shade_path<R, false, true, LEVELS>(rparams<R>(), o, d, sv, ws, pinfo, pix, cch);
+        V3<R> c;
+        const bool lean_px = lean_need != 0u && (pinfo & (kPixCount | lean_need)) == lean_need;
+#if defined(RTMI_DIAG) && defined(RTMI_PX64_ONLY)
+        // diagnostic builds (tools/build_variant.sh): 1 = lean samples only,
+        // 2 = general samples only — a time split, wrong images on purpose
+        if (lean_px != (RTMI_PX64_ONLY == 1)) {
+          c = V3<R>{R(0), R(0), R(0)};
+        } else
+#endif
+        if (lean_px)
+          c = px64_lean_sample(rparams<R>(), o, d, sv, ws, cch);
+        else
+          c = shade_path<R, false, true, LEVELS>(rparams<R>(), o, d, sv, ws, pinfo, pix, cch);
         buf[(j * 3 + 0) * kRow + lane] = c.x;
         buf[(j * 3 + 1) * kRow + lane] = c.y;
         buf[(j * 3 + 2) * kRow + lane] = c.z;
@@ -1032,15 +1310,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVELS > 1 
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      if (lane < P) {
+      // calcPixel's sum (renderer.nim:149-159), each of the 3P chains in its
+      // own lane, in sample order; a full step reads its row two samples per
+      // 128-bit LDS read (rows of pixels skipped this batch are never used)
+      if (lane < 3 * P) {
+        const double* row = buf + lane * kRow;
         const int nv = min(64, p.spp - it * 64);
-        const double* rx = buf + (lane * 3 + 0) * kRow;
-        const double* ry = buf + (lane * 3 + 1) * kRow;
-        const double* rz = buf + (lane * 3 + 2) * kRow;
-        for (int k = 0; k < nv; ++k) {
-          ax = ax + rx[k];
-          ay = ay + ry[k];
-          az = az + rz[k];
+        if (nv == 64) {
+          const double2* r2 = (const double2*)row;
+#pragma unroll 8
+          for (int k = 0; k < 32; ++k) {
+            const double2 v = r2[k];
+            acc = acc + v.x;
+            acc = acc + v.y;
+          }
+        } else {
+          for (int k = 0; k < nv; ++k) acc = acc + row[k];
         }
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1052,21 +1337,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LEVELS > 1 
       if ((it & 15) == 15) flush_stats(ws, tot, lane);
     }
     flush_stats(ws, tot, lane);
-    if (lane < P) {
-      int x, y, out_row;
-      if (pixel_of(b * P + lane, x, y, out_row)) {
-        const float cr = (float)(ax * p.inv_len), cg = (float)(ay * p.inv_len), cb = (float)(az * p.inv_len);
-        if (p.mode == 0 && p.step > 1) {
-          const int xe = min(x + p.step, p.width), ye = min(y + p.step, p.height);
-          for (int yy = y; yy < ye; ++yy)
-            for (int xx = x; xx < xe; ++xx) {
-              float* q = p.fb + ((size_t)yy * p.width + xx) * 3;
-              q[0] = cr; q[1] = cg; q[2] = cb;
-            }
-        } else {
-          float* q = p.fb + ((size_t)out_row * p.width + x) * 3;
-          q[0] = cr; q[1] = cg; q[2] = cb;
-        }
+    // pixel j's three sums to lane j
+    const R ax = __shfl(acc, 3 * lane + 0), ay = __shfl(acc, 3 * lane + 1), az = __shfl(acc, 3 * lane + 2);
+    if (bok) {  // lanes j < P
+      const int x = bx, y = by, out_row = brow;
+      const float cr = (float)(ax * p.inv_len), cg = (float)(ay * p.inv_len), cb = (float)(az * p.inv_len);
+      if (p.mode == 0 && p.step > 1) {
+        const int xe = min(x + p.step, p.width), ye = min(y + p.step, p.height);
+        for (int yy = y; yy < ye; ++yy)
+          for (int xx = x; xx < xe; ++xx) {
+            float* q = p.fb + ((size_t)yy * p.width + xx) * 3;
+            q[0] = cr; q[1] = cg; q[2] = cb;
+          }
+      } else {
+        float* q = p.fb + ((size_t)out_row * p.width + x) * 3;
+        q[0] = cr; q[1] = cg; q[2] = cb;
       }
     }
   }

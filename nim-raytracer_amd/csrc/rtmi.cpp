@@ -229,6 +229,7 @@ struct rt_scene {
   int64_t last_batched = 0, last_fallback = -1;  // rt_scene_last_batch
   int32_t nobj = 0, nlight = 0, nmesh = 0;
   int32_t shadow_mesh = -1;  // the only mesh object, or -1 (FastParams.shadow_mesh)
+  int32_t lean64_plane = -1; // RenderParams.lean_plane of the scene (k_render_px64 lean samples)
   int32_t has_point_light = 0;
   unsigned f32_subset = 0;   // SUB_* feature bits of the scene (kernel specialisation)
   bool any_reflective = false;
@@ -270,6 +271,10 @@ struct rt_scene {
   // fixed direction (rt_common.h LTri, leaf order, ntri per light)
   DevBuf<LTri> lrec;
   DevBuf<LTri> grec;               // lrec in light-grid entry order (FastParams.grid_rec)
+  // the float64 shadow records in light-grid entry order (RenderParams.sh64),
+  // built by the first float64 call that searches the grids
+  DevBuf<ShTri64> sh64;
+  bool sh64_ready = false;
   int64_t lrec_ntri = 0;
   uint32_t lrec_mask = 0;          // the lights that have records
   DevBuf<int32_t> grid_off, grid_ent;
@@ -543,6 +548,9 @@ void fill_precision(const rt_scene_desc* d, const std::vector<std::vector<double
     o.prm[6] = (R)s.box_max[2];
     for (int k = 0; k < 3; ++k) o.albedo[k] = (R)s.albedo[k];
     o.albedo[3] = (R)s.reflection;
+    // albedo / PI in R, one correctly rounded IEEE division as the kernel's
+    // (and the oracle's, rt_oracle.c shade) per-sample quotient
+    for (int k = 0; k < 3; ++k) o.albp[k] = (R)s.albedo[k] / (R)3.14159265358979323846;
     o.type = s.type;
     o.mesh = s.type == RT_MESH ? s.mesh : 0;
     o.xf = classify_xf(s.world_to_object, s.object_to_world);
@@ -1048,6 +1056,15 @@ extern "C" int rt_scene_create(const rt_scene_desc* d, rt_scene** out_scene) {
         s->skip_planes.push_back(sp);
       }
       if (!s->skippable) s->skip_planes.clear();
+      // k_render_px64's lean samples: one mesh + one non-reflective plane,
+      // distant lights only (each with a skip bit)
+      s->lean64_plane = -1;
+      if (s->skippable && s->shadow_mesh >= 0 && d->num_objects == 2 && d->num_lights >= 1 && d->num_lights <= 8) {
+        const int pl = 1 - s->shadow_mesh;
+        bool ok = d->objects[pl].type == RT_PLANE && !(d->objects[pl].reflection > 0.0);
+        for (int li = 0; li < d->num_lights; ++li) ok = ok && d->lights[li].type != RT_POINT_LIGHT;
+        if (ok) s->lean64_plane = pl;
+      }
       // the occupancy prefix sums the per-call shadow skips read (rt_frame.h)
       std::vector<int32_t> sat;
       for (int li = 0; li < std::min(8, d->num_lights); ++li) {
@@ -1169,7 +1186,7 @@ extern "C" int rt_scene_get_info(const rt_scene* s, rt_scene_info* out) {
   // precisions, the light grids and bins, and the per-call buffer sets
   // (fr / fr2 are the bulk at 4K)
   std::lock_guard<std::mutex> lk(const_cast<rt_scene*>(s)->mu);
-  out->device_bytes = (int64_t)(s->f32.bytes() + s->f64.bytes() + s->nodes.bytes() + s->partials.bytes() +
+  out->device_bytes = (int64_t)(s->f32.bytes() + s->f64.bytes() + s->nodes.bytes() + s->partials.bytes() + s->sh64.bytes() +
                                 s->queue.bytes() + s->queue2.bytes() + s->f64_tables.bytes() +
                                 s->fb_scratch.bytes() + s->grids.bytes() + s->grid_off.bytes() +
                                 s->grid_ent.bytes() + s->obj_grids.bytes() + s->obj_grid_mask.bytes() +
@@ -1837,6 +1854,7 @@ void fill_params(rt_scene* s, const PrecisionData<R>& pd, const rt_options* o, c
   p.max_depth = o->max_ray_depth;
   p.flags = (int32_t)o->flags;
   p.shadow_mesh = s->shadow_mesh;
+  p.lean_plane = -1;
   p.seed = o->seed;
   p.sample_scratch = nullptr;
   p.max_iters = (int32_t)std::min<int64_t>(INT32_MAX, 2 * s->num_nodes + 16);
@@ -1965,11 +1983,25 @@ int launch(rt_scene* s, const rt_options* o, const Mapping& mp, float* d_out, hi
       if (lists) {
         p.pix_slots = s->fr.slots.p;
         p.slot_lg = s->fr.slot_lg;
+        p.lean_plane = s->lean64_plane;
       }
       if (binning && s->has_grids) {
         p.grids = s->grids.p;
         p.grid_off = s->grid_off.p;
         p.grid_ent = s->grid_ent.p;
+        if (!s->sh64_ready && s->shadow_mesh >= 0) {
+          if (int rc = s->sh64.alloc(s->grid_ent.n)) return rc;
+          for (int li = 0; li < s->nlight && li < (int)s->grid_host.size(); ++li) {
+            const LightGridHost& lg = s->grid_host[(size_t)li];
+            if (lg.g.gu <= 0 || lg.ent.empty()) continue;
+            const int e = rtmi_build_sh64(s->f64.objects.p, s->shadow_mesh, s->f64.lights.p, li,
+                                          s->grid_ent.p + lg.g.ent_base, (int)lg.ent.size(), s->f64.tris.p,
+                                          (int32_t)s->num_nodes, s->sh64.p + lg.g.ent_base, st);
+            if (e) return fail(RT_E_DEVICE, "shadow record build failed: %s", hipGetErrorString((hipError_t)e));
+          }
+          s->sh64_ready = true;
+        }
+        if (s->sh64_ready) p.sh64 = s->sh64.p;
       }
       p.tri_rec0 = (int32_t)s->num_nodes;
       const long long nbatch = ((long long)mp.nrows * mp.ncols + rtmi_px64_batch() - 1) / rtmi_px64_batch();
@@ -2197,8 +2229,10 @@ int read_stats(rt_scene* s, hipStream_t st, rt_stats* out) {
   // counts it, which is checked here.
   const unsigned long long rays = h[STAT_PRIMARY] + h[STAT_SHADOW] + h[STAT_REFL];
   const unsigned long long tests = (unsigned long long)s->nobj * rays;
+#if !(defined(RTMI_DIAG) && defined(RTMI_PX64_ONLY))  // that diagnostic skips samples on purpose
   if (h[STAT_TESTS] != 0 && h[STAT_TESTS] != tests)
     return fail(RT_E_DEVICE, "inconsistent intersection-test count (%llu vs %llu)", h[STAT_TESTS], tests);
+#endif
   out->num_intersection_tests = tests;
   out->num_intersection_hits = h[STAT_HITS];
   out->num_shadow_rays = h[STAT_SHADOW];

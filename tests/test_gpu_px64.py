@@ -41,6 +41,7 @@ def _dev(ds, opts, y0=0, y1=None, step=1, maxStep=1):
 CASES = [
     ("mesh-bunny", 48, 32, 8),
     ("mesh-bunny", 40, 24, 9),
+    ("mesh-teapot", 40, 28, 8),  # the reference's live scene (mesh-bunny.nim loads teapot.obj)
     ("mesh-mix", 40, 28, 8),
     ("two-meshes", 36, 24, 8),
     ("spheres-reflection", 40, 30, 8),

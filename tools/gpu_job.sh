@@ -8,7 +8,8 @@
 #   tests            pytest -m gpu over $TESTS (default: tests)
 #   bench:CFG[:fp64] one bench.py line (--config CFG, $BENCH_ARGS) -> bench_<cfg>[_fp64].json
 #   prof:CFG[:fp64]  rocprofv3 --kernel-trace --stats of that bench command ($PROF_ARGS) -> prof_<cfg>/
-#   pmc:CFG[:fp64]   three PMC passes (FETCH_SIZE / WRITE_SIZE / SQ issue counters),
+#   pmc:CFG[:fp64|:bvh] three PMC passes (FETCH_SIZE / WRITE_SIZE / SQ issue counters;
+#                    fp64 adds a fourth: the F64 op counts; bvh = --flags 8, RT_FLAG_NO_BINNING),
 #                    one counter group per run -> pmc_<cfg>[_fp64]/ (summarise on the CPU:
 #                    python tools/pmc_summary.py gpurun_out/$OUT/pmc_<cfg> <workload key>)
 #   ab               interleaved A/B of bench.py over library builds: for $AB_REPS reps,
@@ -29,6 +30,7 @@ for st in ${STAGES:-tests}; do
   c=$(echo "${cfg:-C3}" | tr A-Z a-z)
   pa=""; sfx=""
   [ "$prec" = fp64 ] && { pa="--precision fp64"; sfx=_fp64; }
+  [ "$prec" = bvh ] && { pa="--flags 8"; sfx=_bvh; }   # RT_FLAG_NO_BINNING: the BVH path for every ray
   T=$(lim $c)
   case $kind in
     tests)
@@ -46,12 +48,18 @@ for st in ${STAGES:-tests}; do
     pmc)
       P=$O/pmc_$c$sfx
       mkdir -p $P
-      S="--config ${cfg:-C3} $pa --steps 2 --warmup 0 --no-cpu"
+      S="--config ${cfg:-C3} $pa --steps 2 --warmup 0 --no-cpu --no-extra"
       timeout -s KILL $T rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$K" -d $P/fetch -o p -f csv -- python3 bench.py $S > /dev/null 2> $P/fetch.err \
         && timeout -s KILL $T rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$K" -d $P/write -o p -f csv -- python3 bench.py $S > /dev/null 2> $P/write.err \
         && timeout -s KILL $T rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
              --kernel-include-regex "$K" -d $P/sq -o p -f csv -- python3 bench.py $S > /dev/null 2> $P/sq.err \
         || { echo "pmc $c$sfx failed"; tail -5 $P/*.err; exit 1; }
+      # float64: the F64 op mix (an F64 VALU instruction issues over 4 cycles, not 2)
+      if [ "$prec" = fp64 ]; then
+        timeout -s KILL $T rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU_INT64 \
+             --kernel-include-regex "$K" -d $P/f64 -o p -f csv -- python3 bench.py $S > /dev/null 2> $P/f64.err \
+          || { echo "pmc $c$sfx f64 failed"; tail -5 $P/f64.err; exit 1; }
+      fi
       echo "pmc $c$sfx done" ;;
     ab)
       for i in $(seq ${AB_REPS:-2}); do
