@@ -315,7 +315,10 @@ def main():
 
     def finish_frame():
         # complete the previous frame: its gather, then (rank 0) the
-        # un-interleave into the frame buffer, in stream order
+        # un-interleave into the frame buffer, in stream order (a side stream
+        # for the un-interleave measured slower — it shares the 4 hardware
+        # queues with the build and RCCL streams — and so did the stream-value
+        # hand-off instead of events: DESIGN.md (e), round 6)
         if pending[0] is not None:
             pending[0].wait()
             pending[0] = None
