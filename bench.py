@@ -57,7 +57,8 @@ BAND_H = 4             # rows per band (round-robin over ranks)
 
 def _scene(name):
     from rtmi import scenes
-    return {"bunny": scenes.mesh_bunny, "boxes2": scenes.boxes2, "torus": scenes.torus_scene}[name]()
+    return {"bunny": scenes.mesh_bunny, "boxes2": scenes.boxes2, "torus": scenes.torus_scene,
+            "mix": scenes.mesh_mix}[name]()
 
 
 # BASELINE.json configs on one GPU (C4/C5 are quoted on 8 GPUs; at N=1 this is
@@ -67,6 +68,11 @@ CONFIGS = {
     "C3": ("bunny", 1920, 1080, 16, "C3: bunny.geom baked x30 + ground plane, mesh-bunny.nim lights/camera"),
     "C4": ("bunny", 3840, 2160, 32, "C4: bunny.geom baked x30 + ground plane, mesh-bunny.nim lights/camera"),
     "C5": ("torus", 3840, 2160, 64, "C5: 1,000,000-triangle procedural torus + ground, mesh-bunny.nim lights/camera"),
+    # not a BASELINE config: a scene outside the list envelope (a reflective
+    # mesh, a point light, analytic objects around it), so every ray of it
+    # takes the wave-coherent BVH traversal (k_render_fast) — that path's line
+    "BVHMIX": ("mix", 1920, 1080, 8, "mesh-mix: reflective mesh between spheres/boxes, point + distant light "
+                                     "(the BVH path: k_render_fast)"),
 }
 
 
@@ -514,7 +520,8 @@ def main():
             "dtype": "f64" if fp64 else "f32",
             "data": {"bunny": "synthetic rays over the reference's bunny.geom fixture (69,451 triangles)",
                      "boxes2": "synthetic rays over the reference's boxes2.nim scene",
-                     "torus": "synthetic rays over a deterministic procedural 1M-triangle torus"}[scene_name],
+                     "torus": "synthetic rays over a deterministic procedural 1M-triangle torus",
+                     "mix": "synthetic rays over a test scene of this build (mesh-mix)"}[scene_name],
             "config": {
                 "workload": (f"{desc}, {W}x{H}, akGrid {m}x{m} = {m * m} spp, "
                              + ("fp64 parity mode (k_render_px64: the reference's arithmetic, bit-exact "

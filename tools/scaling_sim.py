@@ -36,6 +36,7 @@ from rtmi.renderer import DeviceScene, unshard_bands_device  # noqa: E402
 
 CFG = os.environ.get("CONFIG", "C3")
 name, W, H, M, _desc = CONFIGS[CFG]
+M = int(os.environ.get("GRID", M))  # akGrid m override (spp = m*m): item-length experiments
 REPS = int(os.environ.get("REPS", "5"))
 LINK_GBS = float(os.environ.get("LINK_GBS", "50"))
 ds = DeviceScene(_scene(name))
