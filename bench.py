@@ -224,6 +224,8 @@ def sub_measure(ds, opts, fb, stream, steps, warmup, key):
         c = pmc["counters_mean_per_dispatch"]
         sec = render_ms * 1e-3
         roof = issue_roofline(c, sec)
+        if key.endswith("_fp64"):
+            add_net_of_spills(roof, "k_render_px64ILi4ELi1E")
         if "hbm_bytes_per_launch" in pmc:
             roof["traffic"] = int(pmc["hbm_bytes_per_launch"])
             roof["hbm_gbs"] = round(pmc["hbm_bytes_per_launch"] / sec / 1e9, 1)
@@ -233,6 +235,39 @@ def sub_measure(ds, opts, fb, stream, steps, warmup, key):
     else:
         out["roofline"] = {"pmc": f"no PMC summary [{key}] for these native sources"}
     return out
+
+
+def load_spill_share(kernel_pat):
+    """profiles/spill_share.json (tools/spill_share.py) for these sources:
+    the estimated share of a kernel's VALU instructions that are SGPR-spill
+    lane moves, or None."""
+    from rtmi._lib import kernel_source_hash
+    try:
+        with open(os.path.join(REPO, "profiles", "spill_share.json")) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None
+    if d.get("source_hash") != kernel_source_hash():
+        return None
+    return d.get("kernels", {}).get(kernel_pat)
+
+
+def add_net_of_spills(roof, kernel_pat):
+    """frac net of the kernel's SGPR-spill VALU: the static
+    share and the loop-depth-weighted estimate (4 trips per loop level, an
+    upper bound for the hot loops' trip counts)."""
+    sp = load_spill_share(kernel_pat)
+    if sp is None or roof.get("frac") is None:
+        return
+    w = sp["weighted_share_4_per_level"]
+    roof["spill_valu_share_static"] = sp["static_share"]
+    roof["spill_valu_share_est"] = w
+    roof["frac_net_of_spills_est"] = round(roof["frac"] * (1.0 - w), 4)
+    if "frac_f64_weighted" in roof:
+        roof["frac_f64_weighted_net_of_spills_est"] = round(roof["frac_f64_weighted"] * (1.0 - w), 4)
+    roof["spill_note"] = ("v_writelane/v_readlane (SGPR spills) share of the kernel's VALU: static count, and weighted "
+                          "by 4 trips per loop level from the gfx950 assembly's loop depths (tools/spill_share.py, "
+                          "profiles/spill_share.json)")
 
 
 def load_pmc(workload_key):
@@ -477,6 +512,10 @@ def main():
         c = pmc["counters_mean_per_dispatch"]
         sec = render_ms * 1e-3
         roof.update(issue_roofline(c, sec))
+        if kinds == 15 and not fp64:
+            add_net_of_spills(roof, "k_render_mix1ILi2ELi4E")
+        elif fp64:
+            add_net_of_spills(roof, "k_render_px64ILi4ELi1E")
         if "hbm_bytes_per_launch" in pmc:
             roof["traffic"] = int(pmc["hbm_bytes_per_launch"])
             roof["hbm_gbs"] = round(pmc["hbm_bytes_per_launch"] / sec / 1e9, 1)
