@@ -396,70 +396,10 @@ __device__ __forceinline__ void traverse(const RT_CONST RenderParams<R>& p, int 
 // proof, tests/test_bins_cpu.py), so it equals geom.nim:339-358's loop over
 // all faces. early: the shadow early exit (a lane retires on a found hit at
 // t <= stop, as in leaf()).
-// A TriF64 record's fields read from an LDS slice (list_tris' staging).
-struct TriView {
-  const double* v0;
-  const double* e1;
-  const double* e2;
-};
-
-#ifndef RTMI_PX64_STAGE_CAM
-#define RTMI_PX64_STAGE_CAM 0  // measured slower: 20 VGPR spills at 3 waves (r6g)
-#endif
 template <class R>
 __device__ __forceinline__ void list_tris(const RT_CONST RenderParams<R>& p, const int32_t* ent, int n, V3<R> o, V3<R> d,
                                           bool act, bool early, R stop, R& tbest, int& best_id) {
   using Tri = typename TriOf<R>::type;
-  if constexpr (Prec<R>::exact && RTMI_PX64_STAGE_CAM) {
-    // LDS staging of the float64 records (80 B = 10 doubles): the list's
-    // entries are loaded 64 at a time into a VGPR, four records = 40 doubles
-    // are one vector load into the wave's LDS slice, read back as broadcasts,
-    // and the next four load while these are tested
-    __shared__ double stage_t[4][2][64];
-    const int lane = (int)__lane_id();
-    double* slice = &stage_t[(threadIdx.x >> 6) & 3][0][0];
-    const double* recs = (const double*)p.tris;
-    const int rec0 = p.tri_rec0;
-    const int ngroups = (n + 3) >> 2;
-    const int jl = lane / 10, fl = lane - 10 * jl;  // this lane's record of a group and its double
-    int entv = lane < n ? ent[lane] : 0;
-    int chunk = 0;
-    auto fetch = [&](int g) -> double {
-      const int k = 4 * g + jl;
-      if ((4 * g) >> 6 != chunk) {  // the next 64 entries (lists past 64 faces)
-        chunk = (4 * g) >> 6;
-        entv = 64 * chunk + lane < n ? ent[64 * chunk + lane] : 0;
-      }
-      const int off = __shfl(entv, k & 63);
-      return lane < 40 && k < n ? recs[(size_t)((off >> 6) - rec0) * 10 + fl] : 0.0;
-    };
-    double pre = fetch(0);
-    for (int g = 0; g < ngroups; ++g) {
-      double* buf = slice + (g & 1) * 64;
-      buf[lane] = pre;
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      if (g + 1 < ngroups) pre = fetch(g + 1);
-      const int jn = min(4, n - 4 * g);
-      for (int j = 0; j < jn; ++j) {
-        const double* f = buf + 10 * j;  // TriF64: v0, e1, e2, id
-        const TriView tv{f, f + 3, f + 6};
-        const R t = tri_ref<R>(tv, o, d);
-        const int id = ((const int32_t*)(f + 9))[0];
-        const bool acc = act && t >= R(0) && (t < tbest || (t == tbest && id < best_id));
-        if (acc) {
-          tbest = t;
-          best_id = id;
-        }
-        if (early && j == 3) {
-          act = act && !(best_id >= 0 && tbest <= stop);
-          if (ballot(act) == 0ull) return;
-        }
-      }
-    }
-    return;
-  }
   for (int k = 0; k < n; ++k) {
     const int off = cptr(ent)[k];
     const RT_CONST Tri& tri = cptr(p.tris)[(off >> 6) - p.tri_rec0];
