@@ -121,9 +121,13 @@ constexpr int kBigFace = RTMI_BIG_FACE, kHugeCap = 4096;
 // Per-pixel list slots: at least 2^kSlotLg record offsets per pixel (the
 // host gives small images more, up to 256: rtmi.cpp slot_lg_for). C3 at 1080p
 // lists at most 28 faces per pixel, p99 11; the 1M-face torus at 4K 99, p999
-// 34 — its 1,490 pixels past 32 take the BVH.
+// 34. Round 6: 64 at least (was 32: 4K frames got 32, 2.1 GB per buffer set
+// now): the torus pixels past 32 took the BVH for their camera rays, and
+// with them a rank of 8 ran at 80 % of its share of the whole frame; with 64
+// the ranks' mean is 10.1 ms against 11.3 and the whole frame 72.1 → 71.7 ms
+// (`RTMI_SLOT_LG` A/B, profiles/r6/ab_slots/). 1080p keeps its 64.
 #ifndef RTMI_SLOT_LG
-#define RTMI_SLOT_LG 5
+#define RTMI_SLOT_LG 6
 #endif
 constexpr int kSlotLg = RTMI_SLOT_LG;
 
