@@ -7,7 +7,7 @@ import hashlib
 import os
 import sys
 
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "nim-raytracer_amd"))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "..", "nim-raytracer_amd"))
 import torch  # noqa: E402
 
 from rtmi import Antialias, Options, Precision, akGrid, scenes  # noqa: E402

@@ -64,17 +64,20 @@ for band_h in [int(b) for b in os.environ.get("BANDS", "4").split(",")]:
     for world in [int(w) for w in os.environ.get("WORLDS", "1,2,4,8").split(",")]:
         rows = band_rows(H, band_h, world)
         buf = torch.zeros(rows * W * 3, dtype=torch.float32, device="cuda")
-        per, b2b = [], []
-        for rank in range(world):
+        order = list(range(world))
+        if os.environ.get("RANK_ORDER") == "reverse":  # measurement-order check
+            order.reverse()
+        per, b2b = [0.0] * world, [0.0] * world
+        for rank in order:
             ts = []
             for _ in range(2):  # warm: the first launch of a mapping measures its launch order
                 ds.render_bands_device(opts, buf, band_h, rank, world, stream=stream, stats=False)
             for _ in range(REPS):
                 ts.append(timed(lambda: ds.render_bands_device(opts, buf, band_h, rank, world, stream=stream,
                                                                stats=False), 1))
-            per.append(sorted(ts)[len(ts) // 2])
-            b2b.append(timed(lambda: ds.render_bands_device(opts, buf, band_h, rank, world, stream=stream,
-                                                            stats=False), REPS))
+            per[rank] = sorted(ts)[len(ts) // 2]
+            b2b[rank] = timed(lambda: ds.render_bands_device(opts, buf, band_h, rank, world, stream=stream,
+                                                             stats=False), REPS)
             if rank == 0:
                 res[f"world{world}_split"] = list(ds.last_split())
         gathered = torch.zeros(world * rows * W * 3, dtype=torch.float32, device="cuda")
