@@ -107,6 +107,19 @@ class DeviceScene:
                                            int(world), _stream(stream), C.byref(st) if stats else None))
         return Stats.from_c(st) if stats else None
 
+    def last_pipelined(self):
+        """Whether the last render call was pipelined (its build on the
+        scene's build stream, its own buffer set: rtmi.cpp rt_scene::pipe) —
+        such calls on two alternating streams may render at once."""
+        f = lib().rtmi_test_last_pipelined
+        f.restype = C.c_int
+        f.argtypes = [C.c_void_p, C.POINTER(C.c_int32)]
+        s = C.c_int32()
+        r = f(self.h, C.byref(s))
+        if r < 0:
+            raise RuntimeError("rtmi_test_last_pipelined failed")
+        return bool(r)
+
     def last_split(self):
         """(lean, general) pixel groups of the last render call (two-class launches)."""
         a, b = C.c_int64(), C.c_int64()

@@ -129,3 +129,36 @@ def test_camera_change_between_pipelined_calls(gpu):
     assert not torch.equal(want[0], want[1])
     for g, w in zip(got, want):
         assert torch.equal(g, w)
+
+
+@pytest.mark.parametrize("world", [4, 8])
+def test_overlapping_calls_on_two_streams(gpu, world):
+    """Pipelined calls alternating between two streams A and B with no host
+    sync: the library orders each call after the scene's previous one
+    (render_device waits on `done` across streams), so every buffer equals
+    the serial render and the Stats the last call left equal its serial
+    Stats. (Letting call k + 1 render into call k's tail this way was
+    measured and rejected: DESIGN.md (e), round 6.)"""
+    import torch
+    from rtmi import abi
+    ref_ds = _scene("0")
+    ds = _scene("1")
+    rows = band_rows(H, 4, world)
+    refs, ref_st = [], []
+    for r in range(world):
+        b = torch.full((rows * W * 3,), -7.0, dtype=torch.float32, device="cuda")
+        ref_st.append(ref_ds.render_bands_device(_opts(), b, 4, r, world))
+        refs.append(b)
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    outs = [torch.full((rows * W * 3,), -7.0, dtype=torch.float32, device="cuda") for _ in range(3 * world)]
+    torch.cuda.synchronize()
+    for k in range(3 * world):
+        ds.render_bands_device(_opts(), outs[k], 4, k % world, world, stream=streams[k % 2], stats=False)
+        assert _pipelined(ds)[0], k
+    # the last call's Stats (kept: no RT_FLAG_NO_STATS), read without a sync
+    st = abi.rt_stats()
+    assert lib().rt_scene_last_stats(ds.h, C.byref(st)) == 0
+    assert Stats.from_c(st) == ref_st[(3 * world - 1) % world]
+    torch.cuda.synchronize()
+    for k in range(3 * world):
+        assert torch.equal(outs[k], refs[k % world]), (k, float((outs[k] - refs[k % world]).abs().max()))

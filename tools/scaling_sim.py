@@ -55,29 +55,56 @@ def timed(fn, reps):
     return a.elapsed_time(b) / reps
 
 
+# RSTREAMS=2 (A/B): a rank's pipelined back-to-back calls alternate two
+# streams and two band buffers (measured with a library build that let call
+# k+1 render into call k's tail: slower); 1: one
+# stream, the projection's measurement
+RSTREAMS = int(os.environ.get("RSTREAMS", "1"))
+stream2 = torch.cuda.Stream()
+
+
+def timed_two(fn, reps):
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record(stream)
+    stream2.wait_stream(stream)
+    for k in range(reps):
+        fn(k, stream if k % 2 == 0 else stream2)
+    stream.wait_stream(stream2)
+    b.record(stream)
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / reps
+
+
 fb = torch.zeros(W * H * 3, dtype=torch.float32, device="cuda")
 for band_h in [int(b) for b in os.environ.get("BANDS", "4").split(",")]:
-    res = {"config": CFG, "width": W, "height": H, "spp": M * M, "band_h": band_h, "reps": REPS,
+    res = {"config": CFG, "width": W, "height": H, "spp": M * M, "band_h": band_h, "reps": REPS, "rstreams": RSTREAMS,
            "link_gbs_model": LINK_GBS}
     ds.render_device(opts, fb, stream=stream, stats=False)
     res["whole_frame_b2b_ms"] = round(timed(lambda: ds.render_device(opts, fb, stream=stream, stats=False), REPS), 4)
     for world in [int(w) for w in os.environ.get("WORLDS", "1,2,4,8").split(",")]:
         rows = band_rows(H, band_h, world)
         buf = torch.zeros(rows * W * 3, dtype=torch.float32, device="cuda")
+        bufs2 = [buf, torch.zeros_like(buf)]
         order = list(range(world))
         if os.environ.get("RANK_ORDER") == "reverse":  # measurement-order check
             order.reverse()
         per, b2b = [0.0] * world, [0.0] * world
         for rank in order:
             ts = []
-            for _ in range(2):  # warm: the first launch of a mapping measures its launch order
-                ds.render_bands_device(opts, buf, band_h, rank, world, stream=stream, stats=False)
+            for k in range(2):  # warm: the first launch of a mapping measures its launch order
+                ds.render_bands_device(opts, buf, band_h, rank, world, stream=stream2 if RSTREAMS == 2 and k else stream,
+                                       stats=False)
+            torch.cuda.synchronize()
             for _ in range(REPS):
                 ts.append(timed(lambda: ds.render_bands_device(opts, buf, band_h, rank, world, stream=stream,
                                                                stats=False), 1))
             per[rank] = sorted(ts)[len(ts) // 2]
-            b2b[rank] = timed(lambda: ds.render_bands_device(opts, buf, band_h, rank, world, stream=stream,
-                                                             stats=False), REPS)
+            if RSTREAMS == 2 and ds.last_pipelined():
+                b2b[rank] = timed_two(lambda k, st: ds.render_bands_device(opts, bufs2[k % 2], band_h, rank, world,
+                                                                           stream=st, stats=False), REPS)
+            else:
+                b2b[rank] = timed(lambda: ds.render_bands_device(opts, buf, band_h, rank, world, stream=stream,
+                                                                 stats=False), REPS)
             if rank == 0:
                 res[f"world{world}_split"] = list(ds.last_split())
         gathered = torch.zeros(world * rows * W * 3, dtype=torch.float32, device="cuda")
