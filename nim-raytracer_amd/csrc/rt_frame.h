@@ -119,13 +119,14 @@ enum : int32_t { FC_RESERVED = 0, FC_HEAVY = 1, FC_LEAN = 2, FC_HUGE0 = 3, FC_HU
 constexpr int kBigFace = RTMI_BIG_FACE, kHugeCap = 4096;
 
 // Per-pixel list slots: at least 2^kSlotLg record offsets per pixel (the
-// host gives small images more, up to 256: rtmi.cpp slot_lg_for). C3 at 1080p
-// lists at most 28 faces per pixel, p99 11; the 1M-face torus at 4K 99, p999
-// 34. Round 6: 64 at least (was 32: 4K frames got 32, 2.1 GB per buffer set
-// now): the torus pixels past 32 took the BVH for their camera rays, and
-// with them a rank of 8 ran at 80 % of its share of the whole frame; with 64
-// the ranks' mean is 10.1 ms against 11.3 and the whole frame 72.1 → 71.7 ms
-// (`RTMI_SLOT_LG` A/B, profiles/r6/ab_slots/). 1080p keeps its 64.
+// host gives small images more, up to 256, and 4K frames 128: rtmi.cpp
+// slot_lg_for). C3 at 1080p lists at most 28 faces per pixel, p99 11; the
+// 1M-face torus at 4K 99, p999 34. Round 6: 64 at least (was 32): the torus
+// pixels past 32 took the BVH for their camera rays, and with them a rank of
+// 8 ran at 80 % of its share of the whole frame; with 64 the ranks' mean is
+// 10.1 ms against 11.3 and the whole frame 72.1 → 71.7 ms (`RTMI_SLOT_LG`
+// A/B, profiles/r6/ab_slots/); with 128 at 4K no torus pixel is left to the
+// BVH and every rank of 8 runs 9.6 ms (profiles/r6/ab_slots/lg7_*).
 #ifndef RTMI_SLOT_LG
 #define RTMI_SLOT_LG 6
 #endif

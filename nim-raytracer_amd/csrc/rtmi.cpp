@@ -148,6 +148,12 @@ inline int slot_lg_for(int w, int h) {
   const unsigned long long npx = (unsigned long long)w * (unsigned long long)h;
   int lg = rtmi::kSlotLg;
   while (lg < 8 && (npx << (lg + 1)) <= (1ull << 27)) ++lg;
+  // 4K and up: 128 (4.2 GB per buffer set at 4K). The 1M-face torus (C5)
+  // lists up to 99 faces per pixel at 4K; with 64 slots its 64 fullest
+  // pixels took the one-sample BVH loop at ~100x a mean pixel's cost, up
+  // to ~12 ms of one wave — longer than a rank's whole call at N = 8, so
+  // the 3 ranks holding the dearest of them ran 10-20 % long (rt_frame.h)
+  if (npx >= (1ull << 22)) lg = std::max(lg, 7);
   return lg;
 }
 
@@ -1464,10 +1470,10 @@ int frame_buffers(rt_scene* s, int w, int h, hipStream_t st) {
   // at 1080p, past 32 for 7 % of its pixels at 320x180); a pixel past its
   // slots takes the BVH (exact, slower)
   int lg = f.want_lg >= 0 ? f.want_lg : slot_lg_for(w, h);
-  // slot indices are 32-bit (pixel << lg in the kernels): a requested lg
-  // (test hook / diagnostic) is clamped to keep the block below 2^31 entries
-  // and 2 GiB
-  while (lg > 0 && (((unsigned long long)w * (unsigned long long)h) << lg) + kBinPad >= (1ull << 29)) --lg;
+  // slot indices are 32-bit (pixel << lg + slot, int in the kernels): a
+  // requested lg (test hook / diagnostic) is clamped to keep the block below
+  // 2^31 entries
+  while (lg > 0 && (((unsigned long long)w * (unsigned long long)h) << lg) + kBinPad >= (1ull << 31)) --lg;
   if (f.w == w && f.h == h && (!lists || f.slot_lg == lg)) return RT_OK;
   // an earlier call may still read the old buffers: `st` (the build stream)
   // waits on the last call that used this set (its render kernels, and the

@@ -221,6 +221,32 @@ def test_list_past_its_slots_takes_the_bvh(gpu, lg):
     assert ds.render_device(opts, again) == sref and torch.equal(again, ref)
 
 
+def test_4k_frames_get_128_slots(gpu):
+    """4K frames get 128 list slots per pixel (rtmi.cpp slot_lg_for; 1080p
+    keeps 64): the C5 torus's fullest pixels (up to 99 camera-ray faces at
+    4K, around row 1184) then stay in the batched kernel instead of taking the
+    one-sample BVH loop at ~100x a pixel's cost, and the rows render the same
+    frame and Stats as with 64 slots, where they overflow."""
+    import torch
+    ds = DeviceScene(scenes.torus_scene())
+    opts = Options(width=3840, height=2160, antialias=Antialias(akGrid, 8), bias=BIAS)
+    y0, y1 = 1176, 1192
+    out = torch.zeros(3840 * 2160 * 3, dtype=torch.float32, device="cuda")
+    st = ds.render_device(opts, out, y0=y0, y1=y1)
+    assert _slot_lg(ds) == 7
+    assert ds.last_batch()[1] == 0
+    _slot_lg(ds, 6)
+    ref = torch.zeros_like(out)
+    assert ds.render_device(opts, ref, y0=y0, y1=y1) == st
+    assert ds.last_batch()[1] > 0  # at 64 slots some of these pixels overflow
+    assert torch.equal(out, ref)
+    small = DeviceScene(scenes.mesh_bunny())
+    o2 = Options(width=1920, height=1080, antialias=Antialias(akGrid, 16), bias=BIAS)
+    fb = torch.zeros(1920 * 1080 * 3, dtype=torch.float32, device="cuda")
+    small.render_device(o2, fb, y0=500, y1=508)
+    assert _slot_lg(small) == 6
+
+
 def test_last_split_describes_the_last_call(gpu):
     """fp32 two-class call, then an fp64 call: last_split / last_batch report
     the fp64 call (no lean pixels), not the earlier device counts."""
