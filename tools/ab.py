@@ -42,6 +42,11 @@ def variants():
         v[nm.replace("-", "_") + "_64"] = (scenes.SCENES[nm](), Options(width=1920, height=1080,
                                                                          antialias=Antialias(akGrid, 8), bias=1e-4,
                                                                          maxRayDepth=5, precision=Precision.fp32))
+    # the other analytic scenes (feature subsets of their own), 1080p 64 spp
+    for nm in ("spheres-warm", "spheres-reflection", "spheres-pointlight1", "boxtest"):
+        v[nm.replace("-", "_") + "_64"] = (scenes.SCENES[nm](), Options(width=1920, height=1080,
+                                                                         antialias=Antialias(akGrid, 8), bias=1e-4,
+                                                                         maxRayDepth=5, precision=Precision.fp32))
     # C5 (only when asked for: 72 ms a frame)
     v["c5_full"] = (scenes.torus_scene(), Options(width=3840, height=2160, antialias=Antialias(akGrid, 64), bias=1e-4,
                                                   precision=Precision.fp32))
