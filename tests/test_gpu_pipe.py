@@ -132,7 +132,7 @@ def test_camera_change_between_pipelined_calls(gpu):
 
 
 @pytest.mark.parametrize("world", [4, 8])
-def test_overlapping_calls_on_two_streams(gpu, world):
+def test_pipelined_calls_on_two_streams(gpu, world):
     """Pipelined calls alternating between two streams A and B with no host
     sync: the library orders each call after the scene's previous one
     (render_device waits on `done` across streams), so every buffer equals
