@@ -15,7 +15,9 @@ frame k+1 renders) and so only shows when it takes longer than a render:
 LINK_GBS, default 50 GB/s per link and direction — a conservative figure
 for MI355X's ~153 GB/s links). The projection:
     step_N = b2b_max_N + unshard_N + max(0, gather_N - b2b_max_N)
-and `projected_speedup_N` = step_1 / step_N, step_1 = the faster of the
+and `projected_speedup_N` = step_1 / step_N (`projected_speedup_loop_N`: with
+rank 0's measured loop — band call + un-interleave back to back — in place of
+adding the un-interleave to the slowest rank), step_1 = the faster of the
 whole-frame call and the one-rank band call, both back to back (the
 one-GPU bench line runs the whole frame).
 Prints one JSON line per band height.
@@ -113,6 +115,18 @@ for band_h in [int(b) for b in os.environ.get("BANDS", "4").split(",")]:
         gather = recv_bytes / (max(1, world - 1) * LINK_GBS * 1e9) * 1e3 if world > 1 else 0.0
         b2b_max = max(b2b)
         step = b2b_max + (unshard if world > 1 else 0.0) + max(0.0, gather - b2b_max)
+        if world > 1:
+            # rank 0's own loop as bench.py runs it: its band call, then the
+            # un-interleave of the previous frame on the same stream (which
+            # can fill the gap while the next call's build finishes), back to
+            # back; the RCCL gather's own kernels on rank 0 are not modelled
+            def rank0_step():
+                ds.render_bands_device(opts, buf, band_h, 0, world, stream=stream, stats=False)
+                unshard_bands_device(gathered, fb, W, H, band_h, world, stream=stream)
+            r0 = timed(rank0_step, REPS)
+            step_loop = max([r0] + b2b[1:]) + max(0.0, gather - b2b_max)
+            res[f"world{world}_rank0_loop_ms"] = round(r0, 4)
+            res[f"world{world}_step_loop_ms"] = round(step_loop, 4)
         res[f"world{world}_ranks_ms"] = [round(x, 4) for x in per]
         res[f"world{world}_ranks_b2b_ms"] = [round(x, 4) for x in b2b]
         res[f"world{world}_max_ms"] = round(max(per), 4)
@@ -126,6 +140,8 @@ for band_h in [int(b) for b in os.environ.get("BANDS", "4").split(",")]:
     for w in (2, 4, 8):
         if f"world{w}_step_ms" in res:
             res[f"projected_speedup_{w}"] = round(step1 / res[f"world{w}_step_ms"], 2)
+        if f"world{w}_step_loop_ms" in res:
+            res[f"projected_speedup_loop_{w}"] = round(step1 / res[f"world{w}_step_loop_ms"], 2)
     if "world8_max_ms" in res and "world1_max_ms" in res:
         res["render_speedup_8"] = round(res["world1_max_ms"] / res["world8_max_ms"], 2)
         res["b2b_speedup_8"] = round(res["world1_b2b_max_ms"] / res["world8_b2b_max_ms"], 2)
